@@ -1,0 +1,187 @@
+"""Benchmark: batched programmable bootstrap (PBS) throughput on MI355X.
+
+Workload = BASELINE.json metric config: N=1024, k=1, n=630, l=3, logB=7 (configs[1]'s
+parameters) at batch 4096 per GPU.  A step = one batched PBS (one kernel launch) over the
+rank's 4096 resident LWE ciphertexts.  Multi-GPU = weak scaling: every rank bootstraps its
+own 4096-ciphertext shard; the device-format bootstrapping key is produced once on rank 0
+and broadcast over RCCL (xGMI); there is no collective in the data path.
+
+Usage: python bench.py [--gpus N --steps K --warmup W]
+       (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+METRIC = "PBS/sec (whole node) at N=1024 batch=4096; achieved HBM GB/s"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=4096, help="PBS per GPU per step")
+    ap.add_argument("--cpu-sample", type=int, default=96, help="PBS in the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", type=int, default=8, help="rows checked bit-exactly against the oracle (rank 0)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from concrete_amd import backend as B
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    p = B.CFG2
+    width = 3
+    # ---- keys: deterministic synthetic keyset (product keygen); device key on rank 0 -> RCCL bcast
+    lwe_sk = B.binary_key(p.n, 1)
+    glwe_sk = B.binary_key(p.big_n, 2)
+    fbytes = B.fourier_bsk_bytes(p)
+    t0 = time.perf_counter()
+    if rank == 0:
+        bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 3)
+        fbsk = B.convert_bsk(p, bsk, dev)
+    else:
+        bsk = None
+        fbsk = torch.empty(fbytes // 8, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    t_key = time.perf_counter() - t0
+    t_bcast = 0.0
+    if world > 1:
+        dist.barrier()
+        t0 = time.perf_counter()
+        dist.broadcast(fbsk, src=0)
+        torch.cuda.synchronize()
+        t_bcast = time.perf_counter() - t0
+
+    # ---- this rank's shard: 4096 fresh encryptions of random 3-bit messages, one shared LUT
+    rng = np.random.RandomState(1000 + rank)
+    table = rng.randint(0, 1 << width, size=1 << width).astype(np.uint64)
+    msgs = rng.randint(0, 1 << width, size=args.batch)
+    cts = B.lwe_encrypt(lwe_sk, [B.encode(m, width) for m in msgs], p.n, B.secure_std(1, p.n), 5000 + rank)
+    acc = B.trivial_glwe(p, B.expand_lut(table, p.N, width))
+    d_in = B.to_device(cts, dev)
+    d_lut = B.to_device(acc[None, :], dev)
+    d_out = torch.empty((args.batch, p.lwe_out_size), dtype=torch.int64, device=dev)
+
+    def step():
+        B.pbs(p, fbsk, d_in, d_lut, out=d_out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    # kernel events on the stream the kernels are launched on (torch's current stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record()
+        step()
+        ev[i][1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall, kern_ms = float(t[0]), float(t[1])
+
+    # ---- correctness of what was timed: decrypt-level on every row, bit-exact sample (rank 0)
+    out = B.to_host(d_out)
+    dec = B.lwe_decrypt(glwe_sk, out, p.big_n)
+    ok = sum(int(B.decode(d, width) == table[m]) for d, m in zip(dec, msgs))
+    ok_all = ok
+    if world > 1:
+        t = torch.tensor([ok], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        ok_all = int(t.item())
+
+    result = None
+    if rank == 0:
+        total = args.batch * world * args.steps
+        value = total / wall
+        bytes_per_pbs = p.bsk_bytes_per_pbs()
+        achieved = bytes_per_pbs * args.batch / (kern_ms * 1e-3) / 1e9
+        bitexact = None
+        cpu = None
+        if args.verify or not args.no_cpu_baseline:
+            from oracle import pyoracle as O  # checker / CPU baseline only
+            op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
+            if bsk is None:
+                bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 3)
+            fcpu = O.bsk_to_fourier(op, bsk)
+            if args.verify:
+                ref, _ = O.pbs_batch(op, cts[: args.verify], acc[None, :], fbsk=fcpu, nthreads=args.cpu_threads)
+                bitexact = bool(np.array_equal(ref, out[: args.verify]))
+            if not args.no_cpu_baseline:
+                sample = cts[: args.cpu_sample]
+                t1 = time.perf_counter()
+                O.pbs_batch(op, sample, acc[None, :], fbsk=fcpu, nthreads=args.cpu_threads)
+                dt = time.perf_counter() - t1
+                cpu = {"value": round(len(sample) / dt, 2), "unit": "PBS/s", "cores": args.cpu_threads,
+                       "kind": "port",
+                       "sample": f"{len(sample)} PBS of the same cfg2 workload (exact-limb f64 FFT restatement, "
+                                 f"OpenMP over ciphertexts), {dt:.2f} s wall"}
+        result = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "PBS/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (seeded keygen + fresh LWE encryptions of random 3-bit messages)",
+            "config": {"workload": "batched PBS cfg2: N=1024 k=1 n=630 l=3 logB=7",
+                       "batch_per_gpu": args.batch, "global_batch": args.batch * world,
+                       "parallelism": f"shard{world}", "key_bcast_s": round(t_bcast, 4),
+                       "key_convert_s": round(t_key, 3)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel_ms": round(kern_ms, 3), "bytes_per_pbs": bytes_per_pbs},
+            "cpu_baseline": cpu,
+            "checks": {"decrypt_ok": f"{ok_all}/{args.batch * world}", "bitexact_rows": args.verify,
+                       "bitexact": bitexact},
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,87 @@
+"""ctypes binding of libconcrete_hip.so (the C ABI declared in include/concrete_hip.h).
+
+The shared library is built in-tree (``make -C concrete_amd/csrc``); there is no fallback:
+if it is missing or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libconcrete_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "concrete_hip.h")
+
+u32, u64, i32, vp, dbl = C.c_uint32, C.c_uint64, C.c_int, C.c_void_p, C.c_double
+u64p = C.POINTER(C.c_uint64)
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "cuda_create_stream": (vp, [u32]),
+    "cuda_destroy_stream": (None, [vp, u32]),
+    "cuda_malloc_async": (vp, [u64, vp, u32]),
+    "cuda_memcpy_async_to_gpu": (None, [vp, vp, u64, vp, u32]),
+    "cuda_memcpy_async_to_cpu": (None, [vp, vp, u64, vp, u32]),
+    "cuda_drop": (None, [vp, u32]),
+    "cuda_drop_async": (None, [vp, vp, u32]),
+    "cuda_synchronize_device": (None, [u32]),
+    "cuda_convert_lwe_programmable_bootstrap_key_64": (None, [vp, u32, vp, vp, u32, u32, u32, u32]),
+    "scratch_cuda_programmable_bootstrap_64": (None, [vp, u32, C.POINTER(vp), u32, u32, u32, u32, C.c_bool]),
+    "cleanup_cuda_programmable_bootstrap": (None, [vp, u32, C.POINTER(vp)]),
+    "cuda_programmable_bootstrap_lwe_ciphertext_vector_64": (
+        None, [vp, u32, vp, vp, vp, vp, vp, vp, vp, vp, u32, u32, u32, u32, u32, u32, u32, u32]),
+    "cuda_keyswitch_lwe_ciphertext_vector_64": (None, [vp, u32, vp, vp, vp, vp, vp, u32, u32, u32, u32, u32]),
+    "concrete_hip_abi_version": (u32, []),
+    "concrete_hip_last_error": (C.c_char_p, []),
+    "concrete_hip_pbs_supported": (i32, [u32, u32, u32, u32]),
+    "concrete_hip_bsk_limbs": (u32, [u32, u32, u32]),
+    "concrete_hip_fourier_bsk_size_bytes": (u64, [u32, u32, u32, u32]),
+    "concrete_hip_convert_bsk": (i32, [vp, u32, vp, vp, i32, u32, u32, u32, u32]),
+    "concrete_hip_pbs": (i32, [vp, u32, vp, vp, vp, vp, vp, vp, vp, u32, u32, u32, u32, u32, u32, vp]),
+    "concrete_hip_keyswitch": (i32, [vp, u32, vp, vp, vp, vp, vp, u32, u32, u32, u32, u32]),
+    "concrete_hip_lookup_bsk": (vp, [vp]),
+    "concrete_hip_device_count": (i32, []),
+    "concrete_hip_secure_log2_std": (dbl, [u64, u64]),
+    "concrete_hip_keygen_binary": (None, [vp, u64, u64]),
+    "concrete_hip_lwe_encrypt_batch": (None, [vp, vp, vp, u64, u64, dbl, u64]),
+    "concrete_hip_lwe_decrypt": (u64, [vp, vp, u64]),
+    "concrete_hip_bsk_generate": (None, [vp, vp, vp, u64, u64, u64, u64, u64, dbl, u64]),
+    "concrete_hip_ksk_generate": (None, [vp, vp, vp, u64, u64, u64, u64, dbl, u64]),
+    "concrete_hip_encode_expand_lut": (None, [vp, u64, vp, u64, u32, i32]),
+}
+
+_lib = None
+
+
+class NativeMissing(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libconcrete_hip.so (raises NativeMissing if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeMissing(f"{LIB_PATH} not built: run `make -C concrete_amd/csrc` "
+                                "(or __graft_entry__.build()); there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def declared_symbols():
+    """Function names declared in include/concrete_hip.h."""
+    txt = open(HEADER_PATH).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b([a-z_][a-z0-9_]*)\s*\(", txt)) - {"defined"})
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().concrete_hip_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")

@@ -1,0 +1,327 @@
+// abi.hip — extern "C" entry points of libconcrete_hip.so (declared in include/concrete_hip.h).
+//
+// The cuda_* names are the backend ABI the Concrete runtime links; they
+// keep the reference conventions: void return, abort on failure, stream-ordered work.
+// The concrete_hip_* extensions return status codes for testability.
+#include <stdarg.h>
+
+#include <mutex>
+#include <unordered_map>
+
+#include "../../include/concrete_hip.h"
+#include "common.hpp"
+#include "pbs.hpp"
+
+namespace chip {
+
+static thread_local char g_err[512] = "";
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+}
+const char* last_error() { return g_err; }
+
+static void die(const char* what) {
+  fprintf(stderr, "concrete-hip: %s: %s\n", what, g_err);
+  abort();
+}
+
+// Registry of device Fourier keys created through the legacy convert entry point, keyed by
+// the caller's `dest` allocation (see concrete_hip.h, cuda_convert_lwe_programmable_bootstrap_key_64).
+struct KeyEntry {
+  void* fourier;
+  uint32_t gpu, n, k, level, N;
+};
+static std::mutex g_keys_mu;
+static std::unordered_map<const void*, KeyEntry> g_keys;
+
+static void set_device(uint32_t gpu) { CHIP_CHECK(hipSetDevice((int)gpu)); }
+
+static bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
+  return k == 1 && N == 1024 && level >= 1 && level <= 4 && base_log >= 1 && base_log <= 30 &&
+         level * base_log < 64;
+}
+
+}  // namespace chip
+
+using namespace chip;
+
+extern "C" {
+
+// ----------------------------------------------------------------------------------------
+// device / stream / memory management
+// ----------------------------------------------------------------------------------------
+void* cuda_create_stream(uint32_t gpu_index) {
+  set_device(gpu_index);
+  hipStream_t s;
+  CHIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  return (void*)s;
+}
+
+void cuda_destroy_stream(void* stream, uint32_t gpu_index) {
+  set_device(gpu_index);
+  CHIP_CHECK(hipStreamDestroy((hipStream_t)stream));
+}
+
+void* cuda_malloc_async(uint64_t size, void* stream, uint32_t gpu_index) {
+  set_device(gpu_index);
+  void* p = nullptr;
+  if (size == 0) return nullptr;
+  CHIP_CHECK(hipMallocAsync(&p, size, (hipStream_t)stream));
+  return p;
+}
+
+void cuda_memcpy_async_to_gpu(void* dest, void* src, uint64_t size, void* stream, uint32_t gpu_index) {
+  if (size == 0) return;
+  set_device(gpu_index);
+  CHIP_CHECK(hipMemcpyAsync(dest, src, size, hipMemcpyHostToDevice, (hipStream_t)stream));
+}
+
+void cuda_memcpy_async_to_cpu(void* dest, const void* src, uint64_t size, void* stream, uint32_t gpu_index) {
+  if (size == 0) return;
+  set_device(gpu_index);
+  CHIP_CHECK(hipMemcpyAsync(dest, src, size, hipMemcpyDeviceToHost, (hipStream_t)stream));
+}
+
+static void release_registered(void* ptr) {
+  void* f = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_keys_mu);
+    auto it = g_keys.find(ptr);
+    if (it != g_keys.end()) {
+      f = it->second.fourier;
+      g_keys.erase(it);
+    }
+  }
+  if (f) CHIP_CHECK(hipFree(f));
+}
+
+void cuda_drop(void* ptr, uint32_t gpu_index) {
+  if (!ptr) return;
+  set_device(gpu_index);
+  release_registered(ptr);
+  CHIP_CHECK(hipFree(ptr));
+}
+
+void cuda_drop_async(void* ptr, void* stream, uint32_t gpu_index) {
+  if (!ptr) return;
+  set_device(gpu_index);
+  release_registered(ptr);
+  CHIP_CHECK(hipFreeAsync(ptr, (hipStream_t)stream));
+}
+
+void cuda_synchronize_device(uint32_t gpu_index) {
+  set_device(gpu_index);
+  CHIP_CHECK(hipDeviceSynchronize());
+}
+
+// ----------------------------------------------------------------------------------------
+// extensions
+// ----------------------------------------------------------------------------------------
+uint32_t concrete_hip_abi_version(void) { return 1u; }
+const char* concrete_hip_last_error(void) { return last_error(); }
+int concrete_hip_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int concrete_hip_pbs_supported(uint32_t glwe_dim, uint32_t polynomial_size, uint32_t level_count,
+                               uint32_t base_log) {
+  return pbs_params_ok(glwe_dim, polynomial_size, level_count, base_log) ? 1 : 0;
+}
+
+uint32_t concrete_hip_bsk_limbs(uint32_t polynomial_size, uint32_t level_count, uint32_t base_log) {
+  return default_limbs(polynomial_size, level_count, base_log);
+}
+
+uint64_t concrete_hip_fourier_bsk_size_bytes(uint32_t input_lwe_dim, uint32_t glwe_dim, uint32_t level_count,
+                                             uint32_t polynomial_size) {
+  return fourier_bsk_bytes(input_lwe_dim, glwe_dim, level_count, polynomial_size,
+                           default_limbs(polynomial_size, level_count, 0));
+}
+
+int concrete_hip_convert_bsk(void* stream, uint32_t gpu_index, void* dest_fourier, const void* src,
+                             int src_is_device, uint32_t input_lwe_dim, uint32_t glwe_dim, uint32_t level_count,
+                             uint32_t polynomial_size) {
+  if (!dest_fourier || !src) {
+    set_error("convert_bsk: null pointer");
+    return -1;
+  }
+  if (!pbs_params_ok(glwe_dim, polynomial_size, level_count, 1)) {
+    set_error("convert_bsk: unsupported parameters k=%u N=%u level=%u", glwe_dim, polynomial_size, level_count);
+    return -2;
+  }
+  set_device(gpu_index);
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t std_bytes =
+      (uint64_t)input_lwe_dim * level_count * (glwe_dim + 1) * (glwe_dim + 1) * polynomial_size * 8ull;
+  const uint64_t* src_dev = (const uint64_t*)src;
+  void* tmp = nullptr;
+  if (!src_is_device) {
+    CHIP_CHECK(hipMallocAsync(&tmp, std_bytes, s));
+    CHIP_CHECK(hipMemcpyAsync(tmp, src, std_bytes, hipMemcpyHostToDevice, s));
+    src_dev = (const uint64_t*)tmp;
+  }
+  ConvertArgs a{s, dest_fourier, src_dev, input_lwe_dim, glwe_dim, level_count, polynomial_size,
+                default_limbs(polynomial_size, level_count, 0)};
+  int rc = convert_bsk_launch(a);
+  if (tmp) CHIP_CHECK(hipFreeAsync(tmp, s));
+  return rc;
+}
+
+int concrete_hip_pbs(void* stream, uint32_t gpu_index, uint64_t* lwe_array_out, const uint64_t* lwe_output_indexes,
+                     const uint64_t* lut_vector, const uint64_t* lut_vector_indexes, const uint64_t* lwe_array_in,
+                     const uint64_t* lwe_input_indexes, const void* fourier_bsk, uint32_t lwe_dimension,
+                     uint32_t glwe_dimension, uint32_t polynomial_size, uint32_t base_log, uint32_t level_count,
+                     uint32_t num_samples, uint64_t* resid_bits) {
+  if (num_samples == 0) return 0;
+  if (!lwe_array_out || !lut_vector || !lwe_array_in || !fourier_bsk) {
+    set_error("pbs: null pointer");
+    return -1;
+  }
+  if (!pbs_params_ok(glwe_dimension, polynomial_size, level_count, base_log)) {
+    set_error("pbs: unsupported parameters k=%u N=%u level=%u base_log=%u", glwe_dimension, polynomial_size,
+              level_count, base_log);
+    return -2;
+  }
+  set_device(gpu_index);
+  PbsArgs a{(hipStream_t)stream,
+            lwe_array_out,
+            lwe_output_indexes,
+            lut_vector,
+            lut_vector_indexes,
+            lwe_array_in,
+            lwe_input_indexes,
+            fourier_bsk,
+            lwe_dimension,
+            glwe_dimension,
+            polynomial_size,
+            base_log,
+            level_count,
+            default_limbs(polynomial_size, level_count, base_log),
+            num_samples,
+            (unsigned long long*)resid_bits};
+  return pbs_launch(a);
+}
+
+int concrete_hip_keyswitch(void* stream, uint32_t gpu_index, uint64_t* lwe_array_out,
+                           const uint64_t* lwe_output_indexes, const uint64_t* lwe_array_in,
+                           const uint64_t* lwe_input_indexes, const uint64_t* ksk, uint32_t lwe_dimension_in,
+                           uint32_t lwe_dimension_out, uint32_t base_log, uint32_t level_count,
+                           uint32_t num_samples) {
+  if (num_samples == 0) return 0;
+  if (!lwe_array_out || !lwe_array_in || !ksk) {
+    set_error("keyswitch: null pointer");
+    return -1;
+  }
+  set_device(gpu_index);
+  KsArgs a{(hipStream_t)stream, lwe_array_out, lwe_output_indexes, lwe_array_in, lwe_input_indexes, ksk,
+           lwe_dimension_in,    lwe_dimension_out, base_log,       level_count,  num_samples};
+  return keyswitch_launch(a);
+}
+
+const void* concrete_hip_lookup_bsk(const void* bootstrapping_key) {
+  std::lock_guard<std::mutex> g(g_keys_mu);
+  auto it = g_keys.find(bootstrapping_key);
+  return it == g_keys.end() ? nullptr : it->second.fourier;
+}
+
+// ----------------------------------------------------------------------------------------
+// runtime-facing PBS / KS entry points
+// ----------------------------------------------------------------------------------------
+void cuda_convert_lwe_programmable_bootstrap_key_64(void* stream, uint32_t gpu_index, void* dest, void* src,
+                                                    uint32_t input_lwe_dim, uint32_t glwe_dim,
+                                                    uint32_t level_count, uint32_t polynomial_size) {
+  set_device(gpu_index);
+  const uint64_t bytes = concrete_hip_fourier_bsk_size_bytes(input_lwe_dim, glwe_dim, level_count, polynomial_size);
+  void* f = nullptr;
+  CHIP_CHECK(hipMalloc(&f, bytes));
+  // dest (caller-sized at n*l*(k+1)^2*N*8 bytes) receives the standard key verbatim and is the
+  // conversion source; the Fourier form (larger: exact limbs) lives in the registry.
+  const uint64_t std_bytes =
+      (uint64_t)input_lwe_dim * level_count * (glwe_dim + 1) * (glwe_dim + 1) * polynomial_size * 8ull;
+  CHIP_CHECK(hipMemcpyAsync(dest, src, std_bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+  if (concrete_hip_convert_bsk(stream, gpu_index, f, dest, 1, input_lwe_dim, glwe_dim, level_count,
+                               polynomial_size) != 0)
+    die("cuda_convert_lwe_programmable_bootstrap_key_64");
+  void* old = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_keys_mu);
+    auto it = g_keys.find(dest);
+    if (it != g_keys.end()) old = it->second.fourier;
+    g_keys[dest] = KeyEntry{f, gpu_index, input_lwe_dim, glwe_dim, level_count, polynomial_size};
+  }
+  if (old) {
+    CHIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    CHIP_CHECK(hipFree(old));
+  }
+}
+
+void scratch_cuda_programmable_bootstrap_64(void* stream, uint32_t gpu_index, int8_t** pbs_buffer,
+                                            uint32_t glwe_dimension, uint32_t polynomial_size,
+                                            uint32_t level_count, uint32_t input_lwe_ciphertext_count,
+                                            bool allocate_gpu_memory) {
+  (void)input_lwe_ciphertext_count;
+  if (!pbs_params_ok(glwe_dimension, polynomial_size, level_count, 1)) {
+    set_error("scratch: unsupported parameters k=%u N=%u level=%u", glwe_dimension, polynomial_size, level_count);
+    die("scratch_cuda_programmable_bootstrap_64");
+  }
+  // The kernel keeps all per-ciphertext state in LDS/VGPRs: the buffer is a 256-byte token
+  // (diagnostics word at offset 0) so that the caller's ownership protocol is unchanged.
+  if (!allocate_gpu_memory) {
+    *pbs_buffer = nullptr;
+    return;
+  }
+  set_device(gpu_index);
+  void* p = nullptr;
+  CHIP_CHECK(hipMallocAsync(&p, 256, (hipStream_t)stream));
+  CHIP_CHECK(hipMemsetAsync(p, 0, 256, (hipStream_t)stream));
+  *pbs_buffer = (int8_t*)p;
+}
+
+void cleanup_cuda_programmable_bootstrap(void* stream, uint32_t gpu_index, int8_t** pbs_buffer) {
+  if (!pbs_buffer || !*pbs_buffer) return;
+  set_device(gpu_index);
+  CHIP_CHECK(hipFreeAsync(*pbs_buffer, (hipStream_t)stream));
+  *pbs_buffer = nullptr;
+}
+
+void cuda_programmable_bootstrap_lwe_ciphertext_vector_64(
+    void* stream, uint32_t gpu_index, void* lwe_array_out, void* lwe_output_indexes, void* lut_vector,
+    void* lut_vector_indexes, void* lwe_array_in, void* lwe_input_indexes, void* bootstrapping_key,
+    int8_t* pbs_buffer, uint32_t lwe_dimension, uint32_t glwe_dimension, uint32_t polynomial_size,
+    uint32_t base_log, uint32_t level_count, uint32_t num_samples, uint32_t num_many_lut, uint32_t lut_stride) {
+  (void)pbs_buffer;
+  if (num_many_lut != 1 || lut_stride != 1) {
+    set_error("num_many_lut=%u lut_stride=%u (only 1, 1 is used by the runtime)", num_many_lut, lut_stride);
+    die("cuda_programmable_bootstrap_lwe_ciphertext_vector_64");
+  }
+  const void* f = concrete_hip_lookup_bsk(bootstrapping_key);
+  if (!f) {
+    set_error("bootstrapping key %p was not converted by cuda_convert_lwe_programmable_bootstrap_key_64",
+              bootstrapping_key);
+    die("cuda_programmable_bootstrap_lwe_ciphertext_vector_64");
+  }
+  if (concrete_hip_pbs(stream, gpu_index, (uint64_t*)lwe_array_out, (const uint64_t*)lwe_output_indexes,
+                       (const uint64_t*)lut_vector, (const uint64_t*)lut_vector_indexes,
+                       (const uint64_t*)lwe_array_in, (const uint64_t*)lwe_input_indexes, f, lwe_dimension,
+                       glwe_dimension, polynomial_size, base_log, level_count, num_samples, nullptr) != 0)
+    die("cuda_programmable_bootstrap_lwe_ciphertext_vector_64");
+}
+
+void cuda_keyswitch_lwe_ciphertext_vector_64(void* stream, uint32_t gpu_index, void* lwe_array_out,
+                                             void* lwe_output_indexes, void* lwe_array_in,
+                                             void* lwe_input_indexes, void* ksk, uint32_t lwe_dimension_in,
+                                             uint32_t lwe_dimension_out, uint32_t base_log,
+                                             uint32_t level_count, uint32_t num_samples) {
+  if (concrete_hip_keyswitch(stream, gpu_index, (uint64_t*)lwe_array_out, (const uint64_t*)lwe_output_indexes,
+                             (const uint64_t*)lwe_array_in, (const uint64_t*)lwe_input_indexes,
+                             (const uint64_t*)ksk, lwe_dimension_in, lwe_dimension_out, base_log, level_count,
+                             num_samples) != 0)
+    die("cuda_keyswitch_lwe_ciphertext_vector_64");
+}
+
+}  // extern "C"

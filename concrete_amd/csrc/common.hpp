@@ -1,0 +1,46 @@
+// common.hpp — shared host/device helpers for libconcrete_hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+namespace chip {
+
+// Reference behaviour for the cuda_* ABI: void returns, failures abort the process
+// (concrete-cpu c_api.rs:22-36 `nounwind`; tfhe-cuda-backend check_cuda_error).
+#define CHIP_CHECK(expr)                                                                      \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess) {                                                                   \
+      fprintf(stderr, "concrete-hip: %s failed at %s:%d: %s\n", #expr, __FILE__, __LINE__,    \
+              hipGetErrorString(_e));                                                         \
+      abort();                                                                                \
+    }                                                                                         \
+  } while (0)
+
+// Error state for the concrete_hip_* extension entry points (which return status codes).
+void set_error(const char* fmt, ...);
+const char* last_error();
+
+// Torus helpers -------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint32_t modswitch(uint64_t x, int log2_2n) {
+  // pbs_modulus_switch (tfhe 0.10) == simulation.cpp:64-75: round(x * 2N / 2^64) mod 2N
+  return (uint32_t)((x + (1ull << (63 - log2_2n))) >> (64 - log2_2n));
+}
+
+// Balanced signed decomposition (tfhe 0.10 SignedDecomposer::init_decomposer_state +
+// decompose_one_level; restated in oracle/tfhe_oracle.c:ora_decomp_*).
+__device__ __forceinline__ uint64_t decomp_init(uint64_t x, int nrep) {
+  return (x >> nrep) + ((x >> (nrep - 1)) & 1ull);
+}
+__device__ __forceinline__ int32_t decomp_next(uint64_t& state, int logB) {
+  const uint64_t mask = (1ull << logB) - 1ull;
+  uint64_t res = state & mask;
+  state >>= logB;
+  uint64_t carry = (((res - 1ull) | state) & res) >> (logB - 1);
+  state += carry;
+  return (int32_t)(int64_t)(res - (carry << logB));
+}
+
+}  // namespace chip

@@ -1,0 +1,152 @@
+// fft512.hpp — one-wavefront 512-point complex FFT for the N = 1024 negacyclic product.
+//
+// One wave64 owns one polynomial: lane t holds 8 complex points (16 f64 registers).
+// 512 = 8 x 8 x 8: three in-register radix-8 passes, two intra-wave LDS transposes.
+// Forward (DIF, natural in -> digit-permuted out):
+//   in : lane t holds z[t + 64 m], m = 0..7
+//   out: lane (k0 = t>>3, k1 = t&7) holds Z[k0 + 8 k1 + 64 k2], k2 = 0..7
+// Inverse (the transposed DIT, conjugate twiddles, unnormalised) maps that layout back.
+// The pointwise product never needs natural frequency order, so no reordering pass exists.
+//
+// LDS transpose slot (complex index within the wave's 8 KB scratch):
+//   S(a, b, c) = 64 a + 8 ((b ^ a) & 7) + (c ^ b)
+// found by exhaustive search against the gfx950 ds_read_b128 / ds_write_b128 lane groups
+// (MI355X_MICROARCH.md §LDS): both transposes are bank-conflict free for reads and writes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace chip {
+
+struct __attribute__((aligned(16))) cplx {
+  double re, im;
+};
+
+__device__ __forceinline__ cplx cadd(cplx a, cplx b) { return {a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ cplx csub(cplx a, cplx b) { return {a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ cplx cmul(cplx a, cplx w) {
+  return {__builtin_fma(a.re, w.re, -a.im * w.im), __builtin_fma(a.re, w.im, a.im * w.re)};
+}
+// a * conj(w)
+__device__ __forceinline__ cplx cmulc(cplx a, cplx w) {
+  return {__builtin_fma(a.re, w.re, a.im * w.im), __builtin_fma(a.im, w.re, -a.re * w.im)};
+}
+// a * (-i) (forward) or a * (+i) (inverse)
+template <bool INV>
+__device__ __forceinline__ cplx mul_mi(cplx a) {
+  if constexpr (INV) return {-a.im, a.re};
+  else return {a.im, -a.re};
+}
+// a * w8^1 with w8 = exp(-+ i pi/4)
+template <bool INV>
+__device__ __forceinline__ cplx mul_w8(cplx a) {
+  constexpr double r = 0.70710678118654752440084436210485;
+  if constexpr (INV) return {(a.re - a.im) * r, (a.re + a.im) * r};
+  else return {(a.re + a.im) * r, (a.im - a.re) * r};
+}
+// a * w8^3
+template <bool INV>
+__device__ __forceinline__ cplx mul_w83(cplx a) {
+  constexpr double r = 0.70710678118654752440084436210485;
+  if constexpr (INV) return {(-a.re - a.im) * r, (a.re - a.im) * r};
+  else return {(a.im - a.re) * r, (-a.re - a.im) * r};
+}
+
+// In-register 8-point DFT, natural order in and out: X[k] = sum_m x[m] w8^{+-mk}.
+template <bool INV>
+__device__ __forceinline__ void dft8(cplx (&v)[8]) {
+  // stage 1 (span 4)
+  cplx a0 = cadd(v[0], v[4]), a4 = csub(v[0], v[4]);
+  cplx a1 = cadd(v[1], v[5]), a5 = csub(v[1], v[5]);
+  cplx a2 = cadd(v[2], v[6]), a6 = csub(v[2], v[6]);
+  cplx a3 = cadd(v[3], v[7]), a7 = csub(v[3], v[7]);
+  a5 = mul_w8<INV>(a5);
+  a6 = mul_mi<INV>(a6);
+  a7 = mul_w83<INV>(a7);
+  // stage 2 (span 2)
+  cplx b0 = cadd(a0, a2), b2 = csub(a0, a2);
+  cplx b1 = cadd(a1, a3), b3 = mul_mi<INV>(csub(a1, a3));
+  cplx b4 = cadd(a4, a6), b6 = csub(a4, a6);
+  cplx b5 = cadd(a5, a7), b7 = mul_mi<INV>(csub(a5, a7));
+  // stage 3 (span 1); bit-reversed positions -> natural order
+  v[0] = cadd(b0, b1);
+  v[4] = csub(b0, b1);
+  v[2] = cadd(b2, b3);
+  v[6] = csub(b2, b3);
+  v[1] = cadd(b4, b5);
+  v[5] = csub(b4, b5);
+  v[3] = cadd(b6, b7);
+  v[7] = csub(b6, b7);
+}
+
+__device__ __forceinline__ int xslot(int a, int b, int c) { return 64 * a + 8 * ((b ^ a) & 7) + (c ^ b); }
+
+// Ordering point for intra-wave LDS traffic: LDS operations of one wave execute in issue
+// order, so only the compiler has to be kept from moving them across this point.
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Twiddle tables (LDS-resident, shared by the workgroup):
+//   tw1[k0 * 64 + t] = w512^{t k0}, tw2[k1 * 8 + t0] = w64^{t0 k1}, w_M = exp(-2 pi i / M)
+struct Fft512Tables {
+  const cplx* tw1;  // 512 entries
+  const cplx* tw2;  // 64 entries
+};
+
+__device__ __forceinline__ void fft512_fwd(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane) {
+  const int hi = lane >> 3, lo = lane & 7;
+  dft8<false>(v);
+#pragma unroll
+  for (int k0 = 1; k0 < 8; ++k0) v[k0] = cmul(v[k0], T.tw1[k0 * 64 + lane]);
+  // transpose 1: writer lane (t1 = hi, t0 = lo) element k0 ; reader lane (k0 = hi, t0 = lo) element t1
+#pragma unroll
+  for (int e = 0; e < 8; ++e) xch[xslot(e, hi, lo)] = v[e];
+  wave_lds_fence();
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = xch[xslot(hi, e, lo)];
+  wave_lds_fence();
+  dft8<false>(v);
+#pragma unroll
+  for (int k1 = 1; k1 < 8; ++k1) v[k1] = cmul(v[k1], T.tw2[k1 * 8 + lo]);
+  // transpose 2: writer lane (k0 = hi, t0 = lo) element k1 ; reader lane (k0 = hi, k1 = lo) element t0
+#pragma unroll
+  for (int e = 0; e < 8; ++e) xch[xslot(hi, e, lo)] = v[e];
+  wave_lds_fence();
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = xch[xslot(hi, lo, e)];
+  wave_lds_fence();
+  dft8<false>(v);
+}
+
+__device__ __forceinline__ void fft512_inv(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane) {
+  const int hi = lane >> 3, lo = lane & 7;
+  dft8<true>(v);  // over k2 -> t0 ; lane (k0 = hi, k1 = lo)
+#pragma unroll
+  for (int t0 = 1; t0 < 8; ++t0) v[t0] = cmulc(v[t0], T.tw2[lo * 8 + t0]);
+  // transpose 2': writer lane (k0, k1) element t0 ; reader lane (k0 = hi, t0 = lo) element k1
+#pragma unroll
+  for (int e = 0; e < 8; ++e) xch[xslot(hi, lo, e)] = v[e];
+  wave_lds_fence();
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = xch[xslot(hi, e, lo)];
+  wave_lds_fence();
+  dft8<true>(v);  // over k1 -> t1 ; lane (k0 = hi, t0 = lo)
+#pragma unroll
+  for (int t1 = 0; t1 < 8; ++t1) v[t1] = cmulc(v[t1], T.tw1[hi * 64 + 8 * t1 + lo]);
+  // transpose 1': writer lane (k0 = hi, t0 = lo) element t1 ; reader lane (t1 = hi, t0 = lo) element k0
+#pragma unroll
+  for (int e = 0; e < 8; ++e) xch[xslot(hi, e, lo)] = v[e];
+  wave_lds_fence();
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = xch[xslot(e, hi, lo)];
+  wave_lds_fence();
+  dft8<true>(v);  // over k0 -> m ; lane t holds z[t + 64 m]
+}
+
+// Frequency index held in (lane, slot) after fft512_fwd.
+__host__ __device__ constexpr int fft512_freq(int lane, int slot) { return (lane >> 3) + 8 * (lane & 7) + 64 * slot; }
+
+}  // namespace chip

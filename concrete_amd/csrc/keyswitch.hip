@@ -1,0 +1,95 @@
+// keyswitch.hip — batched LWE keyswitch (exact u64 torus arithmetic).
+//
+// Reference semantics: concrete-cpu c_api/keyswitch.rs:185-223 -> tfhe 0.10
+// keyswitch_lwe_ciphertext (restated in oracle/tfhe_oracle.c:ora_keyswitch):
+//   out = (0, ..., 0, b) - sum_i sum_t d_{i,t} * KSK[i][t],  digits yielded level l first,
+// KSK layout [n_in][l][n_out+1] u64 exactly as the runtime uploads it (context.h:117-145).
+// Batched call shape: cuda_keyswitch_lwe_ciphertext_vector_64 (GPUDFG.cpp:1098-1101).
+//
+// Mapping: a workgroup owns KS_TILE samples; each KSK row (one (i, t) pair, n_out+1 words)
+// is read once per tile with 2 KB coalesced loads and applied to all KS_TILE samples, so
+// the 20.7 MB (cfg2) key is streamed B / KS_TILE times instead of B times.
+#include "common.hpp"
+#include "pbs.hpp"
+
+namespace chip {
+
+constexpr int KS_TILE = 8;
+constexpr int KS_THREADS = 256;
+constexpr int KS_ICHUNK = 32;
+constexpr int KS_MAX_OUT = 3 * KS_THREADS;  // n_out + 1 <= 768
+constexpr int KS_MAX_L = 8;
+
+__global__ void __launch_bounds__(KS_THREADS)
+keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx, const uint64_t* __restrict__ in,
+                 const uint64_t* __restrict__ in_idx, const uint64_t* __restrict__ ksk, uint32_t n_in,
+                 uint32_t n_out, uint32_t base_log, uint32_t level, uint32_t num_samples) {
+  __shared__ int32_t dig[KS_TILE][KS_ICHUNK][KS_MAX_L];
+  const uint32_t s0 = blockIdx.x * KS_TILE;
+  const int tid = threadIdx.x;
+  const uint32_t W = n_out + 1;
+  uint64_t acc[KS_TILE][3];
+#pragma unroll
+  for (int s = 0; s < KS_TILE; ++s)
+#pragma unroll
+    for (int u = 0; u < 3; ++u) acc[s][u] = 0ull;
+  const int nrep = 64 - (int)(level * base_log);
+
+  for (uint32_t i0 = 0; i0 < n_in; i0 += KS_ICHUNK) {
+    __syncthreads();
+    for (int e = tid; e < KS_TILE * KS_ICHUNK; e += KS_THREADS) {
+      const int s = e / KS_ICHUNK, ii = e % KS_ICHUNK;
+      const uint32_t smp = s0 + s, i = i0 + ii;
+      uint64_t a = 0ull;
+      if (smp < num_samples && i < n_in) a = in[(in_idx ? in_idx[smp] : smp) * (uint64_t)(n_in + 1) + i];
+      uint64_t st = decomp_init(a, nrep);
+      for (uint32_t t = 0; t < level; ++t) dig[s][ii][t] = decomp_next(st, (int)base_log);
+    }
+    __syncthreads();
+    const uint32_t iend = min(KS_ICHUNK, (int)(n_in - i0));
+    for (uint32_t ii = 0; ii < iend; ++ii) {
+      for (uint32_t t = 0; t < level; ++t) {
+        const uint64_t* row = ksk + ((uint64_t)(i0 + ii) * level + t) * W;
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const uint32_t j = tid + u * KS_THREADS;
+          const uint64_t kv = j < W ? row[j] : 0ull;
+#pragma unroll
+          for (int s = 0; s < KS_TILE; ++s) acc[s][u] -= (uint64_t)(int64_t)dig[s][ii][t] * kv;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < KS_TILE; ++s) {
+    const uint32_t smp = s0 + s;
+    if (smp >= num_samples) break;
+    const uint64_t* ci = in + (in_idx ? in_idx[smp] : smp) * (uint64_t)(n_in + 1);
+    uint64_t* co = out + (out_idx ? out_idx[smp] : smp) * (uint64_t)W;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const uint32_t j = tid + u * KS_THREADS;
+      if (j < W) co[j] = acc[s][u] + (j == n_out ? ci[n_in] : 0ull);
+    }
+  }
+}
+
+int keyswitch_launch(const KsArgs& a) {
+  if (a.n_out + 1 > (uint32_t)KS_MAX_OUT || a.level > (uint32_t)KS_MAX_L || a.level == 0 ||
+      a.level * a.base_log >= 64 || a.base_log == 0) {
+    set_error("unsupported keyswitch parameters: n_out=%u level=%u base_log=%u", a.n_out, a.level, a.base_log);
+    return -2;
+  }
+  const uint32_t blocks = (a.num_samples + KS_TILE - 1) / KS_TILE;
+  if (blocks == 0) return 0;
+  hipLaunchKernelGGL(keyswitch_kernel, dim3(blocks), dim3(KS_THREADS), 0, a.stream, a.out, a.out_idx, a.in,
+                     a.in_idx, a.ksk, a.n_in, a.n_out, a.base_log, a.level, a.num_samples);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("keyswitch launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+}  // namespace chip

@@ -1,0 +1,64 @@
+// pbs.hpp — host-side descriptors for the PBS and BSK-conversion kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace chip {
+
+// N = 1024 kernel geometry: PBS1024_WAVES independent ciphertexts (one per wave) per
+// workgroup sharing one copy of the twiddle tables in LDS.
+constexpr int PBS1024_WAVES = 4;
+constexpr size_t PBS1024_TABLE_BYTES = (512 + 64 + 512) * 16;  // tw1, tw2, zeta
+__host__ __device__ constexpr size_t pbs1024_wave_bytes(int k) {
+  return (size_t)(k + 1) * 1024 * 8 /* acc */ + 512 * 16 /* transpose scratch */;
+}
+constexpr size_t pbs1024_lds_bytes(int k) { return PBS1024_TABLE_BYTES + PBS1024_WAVES * pbs1024_wave_bytes(k); }
+
+// Number of exact limbs of the key polynomial for a parameter set.
+inline uint32_t default_limbs(uint32_t N, uint32_t level, uint32_t base_log) {
+  (void)level;
+  (void)base_log;
+  return N <= 1024 ? 3u : 6u;
+}
+
+// Size in bytes of the device Fourier bootstrapping key (complex f64 per limb, N/2 per poly).
+inline uint64_t fourier_bsk_bytes(uint32_t n, uint32_t k, uint32_t level, uint32_t N, uint32_t limbs) {
+  return (uint64_t)n * level * (k + 1) * (k + 1) * limbs * (N / 2) * 16ull;
+}
+
+struct PbsArgs {
+  hipStream_t stream;
+  uint64_t* out;
+  const uint64_t* out_idx;
+  const uint64_t* luts;
+  const uint64_t* lut_idx;
+  const uint64_t* in;
+  const uint64_t* in_idx;
+  const void* fbsk;
+  uint32_t n, k, N, base_log, level, limbs, num_samples;
+  unsigned long long* resid;  // optional: max |x - round(x)| over all outputs (f64 bits)
+};
+
+int pbs_launch(const PbsArgs& a);
+
+struct ConvertArgs {
+  hipStream_t stream;
+  void* dest;               // Fourier key, fourier_bsk_bytes()
+  const uint64_t* src_dev;  // standard-domain key on the device [n][l][k+1][k+1][N]
+  uint32_t n, k, level, N, limbs;
+};
+int convert_bsk_launch(const ConvertArgs& a);
+
+struct KsArgs {
+  hipStream_t stream;
+  uint64_t* out;
+  const uint64_t* out_idx;
+  const uint64_t* in;
+  const uint64_t* in_idx;
+  const uint64_t* ksk;
+  uint32_t n_in, n_out, base_log, level, num_samples;
+};
+int keyswitch_launch(const KsArgs& a);
+
+}  // namespace chip

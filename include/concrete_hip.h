@@ -1,0 +1,146 @@
+/*
+ * concrete_hip.h — C ABI of libconcrete_hip.so, the MI355X-native (gfx950) backend for the
+ * batched programmable-bootstrap path of the Concrete compiler runtime.
+ *
+ * Part 1 (cuda_* / scratch_* / cleanup_* names) is exactly the set of backend entry points
+ * libConcretelangRuntime calls when built with CONCRETELANG_CUDA_SUPPORT; the names are kept
+ * because the runtime's compiled call sites use them.  Each declaration cites the reference
+ * call site it replaces (paths relative to /root/reference/compilers/concrete-compiler/compiler).
+ * Conventions: void returns, failures abort (reference `nounwind`,
+ * backends/concrete-cpu/implementation/src/c_api.rs:22-36); everything is stream-ordered;
+ * the caller synchronises.  `stream` is a hipStream_t created by cuda_create_stream.
+ *
+ * Part 2 (concrete_hip_*) are extensions: a size query for the device key format (fixes the
+ * runtime's `len * sizeof(double)` allocation hazard, include/concretelang/Runtime/context.h:101-105),
+ * status-returning variants, and the direct (no key registry) PBS used by the multi-GPU glue.
+ */
+#ifndef CONCRETE_HIP_H
+#define CONCRETE_HIP_H
+
+#include <stdbool.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------------------------
+ * Part 1: runtime-facing ABI (tfhe-cuda-backend names)
+ * ------------------------------------------------------------------------------------------ */
+
+/* lib/Runtime/wrappers.cpp:129,185,283; lib/Runtime/GPUDFG.cpp:191 */
+void *cuda_create_stream(uint32_t gpu_index);
+/* lib/Runtime/wrappers.cpp:160,255,362; lib/Runtime/GPUDFG.cpp:168 */
+void cuda_destroy_stream(void *stream, uint32_t gpu_index);
+/* lib/Runtime/wrappers.cpp:50,146,194; include/concretelang/Runtime/context.h:103-104 */
+void *cuda_malloc_async(uint64_t size, void *stream, uint32_t gpu_index);
+/* lib/Runtime/wrappers.cpp:51,222; lib/Runtime/GPUDFG.cpp:475,1194; context.h:137-139 */
+void cuda_memcpy_async_to_gpu(void *dest, void *src, uint64_t size, void *stream, uint32_t gpu_index);
+/* lib/Runtime/wrappers.cpp:59; lib/Runtime/GPUDFG.cpp:407,463,1034 */
+void cuda_memcpy_async_to_cpu(void *dest, const void *src, uint64_t size, void *stream, uint32_t gpu_index);
+/* lib/Runtime/wrappers.cpp:65,157-159; include/concretelang/Runtime/context.h:47-55 */
+void cuda_drop(void *ptr, uint32_t gpu_index);
+/* lib/Runtime/wrappers.cpp:246-250; lib/Runtime/GPUDFG.cpp:392,422,432,1102 */
+void cuda_drop_async(void *ptr, void *stream, uint32_t gpu_index);
+/* lib/Runtime/wrappers.cpp:155 */
+void cuda_synchronize_device(uint32_t gpu_index);
+
+/* include/concretelang/Runtime/context.h:104-109: H2D + conversion of the standard u64 BSK
+ * (host pointer `src`, layout [n][l][k+1][k+1][N], concrete-cpu bootstrap.rs:417-429) into the
+ * device key format.  `dest` is the caller's allocation of n*l*(k+1)^2*N*8 bytes; the device
+ * format is larger (exact limbs), so the backend keeps it in a registry keyed by `dest` and
+ * releases it when cuda_drop(dest) is called.  The key is usable once the stream is synced. */
+void cuda_convert_lwe_programmable_bootstrap_key_64(void *stream, uint32_t gpu_index, void *dest, void *src,
+                                                    uint32_t input_lwe_dim, uint32_t glwe_dim,
+                                                    uint32_t level_count, uint32_t polynomial_size);
+
+/* lib/Runtime/wrappers.cpp:234,341; lib/Runtime/GPUDFG.cpp:126 */
+void scratch_cuda_programmable_bootstrap_64(void *stream, uint32_t gpu_index, int8_t **pbs_buffer,
+                                            uint32_t glwe_dimension, uint32_t polynomial_size,
+                                            uint32_t level_count, uint32_t input_lwe_ciphertext_count,
+                                            bool allocate_gpu_memory);
+/* lib/Runtime/wrappers.cpp:241,348; lib/Runtime/GPUDFG.cpp:131 */
+void cleanup_cuda_programmable_bootstrap(void *stream, uint32_t gpu_index, int8_t **pbs_buffer);
+
+/* lib/Runtime/wrappers.cpp:237-240,344-347; lib/Runtime/GPUDFG.cpp:1214-1218: batched classic PBS.
+ *   out[out_idx[s]] (kN+1 u64) = PBS(in[in_idx[s]] (n+1 u64), lut_vector[lut_idx[s]] ((k+1)N u64))
+ * bootstrapping_key is the `dest` of cuda_convert_lwe_programmable_bootstrap_key_64.
+ * The last two arguments are passed as (1, 1) by every reference call site (one LUT per
+ * sample, stride 1); other values abort. */
+void cuda_programmable_bootstrap_lwe_ciphertext_vector_64(
+    void *stream, uint32_t gpu_index, void *lwe_array_out, void *lwe_output_indexes, void *lut_vector,
+    void *lut_vector_indexes, void *lwe_array_in, void *lwe_input_indexes, void *bootstrapping_key,
+    int8_t *pbs_buffer, uint32_t lwe_dimension, uint32_t glwe_dimension, uint32_t polynomial_size,
+    uint32_t base_log, uint32_t level_count, uint32_t num_samples, uint32_t num_many_lut, uint32_t lut_stride);
+
+/* lib/Runtime/wrappers.cpp:149-151, GPUDFG.cpp:1098-1101: batched LWE keyswitch; ksk is the
+ * standard u64 key [n_in][l][n_out+1] copied verbatim to the device (context.h:117-145). */
+void cuda_keyswitch_lwe_ciphertext_vector_64(void *stream, uint32_t gpu_index, void *lwe_array_out,
+                                             void *lwe_output_indexes, void *lwe_array_in,
+                                             void *lwe_input_indexes, void *ksk, uint32_t lwe_dimension_in,
+                                             uint32_t lwe_dimension_out, uint32_t base_log,
+                                             uint32_t level_count, uint32_t num_samples);
+
+/* ------------------------------------------------------------------------------------------
+ * Part 2: extensions (return 0 on success, < 0 on error; message via concrete_hip_last_error)
+ * ------------------------------------------------------------------------------------------ */
+
+/* ABI version of this header. */
+uint32_t concrete_hip_abi_version(void);
+/* thread-local message of the last failed concrete_hip_* call */
+const char *concrete_hip_last_error(void);
+/* 1 if (k, N, level, base_log) has a compiled PBS kernel, else 0 */
+int concrete_hip_pbs_supported(uint32_t glwe_dim, uint32_t polynomial_size, uint32_t level_count,
+                               uint32_t base_log);
+/* number of exact key limbs the device format uses for these parameters */
+uint32_t concrete_hip_bsk_limbs(uint32_t polynomial_size, uint32_t level_count, uint32_t base_log);
+/* bytes of the device (Fourier, exact-limb) bootstrapping key */
+uint64_t concrete_hip_fourier_bsk_size_bytes(uint32_t input_lwe_dim, uint32_t glwe_dim, uint32_t level_count,
+                                             uint32_t polynomial_size);
+/* convert a standard u64 BSK (host pointer if src_is_device == 0, else device pointer) into a
+ * caller-owned device buffer of concrete_hip_fourier_bsk_size_bytes() bytes */
+int concrete_hip_convert_bsk(void *stream, uint32_t gpu_index, void *dest_fourier, const void *src,
+                             int src_is_device, uint32_t input_lwe_dim, uint32_t glwe_dim, uint32_t level_count,
+                             uint32_t polynomial_size);
+/* batched PBS on a caller-owned Fourier key (no registry lookup); index arrays may be NULL
+ * (identity for in/out, LUT 0 for lut).  resid_bits: optional device u64 receiving the f64
+ * bits of max |x - round(x)| seen in the exact recombination (diagnostics; slower kernel). */
+int concrete_hip_pbs(void *stream, uint32_t gpu_index, uint64_t *lwe_array_out, const uint64_t *lwe_output_indexes,
+                     const uint64_t *lut_vector, const uint64_t *lut_vector_indexes, const uint64_t *lwe_array_in,
+                     const uint64_t *lwe_input_indexes, const void *fourier_bsk, uint32_t lwe_dimension,
+                     uint32_t glwe_dimension, uint32_t polynomial_size, uint32_t base_log, uint32_t level_count,
+                     uint32_t num_samples, uint64_t *resid_bits);
+/* batched keyswitch, status-returning variant */
+int concrete_hip_keyswitch(void *stream, uint32_t gpu_index, uint64_t *lwe_array_out,
+                           const uint64_t *lwe_output_indexes, const uint64_t *lwe_array_in,
+                           const uint64_t *lwe_input_indexes, const uint64_t *ksk, uint32_t lwe_dimension_in,
+                           uint32_t lwe_dimension_out, uint32_t base_log, uint32_t level_count,
+                           uint32_t num_samples);
+/* Fourier key registered for a `dest` of cuda_convert_lwe_programmable_bootstrap_key_64, or NULL */
+const void *concrete_hip_lookup_bsk(const void *bootstrapping_key);
+/* number of visible devices */
+int concrete_hip_device_count(void);
+
+/* ------------------------------------------------------------------------------------------
+ * Part 3: client-side helpers (host code; synthetic workloads and LUT encoding).  Mirrors the
+ * concrete-cpu client ABI (backends/concrete-cpu/implementation/include/concrete-cpu.h:
+ * concrete_cpu_init_secret_key_u64, concrete_cpu_encrypt_lwe_ciphertext_u64,
+ * concrete_cpu_init_lwe_bootstrap_key_u64, concrete_cpu_init_lwe_keyswitch_key_u64) and the
+ * runtime's LUT expansion (compiler lib/Runtime/wrappers.cpp:388-450).  Deterministic per seed.
+ * ------------------------------------------------------------------------------------------ */
+double concrete_hip_secure_log2_std(uint64_t glwe_dim, uint64_t poly_size);
+void concrete_hip_keygen_binary(uint64_t *sk, uint64_t len, uint64_t seed);
+void concrete_hip_lwe_encrypt_batch(const uint64_t *sk, uint64_t *out, const uint64_t *plaintexts, uint64_t count,
+                                    uint64_t n, double std_torus, uint64_t seed);
+uint64_t concrete_hip_lwe_decrypt(const uint64_t *sk, const uint64_t *ct, uint64_t n);
+void concrete_hip_bsk_generate(uint64_t *bsk, const uint64_t *lwe_sk, const uint64_t *glwe_sk, uint64_t n,
+                               uint64_t k, uint64_t N, uint64_t l, uint64_t logB, double std_torus, uint64_t seed);
+void concrete_hip_ksk_generate(uint64_t *ksk, const uint64_t *sk_in, const uint64_t *sk_out, uint64_t n_in,
+                               uint64_t n_out, uint64_t l, uint64_t logB, double std_torus, uint64_t seed);
+void concrete_hip_encode_expand_lut(uint64_t *out, uint64_t out_size, const uint64_t *in, uint64_t in_size,
+                                    uint32_t out_message_bits, int is_signed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CONCRETE_HIP_H */

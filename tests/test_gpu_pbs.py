@@ -1,0 +1,289 @@
+"""GPU parity tests: libconcrete_hip.so (HIP kernels on cuda:0) vs the CPU oracle.
+
+Bit-exact u64 equality of every output word (integer/torus work: no tolerance), plus
+decrypt-level checks against the reference generators' cleartext vectors and
+size-independent properties at the metric's batch size.
+"""
+import ctypes as C
+import json
+import math
+import os
+from dataclasses import replace
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "reference_lut_fixtures.json")
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def B():
+    from concrete_amd import backend
+    return backend
+
+
+def oparams(oracle, p):
+    return oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, ks_l=p.ks_level, ks_logB=p.ks_base_log)
+
+
+class Setup:
+    def __init__(self, B, oracle, torch, p, seed):
+        self.p = p
+        self.op = oparams(oracle, p)
+        self.lwe_sk = B.binary_key(p.n, seed)
+        self.glwe_sk = B.binary_key(p.big_n, seed + 1)
+        self.bsk = B.bsk_generate(p, self.lwe_sk, self.glwe_sk, seed + 2)
+        self.fbsk_cpu = oracle.bsk_to_fourier(self.op, self.bsk)
+        self.fbsk = B.convert_bsk(p, self.bsk, "cuda:0")
+        torch.cuda.synchronize()
+
+
+@pytest.fixture(scope="module")
+def cfg2(B, oracle, torch_cuda):
+    return Setup(B, oracle, torch_cuda, B.CFG2, 1000)
+
+
+@pytest.fixture(scope="module")
+def small(B, oracle, torch_cuda):
+    return Setup(B, oracle, torch_cuda, replace(B.CFG2, n=24), 2000)
+
+
+def encrypt(B, S, msgs, width, seed, std=None):
+    std = B.secure_std(1, S.p.n) if std is None else std
+    return B.lwe_encrypt(S.lwe_sk, [B.encode(m, width) for m in msgs], S.p.n, std, seed)
+
+
+def lut_acc(B, S, table, width):
+    return B.trivial_glwe(S.p, B.expand_lut(np.array(table, dtype=np.uint64), S.p.N, width))
+
+
+def run_gpu(B, S, cts, luts, torch, lut_idx=None, in_idx=None, out_idx=None, out_rows=None, resid=False):
+    dev = "cuda:0"
+    d_in = B.to_device(cts, dev)
+    d_luts = B.to_device(np.atleast_2d(luts), dev)
+    args = {}
+    n_s = cts.shape[0] if in_idx is None else len(in_idx)
+    for name, a in (("lut_idx", lut_idx), ("in_idx", in_idx), ("out_idx", out_idx)):
+        if a is not None:
+            args[name] = B.to_device(np.asarray(a, dtype=np.uint64), dev)
+    out = torch.zeros(((out_rows or n_s), S.p.lwe_out_size), dtype=torch.int64, device=dev)
+    r = torch.zeros(1, dtype=torch.int64, device=dev) if resid else None
+    B.pbs(S.p, S.fbsk, d_in, d_luts, out=out, num_samples=n_s, resid=r, **args)
+    torch.cuda.synchronize()
+    res = B.to_host(out)
+    if resid:
+        return res, float(np.array([r.item()], dtype=np.int64).view(np.float64)[0])
+    return res
+
+
+def run_oracle(oracle, S, cts, luts, lut_idx=None, in_idx=None, out_idx=None):
+    out, resid = oracle.pbs_batch(S.op, cts, np.atleast_2d(luts), fbsk=S.fbsk_cpu, lut_idx=lut_idx, in_idx=in_idx,
+                                  out_idx=out_idx)
+    return out
+
+
+def test_fourier_key_matches_oracle_transform(B, small, torch_cuda):
+    """Device conversion (double-double FFT) == oracle extended-precision transform, reordered
+    into the kernel's (lane, slot) layout; both are within ~1 ulp of the exact spectrum."""
+    p = small.p
+    g = B.to_host(small.fbsk).view(np.float64).reshape(p.n, p.k + 1, 3, (p.k + 1) * p.level, 8, 64, 2)
+    o = small.fbsk_cpu.reshape(p.n, p.level, p.k + 1, p.k + 1, 3, 2, 512)
+    lane = np.arange(64)
+    slot = np.arange(8)
+    K = (lane[None, :] >> 3) + 8 * (lane[None, :] & 7) + 64 * slot[:, None]  # (8, 64)
+    maxrel = 0.0
+    for v in range(p.level):
+        for row in range(p.k + 1):
+            rq = row * p.level + (p.level - 1 - v)
+            for col in range(p.k + 1):
+                for li in range(3):
+                    ref_re = o[:, v, row, col, li, 0][:, K]
+                    ref_im = o[:, v, row, col, li, 1][:, K]
+                    got = g[:, col, li, rq]
+                    scale = np.max(np.abs(o[:, v, row, col, li]))
+                    err = max(np.max(np.abs(got[..., 0] - ref_re)), np.max(np.abs(got[..., 1] - ref_im)))
+                    maxrel = max(maxrel, err / scale)
+    assert maxrel < 4e-16, maxrel
+
+
+@pytest.mark.parametrize("batch", [1, 3, 4, 5, 64])
+def test_pbs_bit_exact_small(B, oracle, small, torch_cuda, batch):
+    width = 3
+    rng = np.random.RandomState(batch)
+    table = rng.randint(0, 8, size=8)
+    msgs = rng.randint(0, 8, size=batch)
+    cts = encrypt(B, small, msgs, width, 10 + batch, std=2.0 ** -25)
+    acc = lut_acc(B, small, table, width)
+    got = run_gpu(B, small, cts, acc, torch_cuda)
+    ref = run_oracle(oracle, small, cts, acc)
+    assert np.array_equal(got, ref)
+    dec = B.lwe_decrypt(small.glwe_sk, got, small.p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+
+
+def test_pbs_bit_exact_cfg2(B, oracle, cfg2, torch_cuda):
+    width = 3
+    rng = np.random.RandomState(7)
+    table = rng.randint(0, 8, size=8)
+    msgs = rng.randint(0, 8, size=64)
+    cts = encrypt(B, cfg2, msgs, width, 77)
+    acc = lut_acc(B, cfg2, table, width)
+    got, resid = run_gpu(B, cfg2, cts, acc, torch_cuda, resid=True)
+    ref = run_oracle(oracle, cfg2, cts, acc)
+    assert np.array_equal(got, ref)
+    bound = oracle.fft_error_bound(cfg2.op, cfg2.fbsk_cpu)
+    assert resid < bound < 0.5, (resid, bound)
+    dec = B.lwe_decrypt(cfg2.glwe_sk, got, cfg2.p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+
+
+def test_pbs_edge_inputs(B, oracle, small, torch_cuda):
+    """Zero mask elements (tfhe skip rule), mask elements whose modulus switch is 0 or 2N-1,
+    body near 2^64 (modulus switch wraps to 2N), all-zero and all-ones ciphertexts."""
+    p = small.p
+    width = 2
+    rng = np.random.RandomState(5)
+    cts = encrypt(B, small, rng.randint(0, 4, size=8), width, 31, std=2.0 ** -25)
+    cts[0, : p.n // 2] = 0
+    cts[1, :] = 0
+    cts[2, :] = np.uint64(0xFFFFFFFFFFFFFFFF)
+    cts[3, : p.n] = np.uint64(1)                         # ms(1) == 0 but a_i != 0
+    cts[4, : p.n] = np.uint64((1 << 53) - 1)             # just below a modswitch rounding boundary
+    cts[5, p.n] = np.uint64(0xFFFFFFFFFFFFFFFF - 5)      # body rounds up to 2N
+    cts[6, : p.n] = np.uint64(1 << 63)                   # ms = N (negation)
+    acc = lut_acc(B, small, [3, 1, 0, 2], width)
+    got = run_gpu(B, small, cts, acc, torch_cuda)
+    ref = run_oracle(oracle, small, cts, acc)
+    assert np.array_equal(got, ref)
+
+
+def test_pbs_index_arrays_and_mapped_luts(B, oracle, small, torch_cuda):
+    """Runtime index-array semantics (GPUDFG.cpp:1149-1205): permuted inputs/outputs and one
+    LUT per sample (memref_batched_mapped_bootstrap_lwe_cuda_u64, wrappers.cpp:317-325)."""
+    width = 3
+    nb = 12
+    rng = np.random.RandomState(9)
+    msgs = rng.randint(0, 8, size=nb)
+    cts = encrypt(B, small, msgs, width, 41, std=2.0 ** -25)
+    tables = [rng.randint(0, 8, size=8) for _ in range(nb)]
+    luts = np.stack([lut_acc(B, small, t, width) for t in tables])
+    lut_idx = rng.permutation(nb).astype(np.uint64)
+    in_idx = rng.permutation(nb).astype(np.uint64)
+    out_idx = rng.permutation(nb).astype(np.uint64)
+    got = run_gpu(B, small, cts, luts, torch_cuda, lut_idx=lut_idx, in_idx=in_idx, out_idx=out_idx)
+    ref = run_oracle(oracle, small, cts, luts, lut_idx=lut_idx, in_idx=in_idx, out_idx=out_idx)
+    assert np.array_equal(got, ref)
+    dec = B.lwe_decrypt(small.glwe_sk, got, small.p.big_n)
+    for s in range(nb):
+        assert B.decode(dec[out_idx[s]], width) == int(tables[lut_idx[s]][msgs[in_idx[s]]])
+
+
+def test_reference_fixtures_decrypt(B, cfg2, torch_cuda):
+    """Cleartext vectors of the reference generators (p <= 4 fits cfg2's noise budget)."""
+    fx = json.load(open(GOLDEN))
+    cases = [c for c in fx["apply_lookup_table"] + fx["linalg_apply_lookup_table"]
+             if len(c["lut"]) <= 16 and not c["description"].endswith("_2layer")]
+    assert len(cases) >= 20
+    for ci, c in enumerate(cases):
+        width = int(math.log2(len(c["lut"])))
+        cts = encrypt(B, cfg2, c["input"], width, 500 + ci)
+        got = run_gpu(B, cfg2, cts, lut_acc(B, cfg2, c["lut"], width), torch_cuda)
+        dec = B.lwe_decrypt(cfg2.glwe_sk, got, cfg2.p.big_n)
+        assert [B.decode(d, width) for d in dec] == c["expected"], c["description"]
+
+
+def test_metric_batch_properties(B, oracle, cfg2, torch_cuda):
+    """B = 4096 (the metric's batch): every sample decrypts to LUT[m]; 16 random rows bit-exact."""
+    width = 3
+    nb = 4096
+    rng = np.random.RandomState(11)
+    table = rng.randint(0, 8, size=8)
+    msgs = rng.randint(0, 8, size=nb)
+    cts = encrypt(B, cfg2, msgs, width, 1234)
+    acc = lut_acc(B, cfg2, table, width)
+    got = run_gpu(B, cfg2, cts, acc, torch_cuda)
+    dec = B.lwe_decrypt(cfg2.glwe_sk, got, cfg2.p.big_n)
+    assert all(B.decode(d, width) == table[m] for d, m in zip(dec, msgs))
+    pick = rng.choice(nb, size=16, replace=False)
+    ref = run_oracle(oracle, cfg2, cts[pick], acc)
+    assert np.array_equal(got[pick], ref)
+
+
+def test_legacy_abi_sequence(B, oracle, small, torch_cuda):
+    """Replay of memref_batched_bootstrap_lwe_cuda_u64 (wrappers.cpp:164-256) on the cuda_* ABI:
+    stream, H2D, convert (registry), scratch, PBS, cleanup, D2H, drop."""
+    from concrete_amd import _native
+    L = _native.lib()
+    p = small.p
+    width = 3
+    msgs = np.arange(8)
+    cts = encrypt(B, small, msgs, width, 55, std=2.0 ** -25)
+    acc = lut_acc(B, small, [7, 6, 5, 4, 3, 2, 1, 0], width)
+    nb = len(msgs)
+    s = L.cuda_create_stream(0)
+    bsk_bytes = p.bsk_len * 8
+    d_bsk = L.cuda_malloc_async(bsk_bytes, s, 0)
+    L.cuda_convert_lwe_programmable_bootstrap_key_64(s, 0, d_bsk, small.bsk.ctypes.data, p.n, p.k, p.level, p.N)
+    assert L.concrete_hip_lookup_bsk(d_bsk)
+    d_in = L.cuda_malloc_async(cts.nbytes, s, 0)
+    L.cuda_memcpy_async_to_gpu(d_in, cts.ctypes.data, cts.nbytes, s, 0)
+    d_out = L.cuda_malloc_async(nb * p.lwe_out_size * 8, s, 0)
+    d_acc = L.cuda_malloc_async(acc.nbytes, s, 0)
+    L.cuda_memcpy_async_to_gpu(d_acc, acc.ctypes.data, acc.nbytes, s, 0)
+    idx = np.arange(nb, dtype=np.uint64)
+    zeros = np.zeros(nb, dtype=np.uint64)
+    d_idx = L.cuda_malloc_async(idx.nbytes, s, 0)
+    d_lidx = L.cuda_malloc_async(idx.nbytes, s, 0)
+    L.cuda_memcpy_async_to_gpu(d_idx, idx.ctypes.data, idx.nbytes, s, 0)
+    L.cuda_memcpy_async_to_gpu(d_lidx, zeros.ctypes.data, zeros.nbytes, s, 0)
+    buf = C.c_void_p()
+    L.scratch_cuda_programmable_bootstrap_64(s, 0, C.byref(buf), p.k, p.N, p.level, nb, True)
+    L.cuda_programmable_bootstrap_lwe_ciphertext_vector_64(s, 0, d_out, d_idx, d_acc, d_lidx, d_in, d_idx, d_bsk,
+                                                          buf, p.n, p.k, p.N, p.base_log, p.level, nb, 1, 1)
+    L.cleanup_cuda_programmable_bootstrap(s, 0, C.byref(buf))
+    assert not buf.value
+    out = np.zeros((nb, p.lwe_out_size), dtype=np.uint64)
+    L.cuda_memcpy_async_to_cpu(out.ctypes.data, d_out, out.nbytes, s, 0)
+    L.cuda_synchronize_device(0)
+    for ptr in (d_in, d_out, d_acc, d_idx, d_lidx):
+        L.cuda_drop_async(ptr, s, 0)
+    L.cuda_drop(d_bsk, 0)
+    assert not L.concrete_hip_lookup_bsk(d_bsk)
+    L.cuda_destroy_stream(s, 0)
+    ref = run_oracle(oracle, small, cts, acc)
+    assert np.array_equal(out, ref)
+
+
+def test_keyswitch_bit_exact_and_chain(B, oracle, cfg2, torch_cuda):
+    """KS (kN -> n) bit-exact vs the oracle, then the KS -> PBS atomic pattern
+    (FHEToTFHEScalar.cpp:373-437) on the reference's 2-layer fixtures with p <= 2."""
+    p = cfg2.p
+    op = cfg2.op
+    ksk = B.ksk_generate(p, cfg2.glwe_sk, cfg2.lwe_sk, 4321)
+    d_ksk = B.to_device(ksk, "cuda:0")
+    fx = json.load(open(GOLDEN))
+    cases = [c for c in fx["linalg_apply_lookup_table"] if c["description"].endswith("_2layer") and len(c["lut"]) <= 4]
+    assert cases
+    for ci, c in enumerate(cases):
+        width = int(math.log2(len(c["lut"])))
+        xs = c["input"]
+        cts = encrypt(B, cfg2, xs, width, 900 + ci)
+        acc = lut_acc(B, cfg2, c["lut"], width)
+        big = run_gpu(B, cfg2, cts, acc, torch_cuda)            # layer 1: PBS -> kN key
+        d_big = B.to_device(big, "cuda:0")
+        d_small = B.keyswitch(p, d_ksk, d_big)
+        torch_cuda.cuda.synchronize()
+        small_cts = B.to_host(d_small)
+        assert np.array_equal(small_cts, oracle.keyswitch_batch(op, big, ksk))
+        out = run_gpu(B, cfg2, small_cts, acc, torch_cuda)      # layer 2
+        dec = B.lwe_decrypt(cfg2.glwe_sk, out, p.big_n)
+        assert [B.decode(d, width) for d in dec] == c["expected"], c["description"]

@@ -1,0 +1,74 @@
+"""CPU tests of libconcrete_hip.so: it loads, exports every symbol include/concrete_hip.h
+declares, its host-side client helpers agree bit-for-bit with the oracle, and its
+status-returning entry points reject bad arguments before touching a device."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from concrete_amd import _native
+from concrete_amd import backend as B
+
+
+def test_library_exports_every_declared_symbol():
+    L = _native.lib()
+    declared = _native.declared_symbols()
+    assert len(declared) >= 30
+    for name in declared:
+        assert hasattr(L, name), name
+    # and every declared symbol has a ctypes signature in the host binding
+    assert set(declared) <= set(_native.SIGNATURES), set(declared) - set(_native.SIGNATURES)
+
+
+def test_abi_version_and_queries():
+    L = _native.lib()
+    assert L.concrete_hip_abi_version() == 1
+    assert L.concrete_hip_pbs_supported(1, 1024, 3, 7) == 1
+    assert L.concrete_hip_pbs_supported(1, 1024, 3, 30) == 0  # l * logB >= 64
+    assert L.concrete_hip_pbs_supported(2, 1024, 3, 7) == 0
+    assert L.concrete_hip_bsk_limbs(1024, 3, 7) == 3
+    p = B.CFG2
+    # n * l * (k+1)^2 * LIMBS * N/2 complex f64
+    assert B.fourier_bsk_bytes(p) == p.n * p.level * 4 * 3 * 512 * 16
+    assert B.fourier_bsk_bytes(p) == 3 * p.bsk_len * 8  # 3 limbs x 8 B per coefficient
+
+
+def test_status_codes_without_device():
+    L = _native.lib()
+    # unsupported parameters are rejected before any device call
+    rc = L.concrete_hip_pbs(None, 0, 1, None, 1, None, 1, None, 1, 630, 2, 1024, 7, 3, 4, None)
+    assert rc == -2 and b"unsupported" in L.concrete_hip_last_error()
+    rc = L.concrete_hip_pbs(None, 0, None, None, None, None, None, None, None, 630, 1, 1024, 7, 3, 4, None)
+    assert rc == -1
+    assert L.concrete_hip_pbs(None, 0, None, None, None, None, None, None, None, 630, 1, 1024, 7, 3, 0, None) == 0
+    rc = L.concrete_hip_convert_bsk(None, 0, None, None, 0, 630, 1, 3, 1024)
+    assert rc == -1
+
+
+def test_keygen_matches_oracle(oracle):
+    p = B.PbsParams(n=32, k=1, N=1024, level=3, base_log=7, ks_level=4, ks_base_log=3)
+    op = oracle.Params(n=32, k=1, N=1024, l=3, logB=7, ks_l=4, ks_logB=3)
+    for seed in (1, 99):
+        assert np.array_equal(B.binary_key(777, seed), oracle.binary_key(777, seed))
+    lwe_sk = B.binary_key(p.n, 1)
+    glwe_sk = B.binary_key(p.big_n, 2)
+    bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 3)
+    assert np.array_equal(bsk, oracle.keygen_bsk(op, lwe_sk, glwe_sk, 3))
+    ksk = B.ksk_generate(p, glwe_sk, lwe_sk, 4)
+    assert np.array_equal(ksk, oracle.keygen_ksk(op, glwe_sk, lwe_sk, 4))
+    pts = [int(B.encode(m, 3)) for m in range(8)]
+    cts = B.lwe_encrypt(lwe_sk, pts, p.n, 2.0 ** -20, 5)
+    assert np.array_equal(cts, oracle.lwe_encrypt_batch(lwe_sk, pts, p.n, 2.0 ** -20, 5))
+    assert np.array_equal(B.lwe_decrypt(lwe_sk, cts, p.n), oracle.lwe_decrypt_batch(lwe_sk, cts, p.n))
+    for bits in (1, 3, 4):
+        for signed in (False, True):
+            tab = np.arange(1 << bits, dtype=np.uint64)[::-1].copy()
+            assert np.array_equal(B.expand_lut(tab, 1024, bits, signed), oracle.expand_lut(tab, 1024, bits, signed))
+
+
+def test_encode_decode_match_oracle(oracle):
+    for width in (1, 3, 4, 8):
+        for m in range(1 << width):
+            e = B.encode(m, width)
+            assert int(e) == int(oracle.encode(m, width))
+            assert B.decode(e, width) == oracle.decode(e, width) == m

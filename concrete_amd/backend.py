@@ -118,12 +118,16 @@ def encode(m, width: int):
     return np.uint64((int(m) << (64 - (width + 1))) & 0xFFFFFFFFFFFFFFFF)
 
 
-def decode(x, width: int) -> int:
-    """Native unsigned decoding, compiler lib/Common/Transformers.cpp:384-410."""
+def decode(x, width: int, signed: bool = False) -> int:
+    """Native decoding, compiler lib/Common/Transformers.cpp:384-427 (signed: sign-extended)."""
     x = int(x)
     out = x >> (64 - width - 2)
     carry = out % 2
-    return ((out >> 1) + carry) % (1 << (width + 1))
+    out = ((out >> 1) + carry) % (1 << (width + 1))
+    if signed and out >= (1 << (width - 1)):
+        # Transformers.cpp:414-419: output |= UINT64_MAX << precision, read as int64
+        out = (out & ((1 << width) - 1)) - (1 << width)
+    return out
 
 
 def expand_lut(table, N: int, out_bits: int, signed: bool = False) -> np.ndarray:

@@ -32,6 +32,8 @@ def cases(docs):
             x = ins[0].get("scalar", ins[0].get("tensor"))
             res.append({
                 "description": d["description"],
+                "input_signed": bool(ins[0].get("signed", False)),
+                "output_signed": bool(t["outputs"][0].get("signed", False)),
                 "input": x if isinstance(x, list) else [x],
                 "lut": ins[1]["tensor"],
                 "expected": (lambda o: o if isinstance(o, list) else [o])(

@@ -188,17 +188,27 @@ def test_pbs_index_arrays_and_mapped_luts(B, oracle, small, torch_cuda):
 
 
 def test_reference_fixtures_decrypt(B, cfg2, torch_cuda):
-    """Cleartext vectors of the reference generators (p <= 4 fits cfg2's noise budget)."""
+    """Cleartext vectors of the reference generators (p <= 4 fits cfg2's noise budget), incl. the
+    signed/unsigned variants: a signed input first gets the 2^(p-1) offset added to its body and
+    the LUT is expanded half-rotated (FHEToTFHEScalar.cpp:373-413, wrappers.cpp:409-421)."""
     fx = json.load(open(GOLDEN))
     cases = [c for c in fx["apply_lookup_table"] + fx["linalg_apply_lookup_table"]
              if len(c["lut"]) <= 16 and not c["description"].endswith("_2layer")]
-    assert len(cases) >= 20
+    assert len(cases) >= 40
+    kinds = set()
     for ci, c in enumerate(cases):
         width = int(math.log2(len(c["lut"])))
-        cts = encrypt(B, cfg2, c["input"], width, 500 + ci)
-        got = run_gpu(B, cfg2, cts, lut_acc(B, cfg2, c["lut"], width), torch_cuda)
+        xs = [int(x) & ((1 << 64) - 1) for x in c["input"]]
+        cts = encrypt(B, cfg2, xs, width, 500 + ci)
+        if c["input_signed"]:
+            cts[:, cfg2.p.n] += B.encode(1 << (width - 1), width)
+        table = np.array(c["lut"], dtype=np.int64).view(np.uint64)
+        acc = B.trivial_glwe(cfg2.p, B.expand_lut(table, cfg2.p.N, width, c["input_signed"]))
+        got = run_gpu(B, cfg2, cts, acc, torch_cuda)
         dec = B.lwe_decrypt(cfg2.glwe_sk, got, cfg2.p.big_n)
-        assert [B.decode(d, width) for d in dec] == c["expected"], c["description"]
+        assert [B.decode(d, width, c["output_signed"]) for d in dec] == c["expected"], c["description"]
+        kinds.add((c["input_signed"], c["output_signed"]))
+    assert len(kinds) == 4
 
 
 def test_metric_batch_properties(B, oracle, cfg2, torch_cuda):

@@ -40,7 +40,7 @@ static std::unordered_map<const void*, KeyEntry> g_keys;
 static void set_device(uint32_t gpu) { CHIP_CHECK(hipSetDevice((int)gpu)); }
 
 static bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
-  return k == 1 && N == 1024 && level >= 1 && level <= 4 && base_log >= 1 && base_log <= 30 &&
+  return k == 1 && N == 1024 && level >= 1 && level <= 3 && base_log >= 1 && base_log <= 30 &&
          level * base_log < 64;
 }
 
@@ -181,6 +181,10 @@ int concrete_hip_pbs(void* stream, uint32_t gpu_index, uint64_t* lwe_array_out, 
   if (!lwe_array_out || !lut_vector || !lwe_array_in || !fourier_bsk) {
     set_error("pbs: null pointer");
     return -1;
+  }
+  if (lwe_dimension == 0) {
+    set_error("pbs: lwe_dimension must be > 0");
+    return -3;
   }
   if (!pbs_params_ok(glwe_dimension, polynomial_size, level_count, base_log)) {
     set_error("pbs: unsupported parameters k=%u N=%u level=%u base_log=%u", glwe_dimension, polynomial_size,

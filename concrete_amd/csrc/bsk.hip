@@ -165,7 +165,7 @@ static void make_tables(uint32_t N, std::vector<ddc>& zeta, std::vector<ddc>& tw
 }
 
 int convert_bsk_launch(const ConvertArgs& a) {
-  if (!(a.N == 1024 && a.k == 1 && a.limbs == 3 && a.level >= 1 && a.level <= 4)) {
+  if (!(a.N == 1024 && a.k == 1 && a.limbs == 3 && a.level >= 1 && a.level <= 3)) {
     set_error("unsupported BSK conversion parameters: N=%u k=%u level=%u limbs=%u", a.N, a.k, a.level, a.limbs);
     return -2;
   }
@@ -180,8 +180,7 @@ int convert_bsk_launch(const ConvertArgs& a) {
   switch (a.level) {
     case 1: rc = launch_convert<1024, 1, 1, 3>(a, dz, dt); break;
     case 2: rc = launch_convert<1024, 1, 2, 3>(a, dz, dt); break;
-    case 3: rc = launch_convert<1024, 1, 3, 3>(a, dz, dt); break;
-    default: rc = launch_convert<1024, 1, 4, 3>(a, dz, dt); break;
+    default: rc = launch_convert<1024, 1, 3, 3>(a, dz, dt); break;
   }
   // the host tables must outlive the async copies: synchronise before they go out of scope
   CHIP_CHECK(hipStreamSynchronize(a.stream));

@@ -6,14 +6,14 @@
 
 namespace chip {
 
-// N = 1024 kernel geometry: PBS1024_WAVES independent ciphertexts (one per wave) per
-// workgroup sharing one copy of the twiddle tables in LDS.
+// N = 1024 kernel geometry: PBS1024_WAVES ciphertexts (one per wave) per workgroup sharing the
+// twiddle tables and a 2-slot ring of Fourier-key slices in LDS.
 constexpr int PBS1024_WAVES = 4;
 constexpr size_t PBS1024_TABLE_BYTES = (512 + 64 + 512) * 16;  // tw1, tw2, zeta
-__host__ __device__ constexpr size_t pbs1024_wave_bytes(int k) {
-  return (size_t)(k + 1) * 1024 * 8 /* acc */ + 512 * 16 /* transpose scratch */;
+constexpr size_t pbs1024_slice_bytes(int k, int level) { return (size_t)(k + 1) * level * 512 * 16; }
+constexpr size_t pbs1024_lds_bytes(int k, int level) {
+  return PBS1024_TABLE_BYTES + PBS1024_WAVES * 512 * 16 /* transpose scratch */ + 2 * pbs1024_slice_bytes(k, level);
 }
-constexpr size_t pbs1024_lds_bytes(int k) { return PBS1024_TABLE_BYTES + PBS1024_WAVES * pbs1024_wave_bytes(k); }
 
 // Number of exact limbs of the key polynomial for a parameter set.
 inline uint32_t default_limbs(uint32_t N, uint32_t level, uint32_t base_log) {

@@ -188,13 +188,14 @@ def test_pbs_index_arrays_and_mapped_luts(B, oracle, small, torch_cuda):
 
 
 def test_reference_fixtures_decrypt(B, cfg2, torch_cuda):
-    """Cleartext vectors of the reference generators (p <= 4 fits cfg2's noise budget), incl. the
+    """Cleartext vectors of the reference generators (p <= 3: cfg2's PBS output noise, sigma ~5.5e-3,
+    leaves 5.7 sigma to the p = 3 decoding boundary but only 2.8 at p = 4), incl. the
     signed/unsigned variants: a signed input first gets the 2^(p-1) offset added to its body and
     the LUT is expanded half-rotated (FHEToTFHEScalar.cpp:373-413, wrappers.cpp:409-421)."""
     fx = json.load(open(GOLDEN))
     cases = [c for c in fx["apply_lookup_table"] + fx["linalg_apply_lookup_table"]
-             if len(c["lut"]) <= 16 and not c["description"].endswith("_2layer")]
-    assert len(cases) >= 40
+             if len(c["lut"]) <= 8 and not c["description"].endswith("_2layer")]
+    assert len(cases) >= 30
     kinds = set()
     for ci, c in enumerate(cases):
         width = int(math.log2(len(c["lut"])))

@@ -3,15 +3,24 @@
 // One wave64 owns one polynomial: lane t holds 8 complex points (16 f64 registers).
 // 512 = 8 x 8 x 8: three in-register radix-8 passes, two intra-wave LDS transposes.
 // Forward (DIF, natural in -> digit-permuted out):
-//   in : lane t holds z[t + 64 m], m = 0..7
-//   out: lane (k0 = t>>3, k1 = t&7) holds Z[k0 + 8 k1 + 64 k2], k2 = 0..7
-// Inverse (the transposed DIT, conjugate twiddles, unnormalised) maps that layout back.
+//   in : lane t holds x[t + 64 m], m = 0..7 (untwisted: the negacyclic twist is folded in)
+//   out: lane (k0 = t>>3, k1 = t&7) holds Z[k0 + 8 k1 + 64 k2], k2 = 0..7, where
+//        Z = DFT_512(x_j * zeta^j), zeta = exp(i pi / 1024), DFT sign exp(-2 pi i jk / 512)
+// Inverse (the transposed DIT, conjugate twiddles, unnormalised) maps that layout back and
+// applies conj(zeta^j), so inverse(forward(x)) = 512 x.
 // The pointwise product never needs natural frequency order, so no reordering pass exists.
 //
-// LDS transpose slot (complex index within the wave's 8 KB scratch):
-//   S(a, b, c) = 64 a + 8 ((b ^ a) & 7) + (c ^ b)
-// found by exhaustive search against the gfx950 ds_read_b128 / ds_write_b128 lane groups
-// (MI355X_MICROARCH.md §LDS): both transposes are bank-conflict free for reads and writes.
+// Twist folding: zeta^{t + 64 m} = zeta^t * psi^m with psi = zeta^64 = exp(i pi / 16).  psi^m
+// (8 constants) multiplies the pass-1 inputs; zeta^t is merged into the pass-1 output twiddle,
+// giving one per-lane table T1[k0][t] = zeta^t * w512^{t k0} used by both directions.
+//
+// LDS transpose slot (complex index within the wave's 575-slot / 9.2 KB scratch):
+//   S(a, b, c) = 72 a + 9 b + c
+// Affine in every index, so each of the three access patterns is one per-lane base VGPR plus
+// ds_read/ds_write immediate offsets (an XOR swizzle is conflict-free but costs 24 live address
+// VGPRs).  Found by exhaustive search over padded strides against the gfx950 ds_read_b128 /
+// ds_write_b128 lane groups (MI355X_MICROARCH.md §LDS): all writes conflict-free, reads at most
+// 2-way on one of the three patterns.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -55,7 +64,6 @@ __device__ __forceinline__ cplx mul_w83(cplx a) {
 // In-register 8-point DFT, natural order in and out: X[k] = sum_m x[m] w8^{+-mk}.
 template <bool INV>
 __device__ __forceinline__ void dft8(cplx (&v)[8]) {
-  // stage 1 (span 4)
   cplx a0 = cadd(v[0], v[4]), a4 = csub(v[0], v[4]);
   cplx a1 = cadd(v[1], v[5]), a5 = csub(v[1], v[5]);
   cplx a2 = cadd(v[2], v[6]), a6 = csub(v[2], v[6]);
@@ -63,12 +71,10 @@ __device__ __forceinline__ void dft8(cplx (&v)[8]) {
   a5 = mul_w8<INV>(a5);
   a6 = mul_mi<INV>(a6);
   a7 = mul_w83<INV>(a7);
-  // stage 2 (span 2)
   cplx b0 = cadd(a0, a2), b2 = csub(a0, a2);
   cplx b1 = cadd(a1, a3), b3 = mul_mi<INV>(csub(a1, a3));
   cplx b4 = cadd(a4, a6), b6 = csub(a4, a6);
   cplx b5 = cadd(a5, a7), b7 = mul_mi<INV>(csub(a5, a7));
-  // stage 3 (span 1); bit-reversed positions -> natural order
   v[0] = cadd(b0, b1);
   v[4] = csub(b0, b1);
   v[2] = cadd(b2, b3);
@@ -79,7 +85,8 @@ __device__ __forceinline__ void dft8(cplx (&v)[8]) {
   v[7] = csub(b6, b7);
 }
 
-__device__ __forceinline__ int xslot(int a, int b, int c) { return 64 * a + 8 * ((b ^ a) & 7) + (c ^ b); }
+__device__ __forceinline__ int xslot(int a, int b, int c) { return 72 * a + 9 * b + c; }
+constexpr int XCH_SLOTS = 72 * 7 + 9 * 7 + 7 + 1;  // 575 complex slots per wave
 
 // Ordering point for intra-wave LDS traffic: LDS operations of one wave execute in issue
 // order, so only the compiler has to be kept from moving them across this point.
@@ -89,18 +96,52 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Twiddle tables (LDS-resident, shared by the workgroup):
-//   tw1[k0 * 64 + t] = w512^{t k0}, tw2[k1 * 8 + t0] = w64^{t0 k1}, w_M = exp(-2 pi i / M)
+// psi^m = exp(i pi m / 16), m = 0..7 (correctly rounded)
+__device__ __forceinline__ cplx psi_pow(int m) {
+  constexpr double C[8] = {1.0,
+                           0.98078528040323044912618223613424,
+                           0.92387953251128675612818318939679,
+                           0.83146961230254523707878837761791,
+                           0.70710678118654752440084436210485,
+                           0.55557023301960222474283081394853,
+                           0.38268343236508977172845998403040,
+                           0.19509032201612826784828486847702};
+  return {C[m], C[(8 - m) & 7] * (m == 0 ? 0.0 : 1.0)};
+}
+
+// LDS tables shared by the workgroup:
+//   T1[k0 * 64 + t] = zeta^t * w512^{t k0}      (512 entries)
+//   T2[k1 * 8 + t0] = w64^{t0 k1}               (64 entries, symmetric in (k1, t0))
 struct Fft512Tables {
-  const cplx* tw1;  // 512 entries
-  const cplx* tw2;  // 64 entries
+  const cplx* T1;
+  const cplx* T2;
 };
 
+__device__ __forceinline__ void build_fft512_tables(cplx* T1, cplx* T2, int tid, int nthreads) {
+  for (int e = tid; e < 512; e += nthreads) {
+    const int k0 = e >> 6, t = e & 63;
+    double s, c;
+    // angle / pi = t / 1024 - 2 t k0 / 512, reduced mod 2
+    const int num = (t - 4 * ((t * k0) & 511)) & 2047;  // in units of pi / 1024
+    sincospi((double)num / 1024.0, &s, &c);
+    T1[e] = {c, s};
+  }
+  for (int e = tid; e < 64; e += nthreads) {
+    const int k1 = e >> 3, t0 = e & 7;
+    double s, c;
+    sincospi(-2.0 * (double)((t0 * k1) & 63) / 64.0, &s, &c);
+    T2[e] = {c, s};
+  }
+}
+
+// Forward: v[m] = x[t + 64 m] (real-and-imaginary folded digits, untwisted).
 __device__ __forceinline__ void fft512_fwd(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane) {
   const int hi = lane >> 3, lo = lane & 7;
+#pragma unroll
+  for (int m = 1; m < 8; ++m) v[m] = cmul(v[m], psi_pow(m));
   dft8<false>(v);
 #pragma unroll
-  for (int k0 = 1; k0 < 8; ++k0) v[k0] = cmul(v[k0], T.tw1[k0 * 64 + lane]);
+  for (int k0 = 0; k0 < 8; ++k0) v[k0] = cmul(v[k0], T.T1[k0 * 64 + lane]);
   // transpose 1: writer lane (t1 = hi, t0 = lo) element k0 ; reader lane (k0 = hi, t0 = lo) element t1
 #pragma unroll
   for (int e = 0; e < 8; ++e) xch[xslot(e, hi, lo)] = v[e];
@@ -110,7 +151,7 @@ __device__ __forceinline__ void fft512_fwd(cplx (&v)[8], cplx* xch, const Fft512
   wave_lds_fence();
   dft8<false>(v);
 #pragma unroll
-  for (int k1 = 1; k1 < 8; ++k1) v[k1] = cmul(v[k1], T.tw2[k1 * 8 + lo]);
+  for (int k1 = 1; k1 < 8; ++k1) v[k1] = cmul(v[k1], T.T2[k1 * 8 + lo]);
   // transpose 2: writer lane (k0 = hi, t0 = lo) element k1 ; reader lane (k0 = hi, k1 = lo) element t0
 #pragma unroll
   for (int e = 0; e < 8; ++e) xch[xslot(hi, e, lo)] = v[e];
@@ -121,11 +162,13 @@ __device__ __forceinline__ void fft512_fwd(cplx (&v)[8], cplx* xch, const Fft512
   dft8<false>(v);
 }
 
+// Inverse: v[k2] = Y[k0 + 8 k1 + 64 k2] in lane (k0, k1) -> v[m] = sum_k Y_k w^{-jk} * conj(zeta^j),
+// j = t + 64 m in lane t.
 __device__ __forceinline__ void fft512_inv(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane) {
   const int hi = lane >> 3, lo = lane & 7;
   dft8<true>(v);  // over k2 -> t0 ; lane (k0 = hi, k1 = lo)
 #pragma unroll
-  for (int t0 = 1; t0 < 8; ++t0) v[t0] = cmulc(v[t0], T.tw2[lo * 8 + t0]);
+  for (int t0 = 1; t0 < 8; ++t0) v[t0] = cmulc(v[t0], T.T2[lo * 8 + t0]);
   // transpose 2': writer lane (k0, k1) element t0 ; reader lane (k0 = hi, t0 = lo) element k1
 #pragma unroll
   for (int e = 0; e < 8; ++e) xch[xslot(hi, lo, e)] = v[e];
@@ -135,7 +178,7 @@ __device__ __forceinline__ void fft512_inv(cplx (&v)[8], cplx* xch, const Fft512
   wave_lds_fence();
   dft8<true>(v);  // over k1 -> t1 ; lane (k0 = hi, t0 = lo)
 #pragma unroll
-  for (int t1 = 0; t1 < 8; ++t1) v[t1] = cmulc(v[t1], T.tw1[hi * 64 + 8 * t1 + lo]);
+  for (int t1 = 0; t1 < 8; ++t1) v[t1] = cmulc(v[t1], T.T1[hi * 64 + 8 * t1 + lo]);
   // transpose 1': writer lane (k0 = hi, t0 = lo) element t1 ; reader lane (t1 = hi, t0 = lo) element k0
 #pragma unroll
   for (int e = 0; e < 8; ++e) xch[xslot(hi, e, lo)] = v[e];
@@ -143,7 +186,9 @@ __device__ __forceinline__ void fft512_inv(cplx (&v)[8], cplx* xch, const Fft512
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = xch[xslot(e, hi, lo)];
   wave_lds_fence();
-  dft8<true>(v);  // over k0 -> m ; lane t holds z[t + 64 m]
+  dft8<true>(v);  // over k0 -> m ; lane t holds x[t + 64 m] * zeta^t ... times psi^m still to remove
+#pragma unroll
+  for (int m = 1; m < 8; ++m) v[m] = cmulc(v[m], psi_pow(m));
 }
 
 // Frequency index held in (lane, slot) after fft512_fwd.

@@ -6,13 +6,14 @@
 
 namespace chip {
 
-// N = 1024 kernel geometry: PBS1024_WAVES ciphertexts (one per wave) per workgroup sharing the
-// twiddle tables and a 2-slot ring of Fourier-key slices in LDS.
-constexpr int PBS1024_WAVES = 4;
-constexpr size_t PBS1024_TABLE_BYTES = (512 + 64 + 512) * 16;  // tw1, tw2, zeta
-constexpr size_t pbs1024_slice_bytes(int k, int level) { return (size_t)(k + 1) * level * 512 * 16; }
-constexpr size_t pbs1024_lds_bytes(int k, int level) {
-  return PBS1024_TABLE_BYTES + PBS1024_WAVES * 512 * 16 /* transpose scratch */ + 2 * pbs1024_slice_bytes(k, level);
+// N = 1024 kernel geometry: a workgroup of two waves per ciphertext (one GLWE polynomial and
+// one half of the frequency slots per wave).  LDS: the two pass-1/pass-2 twiddle tables and one
+// 9.2 KB transpose scratch per wave (which doubles as the half-spectrum mailbox).
+constexpr size_t PBS1024_TABLE_BYTES = (512 + 64) * 16;
+constexpr size_t PBS1024_XCH_SLOTS = 576;  // >= XCH_SLOTS (fft512.hpp), 16-B slots per wave
+constexpr size_t pbs1024_pair_lds_bytes(int level) {
+  (void)level;
+  return PBS1024_TABLE_BYTES + 2 * PBS1024_XCH_SLOTS * 16;
 }
 
 // Number of exact limbs of the key polynomial for a parameter set.

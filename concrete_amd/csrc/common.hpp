@@ -43,4 +43,15 @@ __device__ __forceinline__ int32_t decomp_next(uint64_t& state, int logB) {
   return (int32_t)(int64_t)(res - (carry << logB));
 }
 
+// same recurrence on a 32-bit state (valid when level * base_log <= 31)
+template <class U>
+__device__ __forceinline__ int32_t decomp_next_t(U& state, int logB) {
+  const U mask = ((U)1 << logB) - (U)1;
+  U res = state & mask;
+  state >>= logB;
+  U carry = (((res - (U)1) | state) & res) >> (logB - 1);
+  state += carry;
+  return (int32_t)res - (int32_t)(carry << logB);
+}
+
 }  // namespace chip

@@ -12,7 +12,8 @@
 // error is certified < 1/2, so rounding recovers the exact integers; the
 // limbs are recombined modulo 2^64.  Results are bit-identical to the schoolbook definition.
 //
-// Mapping (N = 1024, k = 1): a workgroup of two waves bootstraps one ciphertext.  Wave h
+// Mapping (N = 1024, k = 1): two waves per ciphertext, PBS_PAIRS ciphertexts per workgroup.
+// Wave h of a pair
 //   * owns GLWE polynomial h of the accumulator (16 u64 per lane: lane t holds t + 64 m),
 //   * computes the l forward transforms of its own polynomial's digits,
 //   * keeps frequency slots k2 in [4h, 4h + 4) of all (k+1) l digit spectra (the other half
@@ -20,8 +21,12 @@
 //   * runs the multiply-accumulate with the Fourier key on its half of the frequencies for
 //     both output polynomials, trades the partner's half, and runs the l inverse transforms
 //     of its own output polynomial.
-// So each wave needs < 256 VGPRs (two waves per SIMD) and the 630-step CMUX loop stays in one
-// launch; the two waves meet at 2l + 2 workgroup barriers per step.
+// Each wave stays < 256 VGPRs (two waves per SIMD).  The Fourier key is streamed through a
+// 3-group LDS ring (24 KB groups = three spectra of one (column, limb) slice) filled by
+// LDS-DMA (global_load_lds_dwordx4) and read by all PBS_PAIRS pairs, so it crosses the L2->CU
+// port once per workgroup instead of once per ciphertext.  The whole CMUX loop runs in one
+// launch with the workgroup in lockstep (one raw s_barrier per key group and per half-spectrum
+// exchange).
 #include <type_traits>
 
 #include "common.hpp"
@@ -58,48 +63,85 @@ __device__ __forceinline__ uint64_t stamp() {
   __builtin_amdgcn_sched_barrier(0);
   return t;
 }
-constexpr int NSTAMP = 8;  // rot+decomp, fwd+xchg, mac, y-xchg, inv+recomb, -, total, steps
+constexpr int NSTAMP = 8;  // rot+decomp, fwd+xchg, mac+vmcnt, y-xchg, inv+recomb, ring barrier, total, steps
 
-template <int L, bool RESID, bool STAMPS>
-__global__ void __launch_bounds__(128, 2)
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <int N_WAIT>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N_WAIT >= 0 && N_WAIT < 64, "vmcnt range");
+  // gfx9 encoding: vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt_hi[15:14]
+  __builtin_amdgcn_s_waitcnt((N_WAIT & 15) | (7 << 4) | (15 << 8) | ((N_WAIT >> 4) << 14));
+}
+
+template <int L, bool RESID, bool STAMPS, bool STATE32>
+__global__ void __launch_bounds__(PBS_PAIRS * 128, 2)
 pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx,
                     const uint64_t* __restrict__ luts, const uint64_t* __restrict__ lut_idx,
                     const uint64_t* __restrict__ in, const uint64_t* __restrict__ in_idx,
-                    const cplx* __restrict__ fbsk, uint32_t n, uint32_t base_log,
+                    const cplx* __restrict__ fbsk, uint32_t n, uint32_t base_log, uint32_t num_samples,
                     unsigned long long* __restrict__ resid_out) {
   constexpr int K = 1, K1 = 2, N = 1024, LOG2_2N = 11, LIMBS = 3, RQ = K1 * L;
   constexpr int SLICE = RQ * 512;            // complex values per (column, limb) key slice
   constexpr int PER_I = K1 * LIMBS * SLICE;  // complex values per Fourier GGSW
   static_assert(XCH_SLOTS <= (int)PBS1024_XCH_SLOTS, "transpose scratch");
+  constexpr int NW = 2 * PBS_PAIRS;           // waves per workgroup
+  constexpr int GROUP = L * 512;              // complex values per ring group (one row of a slice)
+  constexpr int NGRP = K1 * K1 * LIMBS;       // ring groups per CMUX step
+  constexpr int GLDS = GROUP / 64 / NW;       // 1 KB LDS-DMA pieces per wave per group
+  static_assert(GROUP % (64 * NW) == 0, "group split");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cplx* T1 = reinterpret_cast<cplx*>(smem);
   cplx* T2 = T1 + 512;
-  cplx* xch_all = T2 + 64;  // 2 x PBS1024_XCH_SLOTS: per-wave transpose scratch, also the mailbox
+  cplx* xch_all = T2 + 64;                       // NW x PBS1024_XCH_SLOTS: transpose scratch,
+  cplx* ring = xch_all + NW * PBS1024_XCH_SLOTS;  // also the mailbox; 3 x GROUP key ring
 
-  const int h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave = polynomial = half
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = w & 1;  // polynomial = frequency half
   const int lane = threadIdx.x & 63;
-  const uint32_t s = blockIdx.x;
-  cplx* xch = xch_all + h * PBS1024_XCH_SLOTS;
+  const uint32_t s = blockIdx.x * PBS_PAIRS + (w >> 1);
+  const bool active = s < num_samples;
+  cplx* xch = xch_all + w * PBS1024_XCH_SLOTS;
   uint64_t* xch64 = reinterpret_cast<uint64_t*>(xch);
   cplx* mybox = xch;                                  // the half-spectrum mailbox is the
-  const cplx* partnerbox = xch_all + (1 - h) * PBS1024_XCH_SLOTS;   // transpose scratch, between transforms
+  const cplx* partnerbox = xch_all + (w ^ 1) * PBS1024_XCH_SLOTS;   // transpose scratch, between transforms
 
-  build_fft512_tables(T1, T2, threadIdx.x, 128);
+  // ---- key ring: group g = (step g / NGRP, slice (g % NGRP) / 2, row g % 2) -> slot g % 3 ----
+  // slice order (c, li) = (0,0), (1,0), (0,1), (1,1), ... : both waves of a pair read the same
+  // slice at the same time (their own halves of its frequency slots)
+  const uint64_t total_groups = (uint64_t)n * NGRP;
+  auto issue_group = [&](uint64_t g) {
+    const uint64_t i = g / NGRP;
+    const int r = (int)(g % NGRP);
+    const int sl = r >> 1, row = r & 1;
+    const int c = sl % K1, li = sl / K1;
+    const cplx* src = fbsk + i * (uint64_t)PER_I + (c * LIMBS + li) * SLICE + row * GROUP;
+    cplx* dst = ring + (int)(g % 3) * GROUP;
+#pragma unroll
+    for (int j = 0; j < GLDS; ++j) {
+      const int piece = w * GLDS + j;
+      __builtin_amdgcn_global_load_lds(src + piece * 64 + lane, (lds_ptr_t)(dst + piece * 64), 16, 0, 0);
+    }
+  };
+  issue_group(0);
+  if (total_groups > 1) issue_group(1);
+
+  build_fft512_tables(T1, T2, threadIdx.x, PBS_PAIRS * 128);
   __syncthreads();
   const Fft512Tables T{T1, T2};
 
-  const uint64_t* lwe = in + (in_idx ? in_idx[s] : s) * (uint64_t)(n + 1);
-  const uint64_t* lut = luts + (lut_idx ? lut_idx[s] : 0ull) * (uint64_t)(K1 * N);
+  const uint64_t* lwe = in + (active ? (in_idx ? in_idx[s] : s) : 0) * (uint64_t)(n + 1);
+  const uint64_t* lut = luts + (active && lut_idx ? lut_idx[s] : 0ull) * (uint64_t)(K1 * N);
 
   // acc_h = LUT_h * X^{-ms(b)}  (blind_rotate_assign: polynomial_wrapping_monic_monomial_div)
   uint64_t A[16];
   {
-    const uint32_t bt = modswitch(lwe[n], LOG2_2N);
+    const uint32_t bt = active ? modswitch(lwe[n], LOG2_2N) : 0u;
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       const uint32_t src = (uint32_t)(lane + 64 * m + bt) & (2 * N - 1);
-      const uint64_t v = lut[h * N + (src & (N - 1))];
+      const uint64_t v = active ? lut[h * N + (src & (N - 1))] : 0ull;
       A[m] = src < N ? v : 0ull - v;
     }
   }
@@ -111,31 +153,36 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   uint64_t t_begin = 0, tp = 0;
   if constexpr (STAMPS) t_begin = stamp();
 
-  uint64_t a_next = lwe[0];
+  uint64_t a_next = active ? lwe[0] : 0ull;
   for (uint32_t i = 0; i < n; ++i) {
     const uint64_t ai = a_next;
-    if (i + 1 < n) a_next = lwe[i + 1];
+    if (i + 1 < n) a_next = active ? lwe[i + 1] : 0ull;
     const uint32_t at = modswitch(ai, LOG2_2N);
     // tfhe skips a zero mask element; at == 0 gives X^0 acc - acc = 0 whose product is 0.
-    // The condition depends only on the ciphertext: uniform across the pair.
-    if (ai == 0ull || at == 0u) continue;
+    // The condition depends only on the ciphertext (uniform across the pair); a skipping pair
+    // still takes part in every workgroup barrier and key-ring refill.
+    const bool work = ai != 0ull && at != 0u;
     if constexpr (STAMPS) {
       tp = stamp();
-      acc_t[7] += 1;
+      acc_t[7] += work;
     }
 
     // ---- own polynomial: ct1 = acc * X^{at} - acc, decomposer state per coefficient ------
-    uint64_t st[16];
+    // decomposer state < 2^(l * logB): 32-bit when l * logB <= 31 (cfg2: 21 bits)
+    using state_t = typename std::conditional<STATE32, uint32_t, uint64_t>::type;
+    state_t st[16];
+    if (work) {
 #pragma unroll
-    for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = A[m];
-    wave_lds_fence();
+      for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = A[m];
+      wave_lds_fence();
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      const uint32_t src = (uint32_t)(lane + 64 * m - (int)at) & (2 * N - 1);
-      const uint64_t rv = xch64[src & (N - 1)];
-      st[m] = decomp_init((src < N ? rv : 0ull - rv) - A[m], nrep);
+      for (int m = 0; m < 16; ++m) {
+        const uint32_t src = (uint32_t)(lane + 64 * m - (int)at) & (2 * N - 1);
+        const uint64_t rv = xch64[src & (N - 1)];
+        st[m] = (state_t)decomp_init((src < N ? rv : 0ull - rv) - A[m], nrep);
+      }
+      wave_lds_fence();
     }
-    wave_lds_fence();
     if constexpr (STAMPS) {
       uint64_t t = stamp();
       acc_t[0] += t - tp;
@@ -147,34 +194,38 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     cplx X[K1][L][4];
 #pragma unroll
     for (int q = 0; q < L; ++q) {
-      cplx v[8];
-      // digits of level l - q (the decomposition iterator yields the least significant first)
-      int32_t d[16];
+      if (work) {
+        // digits of level l - q (the decomposition iterator yields the least significant first)
+        int32_t d[16];
 #pragma unroll
-      for (int m = 0; m < 16; ++m) d[m] = decomp_next(st[m], logB);
+        for (int m = 0; m < 16; ++m) d[m] = decomp_next_t(st[m], logB);
+        cplx v[8];
 #pragma unroll
-      for (int m = 0; m < 8; ++m) v[m] = {(double)d[m], (double)d[m + 8]};
-      fft512_fwd(v, xch, T, lane);
-      if (h == 0) {
+        for (int m = 0; m < 8; ++m) v[m] = {(double)d[m], (double)d[m + 8]};
+        fft512_fwd(v, xch, T, lane);
+        if (h == 0) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          X[0][q][j] = v[j];
-          mybox[j * 64 + lane] = v[4 + j];
-        }
-      } else {
+          for (int j = 0; j < 4; ++j) {
+            X[0][q][j] = v[j];
+            mybox[j * 64 + lane] = v[4 + j];
+          }
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          X[1][q][j] = v[4 + j];
-          mybox[j * 64 + lane] = v[j];
+          for (int j = 0; j < 4; ++j) {
+            X[1][q][j] = v[4 + j];
+            mybox[j * 64 + lane] = v[j];
+          }
         }
       }
       pair_barrier();
-      if (h == 0) {
+      if (work) {
+        if (h == 0) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) X[1][q][j] = partnerbox[j * 64 + lane];
-      } else {
+          for (int j = 0; j < 4; ++j) X[1][q][j] = partnerbox[j * 64 + lane];
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) X[0][q][j] = partnerbox[j * 64 + lane];
+          for (int j = 0; j < 4; ++j) X[0][q][j] = partnerbox[j * 64 + lane];
+        }
       }
       pair_barrier();  // partner has read my mailbox: my scratch is free again
     }
@@ -184,50 +235,57 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
       tp = t;
     }
 
-    // ---- per limb: MAC for both output polynomials on my half, trade halves, inverse ----
-    const cplx* Gi = fbsk + (uint64_t)i * PER_I + (4 * h) * 64 + lane;
+    // ---- per limb: MAC for both output polynomials on my half (key from the LDS ring),
+    //      trade halves through the mailbox, inverse transform of my polynomial -------------
     static_for<0, LIMBS>([&](auto LI) {
       constexpr int li = decltype(LI)::value;
       cplx Ymine[4];
 #pragma unroll
-      for (int cc = 0; cc < K1; ++cc) {
-        // the partner's polynomial first (its half goes to the mailbox), then mine
-        const int c = cc == 0 ? 1 - h : h;
-        const cplx* G = Gi + (c * LIMBS + li) * SLICE;
+      for (int c = 0; c < K1; ++c) {
         cplx Y[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) Y[j] = {0.0, 0.0};
-        // rolling prefetch: key slots of spectrum rq + PF are in flight while rq is consumed
-        constexpr int PF = 2;
-        cplx gq[PF + 1][4];
 #pragma unroll
-        for (int p = 0; p < PF; ++p)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) gq[p][j] = G[(p * 8 + j) * 64];
-        static_for<0, RQ>([&](auto RQI) {
-          constexpr int rq = decltype(RQI)::value;
-          if constexpr (rq + PF < RQ) {
-            // an opaque copy of the pointer pins these loads here (no hoisting of the whole slice)
-            const cplx* Gl = G;
-            asm volatile("" : "+v"(Gl));
-#pragma unroll
-            for (int j = 0; j < 4; ++j) gq[(rq + PF) % (PF + 1)][j] = Gl[((rq + PF) * 8 + j) * 64];
+        for (int row = 0; row < K1; ++row) {
+          const uint64_t g = (uint64_t)i * NGRP + (li * K1 + c) * K1 + row;
+          // group g landed for this wave's pieces (group g + 1 may stay in flight) ...
+          if (g + 1 < total_groups) wait_vmcnt<GLDS>();
+          else wait_vmcnt<0>();
+          if constexpr (STAMPS) {
+            uint64_t t = stamp();
+            acc_t[2] += t - tp;
+            tp = t;
           }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const cplx gv = gq[rq % (PF + 1)][j];
-            const cplx x = X[rq / L][rq % L][j];
-            Y[j].re = __builtin_fma(x.re, gv.re, __builtin_fma(-x.im, gv.im, Y[j].re));
-            Y[j].im = __builtin_fma(x.re, gv.im, __builtin_fma(x.im, gv.re, Y[j].im));
+          // ... and for every wave's pieces; everyone is also done with group g - 1
+          pair_barrier();
+          if constexpr (STAMPS) {
+            uint64_t t = stamp();
+            acc_t[5] += t - tp;
+            tp = t;
           }
-          __builtin_amdgcn_sched_barrier(0);
-        });
-        if (cc == 0) {
+          // refill the slot of group g - 1 with group g + 2
+          if (g + 2 < total_groups) issue_group(g + 2);
+          if (work) {
+            const cplx* G = ring + (int)(g % 3) * GROUP + (4 * h) * 64 + lane;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) mybox[j * 64 + lane] = Y[j];
-        } else {
+            for (int q = 0; q < L; ++q)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) Ymine[j] = Y[j];
+              for (int j = 0; j < 4; ++j) {
+                const cplx gv = G[(q * 8 + j) * 64];
+                const cplx x = X[row][q][j];
+                Y[j].re = __builtin_fma(x.re, gv.re, __builtin_fma(-x.im, gv.im, Y[j].re));
+                Y[j].im = __builtin_fma(x.re, gv.im, __builtin_fma(x.im, gv.re, Y[j].im));
+              }
+          }
+        }
+        if (work) {
+          if (c == h) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) Ymine[j] = Y[j];
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) mybox[j * 64 + lane] = Y[j];
+          }
         }
       }
       if constexpr (STAMPS) {
@@ -237,17 +295,19 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
       }
       pair_barrier();
       cplx v[8];
-      if (h == 0) {
+      if (work) {
+        if (h == 0) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          v[j] = Ymine[j];
-          v[4 + j] = partnerbox[j * 64 + lane];
-        }
-      } else {
+          for (int j = 0; j < 4; ++j) {
+            v[j] = Ymine[j];
+            v[4 + j] = partnerbox[j * 64 + lane];
+          }
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          v[j] = partnerbox[j * 64 + lane];
-          v[4 + j] = Ymine[j];
+          for (int j = 0; j < 4; ++j) {
+            v[j] = partnerbox[j * 64 + lane];
+            v[4 + j] = Ymine[j];
+          }
         }
       }
       pair_barrier();
@@ -256,22 +316,24 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         acc_t[3] += t - tp;
         tp = t;
       }
-      fft512_inv(v, xch, T, lane);
+      if (work) {
+        fft512_inv(v, xch, T, lane);
 #pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const double tr = v[m].re + RND_MAGIC, ti = v[m].im + RND_MAGIC;
-        if constexpr (RESID) {
-          max_resid = fmax(max_resid, fabs(v[m].re - (tr - RND_MAGIC)));
-          max_resid = fmax(max_resid, fabs(v[m].im - (ti - RND_MAGIC)));
-        }
-        // bits(t) = MAGIC_BITS + round(v): the constant of all limbs is removed with limb 0
-        // (it must not survive into the next step's rotation: X^a * const != const)
-        if constexpr (li == 0) {
-          A[m] += (uint64_t)__double_as_longlong(tr) - MAGIC_ALL;
-          A[m + 8] += (uint64_t)__double_as_longlong(ti) - MAGIC_ALL;
-        } else {
-          A[m] += (uint64_t)__double_as_longlong(tr) << limb_shift(li);
-          A[m + 8] += (uint64_t)__double_as_longlong(ti) << limb_shift(li);
+        for (int m = 0; m < 8; ++m) {
+          const double tr = v[m].re + RND_MAGIC, ti = v[m].im + RND_MAGIC;
+          if constexpr (RESID) {
+            max_resid = fmax(max_resid, fabs(v[m].re - (tr - RND_MAGIC)));
+            max_resid = fmax(max_resid, fabs(v[m].im - (ti - RND_MAGIC)));
+          }
+          // bits(t) = MAGIC_BITS + round(v): the constant of all limbs is removed with limb 0
+          // (it must not survive into the next step's rotation: X^a * const != const)
+          if constexpr (li == 0) {
+            A[m] += (uint64_t)__double_as_longlong(tr) - MAGIC_ALL;
+            A[m + 8] += (uint64_t)__double_as_longlong(ti) - MAGIC_ALL;
+          } else {
+            A[m] += (uint64_t)__double_as_longlong(tr) << limb_shift(li);
+            A[m + 8] += (uint64_t)__double_as_longlong(ti) << limb_shift(li);
+          }
         }
       }
       if constexpr (STAMPS) {
@@ -285,14 +347,15 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   if constexpr (STAMPS) {
     acc_t[6] = stamp() - t_begin;
     if (lane == 0 && resid_out) {
-      unsigned long long* dst = resid_out + ((uint64_t)blockIdx.x * 2 + h) * NSTAMP;
+      unsigned long long* dst = resid_out + ((uint64_t)blockIdx.x * NW + w) * NSTAMP;
       for (int q = 0; q < NSTAMP; ++q) dst[q] = acc_t[q];
     }
   }
 
   // ---- sample extract (nth = 0): out[j] = -A_0[N - j] (j > 0), A_0[0]; body B[0] -------
-  uint64_t* o = out + (out_idx ? out_idx[s] : s) * (uint64_t)(K * N + 1);
-  if (h == 0) {
+  uint64_t* o = out + (active ? (out_idx ? out_idx[s] : s) : 0) * (uint64_t)(K * N + 1);
+  if (!active) {
+  } else if (h == 0) {
 #pragma unroll
     for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = A[m];
     wave_lds_fence();
@@ -308,7 +371,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 
   if constexpr (RESID && !STAMPS) {
     for (int off = 32; off > 0; off >>= 1) max_resid = fmax(max_resid, __shfl_xor(max_resid, off));
-    if (lane == 0 && resid_out) atomicMax(resid_out, (unsigned long long)__double_as_longlong(max_resid));
+    if (lane == 0 && active && resid_out) atomicMax(resid_out, (unsigned long long)__double_as_longlong(max_resid));
   }
 }
 
@@ -318,10 +381,12 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 template <int L, bool RESID, bool STAMPS>
 static int launch_pair_t(const PbsArgs& a) {
   const size_t lds = pbs1024_pair_lds_bytes(L);
-  auto kern = pbs1024_pair_kernel<L, RESID, STAMPS>;
+  auto kern = L * a.base_log <= 31 ? pbs1024_pair_kernel<L, RESID, STAMPS, true>
+                                   : pbs1024_pair_kernel<L, RESID, STAMPS, false>;
   CHIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(kern, dim3(a.num_samples), dim3(128), lds, a.stream, a.out, a.out_idx, a.luts, a.lut_idx, a.in,
-                     a.in_idx, reinterpret_cast<const cplx*>(a.fbsk), a.n, a.base_log, a.resid);
+  const uint32_t blocks = (a.num_samples + PBS_PAIRS - 1) / PBS_PAIRS;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(PBS_PAIRS * 128), lds, a.stream, a.out, a.out_idx, a.luts, a.lut_idx,
+                     a.in, a.in_idx, reinterpret_cast<const cplx*>(a.fbsk), a.n, a.base_log, a.num_samples, a.resid);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("pbs launch failed: %s", hipGetErrorString(e));
@@ -334,7 +399,7 @@ template <int L>
 static int launch_pair(const PbsArgs& a) {
   if (a.num_samples == 0) return 0;
   // diagnostic: CONCRETE_HIP_PBS_STAMPS=1 runs the s_memtime-instrumented build; `resid` must then
-  // point at 2 * num_samples * 8 u64 (per-wave cycle sums per phase)
+  // point at 2 * PBS_PAIRS * ceil(num_samples / PBS_PAIRS) * 8 u64 (per-wave cycle sums per phase)
   static const bool stamps = getenv("CONCRETE_HIP_PBS_STAMPS") && atoi(getenv("CONCRETE_HIP_PBS_STAMPS"));
   if (stamps) return launch_pair_t<L, true, true>(a);
   return a.resid ? launch_pair_t<L, true, false>(a) : launch_pair_t<L, false, false>(a);

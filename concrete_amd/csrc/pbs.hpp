@@ -10,10 +10,10 @@ namespace chip {
 // one half of the frequency slots per wave).  LDS: the two pass-1/pass-2 twiddle tables and one
 // 9.2 KB transpose scratch per wave (which doubles as the half-spectrum mailbox).
 constexpr size_t PBS1024_TABLE_BYTES = (512 + 64) * 16;
+constexpr int PBS_PAIRS = 4;                // ciphertexts (wave pairs) per workgroup
 constexpr size_t PBS1024_XCH_SLOTS = 576;  // >= XCH_SLOTS (fft512.hpp), 16-B slots per wave
 constexpr size_t pbs1024_pair_lds_bytes(int level) {
-  (void)level;
-  return PBS1024_TABLE_BYTES + 2 * PBS1024_XCH_SLOTS * 16;
+  return PBS1024_TABLE_BYTES + 2 * PBS_PAIRS * PBS1024_XCH_SLOTS * 16 + 3 * (size_t)level * 512 * 16;
 }
 
 // Number of exact limbs of the key polynomial for a parameter set.

@@ -26,13 +26,39 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "PBS/sec (whole node) at N=1024 batch=4096; achieved HBM GB/s"
 
 
+KERNEL_SOURCES = ("concrete_amd/csrc/pbs.hip", "concrete_amd/csrc/pbs.hpp", "concrete_amd/csrc/fft512.hpp",
+                  "concrete_amd/csrc/common.hpp")
+
+
+def kernel_source_hash() -> str:
+    import hashlib
+    h = hashlib.sha1()
+    for f in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(batch: int):
+    """Per-launch HBM bytes from the committed PMC record (tools/pmc_traffic.py) when it was
+    measured on these kernel sources at this batch; else None."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pbs_traffic.json")), reverse=True):
+        with open(f) as fh:
+            rec = json.load(fh)
+        if rec.get("source_hash") == kernel_source_hash() and rec.get("batch") == batch:
+            return rec["traffic_bytes"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=4096, help="PBS per GPU per step")
-    ap.add_argument("--cpu-sample", type=int, default=96, help="PBS in the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=4096,
+                    help="PBS in the bounded CPU-baseline sample (default: one full 4096 batch, ~10-15 s)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", type=int, default=8, help="rows checked bit-exactly against the oracle (rank 0)")
@@ -45,6 +71,7 @@ def main():
     import torch.distributed as dist
 
     from concrete_amd import backend as B
+    from concrete_amd import dist as D
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -75,7 +102,7 @@ def main():
     if world > 1:
         dist.barrier()
         t0 = time.perf_counter()
-        dist.broadcast(fbsk, src=0)
+        D.broadcast_key(fbsk, src=0)
         torch.cuda.synchronize()
         t_bcast = time.perf_counter() - t0
 
@@ -116,6 +143,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall, kern_ms = float(t[0]), float(t[1])
 
+    # ---- final gather of the output rows onto rank 0 (outside the timed PBS region)
+    t_gather = 0.0
+    if world > 1:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        full = D.gather_rows(d_out, args.batch * world, dst=0)
+        torch.cuda.synchronize()
+        t_gather = time.perf_counter() - t0
+        del full
+
     # ---- correctness of what was timed: decrypt-level on every row, bit-exact sample (rank 0)
     out = B.to_host(d_out)
     dec = B.lwe_decrypt(glwe_sk, out, p.big_n)
@@ -134,6 +171,7 @@ def main():
         achieved = bytes_per_pbs * args.batch / (kern_ms * 1e-3) / 1e9
         bitexact = None
         cpu = None
+        traffic, traffic_src = pmc_traffic(args.batch)
         if args.verify or not args.no_cpu_baseline:
             from oracle import pyoracle as O  # checker / CPU baseline only
             op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
@@ -167,10 +205,10 @@ def main():
             "data": "synthetic (seeded keygen + fresh LWE encryptions of random 3-bit messages)",
             "config": {"workload": "batched PBS cfg2: N=1024 k=1 n=630 l=3 logB=7",
                        "batch_per_gpu": args.batch, "global_batch": args.batch * world,
-                       "parallelism": f"shard{world}", "key_bcast_s": round(t_bcast, 4),
+                       "parallelism": f"shard{world}", "key_bcast_s": round(t_bcast, 4), "gather_s": round(t_gather, 4),
                        "key_convert_s": round(t_key, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_src": traffic_src,
                          "kernel_ms": round(kern_ms, 3), "bytes_per_pbs": bytes_per_pbs},
             "cpu_baseline": cpu,
             "checks": {"decrypt_ok": f"{ok_all}/{args.batch * world}", "bitexact_rows": args.verify,

@@ -1,7 +1,9 @@
 #!/bin/bash
-# PMC passes over one bench step (run on the GPU box from the repo root).  Usage: tools/pmc.sh TAG
+# PMC passes over one bench step (run on the GPU box from the repo root).
+# Usage: tools/pmc.sh TAG [PASSES]   PASSES = subset of "abcde" (default all; "de" = HBM traffic only)
 set -e
 TAG=${1:-pmc}
+PASSES=${2:-abcde}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp
@@ -11,9 +13,9 @@ run() {  # name counters...
   timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o run -- \
     python $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline --verify 0 > $OUT/$name.log 2>&1
 }
-run a SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS
-run b SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 SQ_INSTS_LDS SQ_INSTS_SALU
-run c SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_CVT SQ_LDS_ADDR_CONFLICT
-run d FETCH_SIZE
-run e WRITE_SIZE TCC_HIT TCC_MISS
+[[ $PASSES == *a* ]] && run a SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS
+[[ $PASSES == *b* ]] && run b SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 SQ_INSTS_LDS SQ_INSTS_SALU
+[[ $PASSES == *c* ]] && run c SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_CVT SQ_LDS_ADDR_CONFLICT
+[[ $PASSES == *d* ]] && run d FETCH_SIZE
+[[ $PASSES == *e* ]] && run e WRITE_SIZE TCC_HIT TCC_MISS
 echo pmc done

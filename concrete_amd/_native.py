@@ -10,7 +10,8 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libconcrete_hip.so")
+# CONCRETE_HIP_LIB: alternative build of the same ABI (kernel experiments, tools/variant.sh)
+LIB_PATH = os.environ.get("CONCRETE_HIP_LIB") or os.path.join(_HERE, "libconcrete_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "concrete_hip.h")
 
 u32, u64, i32, vp, dbl = C.c_uint32, C.c_uint64, C.c_int, C.c_void_p, C.c_double

@@ -135,60 +135,136 @@ __device__ __forceinline__ void build_fft512_tables(cplx* T1, cplx* T2, int tid,
 }
 
 // Forward: v[m] = x[t + 64 m] (real-and-imaginary folded digits, untwisted).
-__device__ __forceinline__ void fft512_fwd(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane) {
-  const int hi = lane >> 3, lo = lane & 7;
+// Stages: P1 (twist, pass 1, twiddles) | W1 R1 (transpose 1) | P2 (pass 2, twiddles) | W2 R2 | P3.
+__device__ __forceinline__ void fwd_p1(cplx (&v)[8], const Fft512Tables& T, int lane) {
 #pragma unroll
   for (int m = 1; m < 8; ++m) v[m] = cmul(v[m], psi_pow(m));
   dft8<false>(v);
 #pragma unroll
   for (int k0 = 0; k0 < 8; ++k0) v[k0] = cmul(v[k0], T.T1[k0 * 64 + lane]);
-  // transpose 1: writer lane (t1 = hi, t0 = lo) element k0 ; reader lane (k0 = hi, t0 = lo) element t1
+}
+// transpose 1: writer lane (t1 = hi, t0 = lo) element k0 ; reader lane (k0 = hi, t0 = lo) element t1
+__device__ __forceinline__ void fwd_w1(const cplx (&v)[8], cplx* xch, int hi, int lo) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) xch[xslot(e, hi, lo)] = v[e];
-  wave_lds_fence();
+}
+__device__ __forceinline__ void fwd_r1(cplx (&v)[8], const cplx* xch, int hi, int lo) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = xch[xslot(hi, e, lo)];
-  wave_lds_fence();
+}
+__device__ __forceinline__ void fwd_p2(cplx (&v)[8], const Fft512Tables& T, int lo) {
   dft8<false>(v);
 #pragma unroll
   for (int k1 = 1; k1 < 8; ++k1) v[k1] = cmul(v[k1], T.T2[k1 * 8 + lo]);
-  // transpose 2: writer lane (k0 = hi, t0 = lo) element k1 ; reader lane (k0 = hi, k1 = lo) element t0
+}
+// transpose 2: writer lane (k0 = hi, t0 = lo) element k1 ; reader lane (k0 = hi, k1 = lo) element t0
+__device__ __forceinline__ void fwd_w2(const cplx (&v)[8], cplx* xch, int hi, int lo) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) xch[xslot(hi, e, lo)] = v[e];
-  wave_lds_fence();
+}
+__device__ __forceinline__ void fwd_r2(cplx (&v)[8], const cplx* xch, int hi, int lo) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = xch[xslot(hi, lo, e)];
+}
+
+__device__ __forceinline__ void fft512_fwd(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane) {
+  const int hi = lane >> 3, lo = lane & 7;
+  fwd_p1(v, T, lane);
+  fwd_w1(v, xch, hi, lo);
+  wave_lds_fence();
+  fwd_r1(v, xch, hi, lo);
+  wave_lds_fence();
+  fwd_p2(v, T, lo);
+  fwd_w2(v, xch, hi, lo);
+  wave_lds_fence();
+  fwd_r2(v, xch, hi, lo);
   wave_lds_fence();
   dft8<false>(v);
 }
 
-// Inverse: v[k2] = Y[k0 + 8 k1 + 64 k2] in lane (k0, k1) -> v[m] = sum_k Y_k w^{-jk} * conj(zeta^j),
-// j = t + 64 m in lane t.
-__device__ __forceinline__ void fft512_inv(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane) {
+// Two independent forward transforms through ONE scratch, software-pipelined: each
+// transpose's LDS round trip is covered by the other transform's butterflies.  LDS operations
+// of a wave execute in issue order, so b's writes cannot overtake a's earlier reads.
+__device__ __forceinline__ void fft512_fwd2(cplx (&a)[8], cplx (&b)[8], cplx* xch, const Fft512Tables& T,
+                                            int lane) {
   const int hi = lane >> 3, lo = lane & 7;
+  fwd_p1(a, T, lane);
+  fwd_w1(a, xch, hi, lo);
+  wave_lds_fence();
+  fwd_r1(a, xch, hi, lo);
+  wave_lds_fence();
+  fwd_p1(b, T, lane);
+  wave_lds_fence();
+  fwd_w1(b, xch, hi, lo);
+  wave_lds_fence();
+  fwd_r1(b, xch, hi, lo);
+  wave_lds_fence();
+  fwd_p2(a, T, lo);
+  wave_lds_fence();
+  fwd_w2(a, xch, hi, lo);
+  wave_lds_fence();
+  fwd_r2(a, xch, hi, lo);
+  wave_lds_fence();
+  fwd_p2(b, T, lo);
+  wave_lds_fence();
+  fwd_w2(b, xch, hi, lo);
+  wave_lds_fence();
+  fwd_r2(b, xch, hi, lo);
+  wave_lds_fence();
+  dft8<false>(a);
+  dft8<false>(b);
+}
+
+// Inverse: v[k2] = Y[k0 + 8 k1 + 64 k2] in lane (k0, k1) -> v[m] = sum_k Y_k w^{-jk} * conj(zeta^j),
+// j = t + 64 m in lane t.  Stages: P1 | W1 R1 | P2 | W2 R2 | P3 (the kernel interleaves them
+// with other work, so each is callable on its own).
+__device__ __forceinline__ void inv_p1(cplx (&v)[8], const Fft512Tables& T, int lo) {
   dft8<true>(v);  // over k2 -> t0 ; lane (k0 = hi, k1 = lo)
 #pragma unroll
   for (int t0 = 1; t0 < 8; ++t0) v[t0] = cmulc(v[t0], T.T2[lo * 8 + t0]);
-  // transpose 2': writer lane (k0, k1) element t0 ; reader lane (k0 = hi, t0 = lo) element k1
+}
+// transpose 2': writer lane (k0, k1) element t0 ; reader lane (k0 = hi, t0 = lo) element k1
+__device__ __forceinline__ void inv_w1(const cplx (&v)[8], cplx* xch, int hi, int lo) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) xch[xslot(hi, lo, e)] = v[e];
-  wave_lds_fence();
+}
+__device__ __forceinline__ void inv_r1(cplx (&v)[8], const cplx* xch, int hi, int lo) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = xch[xslot(hi, e, lo)];
-  wave_lds_fence();
+}
+__device__ __forceinline__ void inv_p2(cplx (&v)[8], const Fft512Tables& T, int hi, int lo) {
   dft8<true>(v);  // over k1 -> t1 ; lane (k0 = hi, t0 = lo)
 #pragma unroll
   for (int t1 = 0; t1 < 8; ++t1) v[t1] = cmulc(v[t1], T.T1[hi * 64 + 8 * t1 + lo]);
-  // transpose 1': writer lane (k0 = hi, t0 = lo) element t1 ; reader lane (t1 = hi, t0 = lo) element k0
+}
+// transpose 1': writer lane (k0 = hi, t0 = lo) element t1 ; reader lane (t1 = hi, t0 = lo) element k0
+__device__ __forceinline__ void inv_w2(const cplx (&v)[8], cplx* xch, int hi, int lo) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) xch[xslot(hi, e, lo)] = v[e];
-  wave_lds_fence();
+}
+__device__ __forceinline__ void inv_r2(cplx (&v)[8], const cplx* xch, int hi, int lo) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = xch[xslot(e, hi, lo)];
-  wave_lds_fence();
+}
+__device__ __forceinline__ void inv_p3(cplx (&v)[8]) {
   dft8<true>(v);  // over k0 -> m ; lane t holds x[t + 64 m] * zeta^t ... times psi^m still to remove
 #pragma unroll
   for (int m = 1; m < 8; ++m) v[m] = cmulc(v[m], psi_pow(m));
+}
+
+__device__ __forceinline__ void fft512_inv(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane) {
+  const int hi = lane >> 3, lo = lane & 7;
+  inv_p1(v, T, lo);
+  inv_w1(v, xch, hi, lo);
+  wave_lds_fence();
+  inv_r1(v, xch, hi, lo);
+  wave_lds_fence();
+  inv_p2(v, T, hi, lo);
+  inv_w2(v, xch, hi, lo);
+  wave_lds_fence();
+  inv_r2(v, xch, hi, lo);
+  wave_lds_fence();
+  inv_p3(v);
 }
 
 // Frequency index held in (lane, slot) after fft512_fwd.

@@ -55,6 +55,20 @@ constexpr int limb_shift(int li) { return li * 21 + (li > 0 ? 1 : 0); }
 // no vmcnt drain (key loads may stay in flight).
 __device__ __forceinline__ void pair_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+#ifndef DIAG_NOMAC
+#define DIAG_NOMAC 0  // diagnostic builds only: skip the key MAC (wrong results)
+#endif
+#ifndef FWD_BATCH
+#define FWD_BATCH 1  // forward transforms software-pipelined together (1 or 2; 2 spills at l = 3)
+#endif
+
+// Barrier of the half-spectrum exchanges (DIAG_NOXBAR: timing-only builds without it)
+#ifdef DIAG_NOXBAR
+__device__ __forceinline__ void xchg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+#else
+__device__ __forceinline__ void xchg_barrier() { pair_barrier(); }
+#endif
+
 // Diagnostic cycle stamps (STAMPS builds only; never in the product kernel).
 __device__ __forceinline__ uint64_t stamp() {
   uint64_t t;
@@ -190,44 +204,59 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     }
 
     // ---- forward transforms; keep my half of the slots, mail the other half -------------
-    // X[row][q][j]: digit spectrum (row, level q) at slot k2 = 4h + j
+    // X[row][q][j]: digit spectrum (row, level q) at slot k2 = 4h + j.  Levels are transformed
+    // two at a time (software-pipelined through the one scratch), then both halves traded.
     cplx X[K1][L][4];
 #pragma unroll
-    for (int q = 0; q < L; ++q) {
+    for (int q0 = 0; q0 < L; q0 += FWD_BATCH) {
+      const int NQ = (q0 + 1 < L) ? FWD_BATCH : 1;
       if (work) {
         // digits of level l - q (the decomposition iterator yields the least significant first)
-        int32_t d[16];
+        cplx v[2][8];
 #pragma unroll
-        for (int m = 0; m < 16; ++m) d[m] = decomp_next_t(st[m], logB);
-        cplx v[8];
+        for (int t = 0; t < NQ; ++t) {
+          int32_t d[16];
 #pragma unroll
-        for (int m = 0; m < 8; ++m) v[m] = {(double)d[m], (double)d[m + 8]};
-        fft512_fwd(v, xch, T, lane);
+          for (int m = 0; m < 16; ++m) d[m] = decomp_next_t(st[m], logB);
+#pragma unroll
+          for (int m = 0; m < 8; ++m) v[t][m] = {(double)d[m], (double)d[m + 8]};
+        }
+        if (NQ == 2) fft512_fwd2(v[0], v[1], xch, T, lane);
+        else fft512_fwd(v[0], xch, T, lane);
+        // (X is indexed by the uniform h through branches: a dynamic index would put X in scratch)
         if (h == 0) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            X[0][q][j] = v[j];
-            mybox[j * 64 + lane] = v[4 + j];
-          }
+          for (int t = 0; t < NQ; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              X[0][q0 + t][j] = v[t][j];
+              mybox[(t * 4 + j) * 64 + lane] = v[t][4 + j];
+            }
         } else {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            X[1][q][j] = v[4 + j];
-            mybox[j * 64 + lane] = v[j];
-          }
+          for (int t = 0; t < NQ; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              X[1][q0 + t][j] = v[t][4 + j];
+              mybox[(t * 4 + j) * 64 + lane] = v[t][j];
+            }
         }
       }
-      pair_barrier();
+      xchg_barrier();
       if (work) {
         if (h == 0) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) X[1][q][j] = partnerbox[j * 64 + lane];
+          for (int t = 0; t < NQ; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) X[1][q0 + t][j] = partnerbox[(t * 4 + j) * 64 + lane];
         } else {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) X[0][q][j] = partnerbox[j * 64 + lane];
+          for (int t = 0; t < NQ; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) X[0][q0 + t][j] = partnerbox[(t * 4 + j) * 64 + lane];
         }
       }
-      pair_barrier();  // partner has read my mailbox: my scratch is free again
+      xchg_barrier();  // partner has read my mailbox: my scratch is free again
     }
     if constexpr (STAMPS) {
       uint64_t t = stamp();
@@ -236,8 +265,32 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     }
 
     // ---- per limb: MAC for both output polynomials on my half (key from the LDS ring),
-    //      trade halves through the mailbox, inverse transform of my polynomial -------------
-    static_for<0, LIMBS>([&](auto LI) {
+    //      trade halves through the mailbox, inverse transform of my polynomial.  The inverse
+    //      transform of limb li - 1 is spread over the first three key windows of limb li, so
+    //      its butterflies run while the key DMA of those windows is in flight. -------------
+    const int hi = lane >> 3, lo = lane & 7;
+    // bits(v + MAGIC) = MAGIC_BITS + round(v): limb li's exact integers, shifted into A.  The
+    // constant of all limbs is removed with limb 0 (it must not survive into the next step's
+    // rotation: X^a * const != const).
+    auto recombine = [&](const cplx (&v)[8], auto LIc) __attribute__((always_inline)) {
+      constexpr int lr = decltype(LIc)::value;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const double tr = v[m].re + RND_MAGIC, ti = v[m].im + RND_MAGIC;
+        if constexpr (RESID) {
+          max_resid = fmax(max_resid, fabs(v[m].re - (tr - RND_MAGIC)));
+          max_resid = fmax(max_resid, fabs(v[m].im - (ti - RND_MAGIC)));
+        }
+        if constexpr (lr == 0) {
+          A[m] += (uint64_t)__double_as_longlong(tr) - MAGIC_ALL;
+          A[m + 8] += (uint64_t)__double_as_longlong(ti) - MAGIC_ALL;
+        } else {
+          A[m] += (uint64_t)__double_as_longlong(tr) << limb_shift(lr);
+          A[m + 8] += (uint64_t)__double_as_longlong(ti) << limb_shift(lr);
+        }
+      }
+    };
+    static_for<0, LIMBS>([&](auto LI) __attribute__((always_inline)) {
       constexpr int li = decltype(LI)::value;
       cplx Ymine[4];
 #pragma unroll
@@ -264,18 +317,47 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             tp = t;
           }
           // refill the slot of group g - 1 with group g + 2
+#ifndef DIAG_NODMA
           if (g + 2 < total_groups) issue_group(g + 2);
+#endif
           if (work) {
-            const cplx* G = ring + (int)(g % 3) * GROUP + (4 * h) * 64 + lane;
+            auto mac = [&]() __attribute__((always_inline)) {
+              const cplx* G = ring + (int)(g % 3) * GROUP + (4 * h) * 64 + lane;
 #pragma unroll
-            for (int q = 0; q < L; ++q)
+              for (int q = 0; q < (DIAG_NOMAC ? 0 : L); ++q)
 #pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                const cplx gv = G[(q * 8 + j) * 64];
-                const cplx x = X[row][q][j];
-                Y[j].re = __builtin_fma(x.re, gv.re, __builtin_fma(-x.im, gv.im, Y[j].re));
-                Y[j].im = __builtin_fma(x.re, gv.im, __builtin_fma(x.im, gv.re, Y[j].im));
+                for (int j = 0; j < 4; ++j) {
+                  const cplx gv = G[(q * 8 + j) * 64];
+                  const cplx x = X[row][q][j];
+                  Y[j].re = __builtin_fma(x.re, gv.re, __builtin_fma(-x.im, gv.im, Y[j].re));
+                  Y[j].im = __builtin_fma(x.re, gv.im, __builtin_fma(x.im, gv.re, Y[j].im));
+                }
+            };
+            // deferred inverse transform of limb li - 1 (its pass 1 ran before this limb and
+            // left the data in my scratch): pass 2 in window 0, pass 3 in window 1
+            auto inv_stage = [&]() __attribute__((always_inline)) {
+              if constexpr (li > 0) {
+                const int win = c * K1 + row;
+                if (win == 0) {
+                  cplx vp[8];
+                  wave_lds_fence();
+                  inv_r1(vp, xch, hi, lo);
+                  inv_p2(vp, T, hi, lo);
+                  wave_lds_fence();
+                  inv_w2(vp, xch, hi, lo);
+                  wave_lds_fence();
+                } else if (win == 1) {
+                  cplx vp[8];
+                  wave_lds_fence();
+                  inv_r2(vp, xch, hi, lo);
+                  inv_p3(vp);
+                  recombine(vp, std::integral_constant<int, li - 1>{});
+                  wave_lds_fence();
+                }
               }
+            };
+            mac();
+            inv_stage();
           }
         }
         if (work) {
@@ -293,47 +375,38 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         acc_t[2] += t - tp;
         tp = t;
       }
-      pair_barrier();
-      cplx v[8];
+      xchg_barrier();
+      cplx vp[8];
       if (work) {
         if (h == 0) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            v[j] = Ymine[j];
-            v[4 + j] = partnerbox[j * 64 + lane];
+            vp[j] = Ymine[j];
+            vp[4 + j] = partnerbox[j * 64 + lane];
           }
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            v[j] = partnerbox[j * 64 + lane];
-            v[4 + j] = Ymine[j];
+            vp[j] = partnerbox[j * 64 + lane];
+            vp[4 + j] = Ymine[j];
           }
         }
       }
-      pair_barrier();
+      xchg_barrier();  // partner has read my mailbox: my scratch is free again
       if constexpr (STAMPS) {
         uint64_t t = stamp();
         acc_t[3] += t - tp;
         tp = t;
       }
       if (work) {
-        fft512_inv(v, xch, T, lane);
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-          const double tr = v[m].re + RND_MAGIC, ti = v[m].im + RND_MAGIC;
-          if constexpr (RESID) {
-            max_resid = fmax(max_resid, fabs(v[m].re - (tr - RND_MAGIC)));
-            max_resid = fmax(max_resid, fabs(v[m].im - (ti - RND_MAGIC)));
-          }
-          // bits(t) = MAGIC_BITS + round(v): the constant of all limbs is removed with limb 0
-          // (it must not survive into the next step's rotation: X^a * const != const)
-          if constexpr (li == 0) {
-            A[m] += (uint64_t)__double_as_longlong(tr) - MAGIC_ALL;
-            A[m + 8] += (uint64_t)__double_as_longlong(ti) - MAGIC_ALL;
-          } else {
-            A[m] += (uint64_t)__double_as_longlong(tr) << limb_shift(li);
-            A[m + 8] += (uint64_t)__double_as_longlong(ti) << limb_shift(li);
-          }
+        if constexpr (li == LIMBS - 1) {
+          fft512_inv(vp, xch, T, lane);
+          recombine(vp, LI);
+        } else {
+          // pass 1 now; passes 2 and 3 ride in the next limb's first two key windows
+          inv_p1(vp, T, lo);
+          inv_w1(vp, xch, hi, lo);
+          wave_lds_fence();
         }
       }
       if constexpr (STAMPS) {

@@ -26,8 +26,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "PBS/sec (whole node) at N=1024 batch=4096; achieved HBM GB/s"
 
 
-KERNEL_SOURCES = ("concrete_amd/csrc/pbs.hip", "concrete_amd/csrc/pbs.hpp", "concrete_amd/csrc/fft512.hpp",
-                  "concrete_amd/csrc/common.hpp")
+KERNEL_SOURCES = ("concrete_amd/csrc/pbs.hip", "concrete_amd/csrc/pbs2048.hip", "concrete_amd/csrc/pbs.hpp",
+                  "concrete_amd/csrc/fft512.hpp", "concrete_amd/csrc/kernel_util.hpp", "concrete_amd/csrc/common.hpp")
 
 
 def kernel_source_hash() -> str:
@@ -39,14 +39,15 @@ def kernel_source_hash() -> str:
     return h.hexdigest()[:16]
 
 
-def pmc_traffic(batch: int):
+def pmc_traffic(batch: int, config: str):
     """Per-launch HBM bytes from the committed PMC record (tools/pmc_traffic.py) when it was
     measured on these kernel sources at this batch; else None."""
     import glob
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pbs_traffic.json")), reverse=True):
         with open(f) as fh:
             rec = json.load(fh)
-        if rec.get("source_hash") == kernel_source_hash() and rec.get("batch") == batch:
+        if (rec.get("source_hash") == kernel_source_hash() and rec.get("batch") == batch
+                and rec.get("config", "cfg2") == config):
             return rec["traffic_bytes"], os.path.relpath(f, ROOT)
     return None, None
 
@@ -54,11 +55,14 @@ def pmc_traffic(batch: int):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", choices=("cfg2", "cfg4"), default="cfg2",
+                    help="cfg2: N=1024 n=630 l=3 logB=7 (the metric's config); cfg4: N=2048 n=742 l=1 logB=23")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=4096, help="PBS per GPU per step")
-    ap.add_argument("--cpu-sample", type=int, default=4096,
-                    help="PBS in the bounded CPU-baseline sample (default: one full 4096 batch, ~10-15 s)")
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="PBS in the bounded CPU-baseline sample (default: cfg2 4096 = one full batch, "
+                         "cfg4 1024; ~10-20 s)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", type=int, default=8, help="rows checked bit-exactly against the oracle (rank 0)")
@@ -83,8 +87,10 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    p = B.CFG2
-    width = 3
+    p = B.CFG2 if args.config == "cfg2" else B.CFG4
+    width = 3 if args.config == "cfg2" else 5
+    if not args.cpu_sample:
+        args.cpu_sample = 4096 if args.config == "cfg2" else 1024
     # ---- keys: deterministic synthetic keyset (product keygen); device key on rank 0 -> RCCL bcast
     lwe_sk = B.binary_key(p.n, 1)
     glwe_sk = B.binary_key(p.big_n, 2)
@@ -171,10 +177,10 @@ def main():
         achieved = bytes_per_pbs * args.batch / (kern_ms * 1e-3) / 1e9
         bitexact = None
         cpu = None
-        traffic, traffic_src = pmc_traffic(args.batch)
+        traffic, traffic_src = pmc_traffic(args.batch, args.config)
         if args.verify or not args.no_cpu_baseline:
             from oracle import pyoracle as O  # checker / CPU baseline only
-            op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
+            op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, limbs=O.limbs_for(p.N))
             if bsk is None:
                 bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 3)
             fcpu = O.bsk_to_fourier(op, bsk)
@@ -188,10 +194,10 @@ def main():
                 dt = time.perf_counter() - t1
                 cpu = {"value": round(len(sample) / dt, 2), "unit": "PBS/s", "cores": args.cpu_threads,
                        "kind": "port",
-                       "sample": f"{len(sample)} PBS of the same cfg2 workload (exact-limb f64 FFT restatement, "
-                                 f"OpenMP over ciphertexts), {dt:.2f} s wall"}
+                       "sample": f"{len(sample)} PBS of the same {args.config} workload (exact-limb f64 FFT "
+                                 f"restatement, {op.limbs} limbs, OpenMP over ciphertexts), {dt:.2f} s wall"}
         result = {
-            "metric": METRIC,
+            "metric": METRIC if args.config == "cfg2" else f"PBS/sec (whole node) at N={p.N} batch={args.batch}",
             "value": round(value, 1),
             "unit": "PBS/s",
             "n_gpus": world,
@@ -202,8 +208,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic (seeded keygen + fresh LWE encryptions of random 3-bit messages)",
-            "config": {"workload": "batched PBS cfg2: N=1024 k=1 n=630 l=3 logB=7",
+            "data": f"synthetic (seeded keygen + fresh LWE encryptions of random {width}-bit messages)",
+            "config": {"workload": f"batched PBS {args.config}: N={p.N} k={p.k} n={p.n} l={p.level} logB={p.base_log}",
                        "batch_per_gpu": args.batch, "global_batch": args.batch * world,
                        "parallelism": f"shard{world}", "key_bcast_s": round(t_bcast, 4), "gather_s": round(t_gather, 4),
                        "key_convert_s": round(t_key, 3)},

@@ -40,8 +40,11 @@ static std::unordered_map<const void*, KeyEntry> g_keys;
 static void set_device(uint32_t gpu) { CHIP_CHECK(hipSetDevice((int)gpu)); }
 
 static bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
-  return k == 1 && N == 1024 && level >= 1 && level <= 3 && base_log >= 1 && base_log <= 30 &&
-         level * base_log < 64;
+  if (k != 1 || base_log < 1) return false;
+  if (N == 1024) return level >= 1 && level <= 3 && base_log <= 30 && level * base_log < 64;
+  // N = 2048: one level whose digit splits into two 12-bit sub-digits (pbs2048.hip)
+  if (N == 2048) return level == 1 && base_log <= 2 * PBS2_SUB_BITS;
+  return false;
 }
 
 }  // namespace chip

@@ -58,6 +58,47 @@ __device__ __forceinline__ ddc ddc_mul(ddc a, ddc w) {
   return {dd_add(dd_mul(a.re, w.re), dd_neg(dd_mul(a.im, w.im))), dd_add(dd_mul(a.re, w.im), dd_mul(a.im, w.re))};
 }
 
+// balanced signed limb `limb` of a 64-bit word (limb widths 64/LIMBS, the first 64 % LIMBS one
+// bit wider: 22/21/21 for 3 limbs, 16 x 4 for 4): x = sum_t limb_t 2^{s_t} (mod 2^64)
+template <int LIMBS>
+__device__ __forceinline__ double limb_value(uint64_t rem, uint32_t limb) {
+  int64_t lv = 0;
+  for (int t = 0; t <= (int)limb; ++t) {
+    int w = 64 / LIMBS + (t < 64 % LIMBS ? 1 : 0);
+    uint64_t mask = (1ull << w) - 1ull;
+    uint64_t vv = rem & mask;
+    int64_t sgn = (vv >= (1ull << (w - 1))) ? (int64_t)vv - (int64_t)(1ull << w) : (int64_t)vv;
+    lv = sgn;
+    rem = (rem - (uint64_t)sgn) >> w;
+  }
+  return (double)lv;
+}
+
+// In-LDS radix-2 DIT over buf (bit-reversed input, natural output, forward sign), then the
+// scatter into the PBS kernels' register layout (slot-major, fft512_freq order), scaled 1/M.
+template <int M>
+__device__ __forceinline__ void dd_fft_scatter(ddc* buf, const ddc* __restrict__ tw_t, cplx* __restrict__ d) {
+  for (int h = 1; h < M; h <<= 1) {
+    for (int b = threadIdx.x; b < M / 2; b += blockDim.x) {
+      const int grp = b / h, pos = b % h;
+      const int i0 = grp * 2 * h + pos, i1 = i0 + h;
+      const ddc w = tw_t[pos * (M / (2 * h))];
+      const ddc x0 = buf[i0];
+      const ddc x1 = ddc_mul(buf[i1], w);
+      buf[i0] = {dd_add(x0.re, x1.re), dd_add(x0.im, x1.im)};
+      buf[i1] = {dd_add(x0.re, dd_neg(x1.re)), dd_add(x0.im, dd_neg(x1.im))};
+    }
+    __syncthreads();
+  }
+  const double scale = 1.0 / (double)M;
+  for (int e = threadIdx.x; e < M; e += blockDim.x) {
+    const int lane = e & 63, slot = e >> 6;
+    const int f = fft512_freq(lane, slot);
+    const ddc x = buf[f];
+    d[e] = {(x.re.hi + x.re.lo) * scale, (x.im.hi + x.im.lo) * scale};
+  }
+}
+
 // tables: zeta[j] = exp(i pi j / N) for j < N/2 ; tw[t] = exp(-2 pi i t / (N/2)) for t < N/4
 template <int N, int K, int L, int LIMBS>
 __global__ void __launch_bounds__(256) convert_bsk_kernel(cplx* __restrict__ dest, const uint64_t* __restrict__ src,
@@ -76,53 +117,44 @@ __global__ void __launch_bounds__(256) convert_bsk_kernel(cplx* __restrict__ des
   const uint64_t i = poly / ((uint64_t)K1 * K1 * L);
   const uint64_t* g = src + poly * N;
 
-  // balanced limb `limb` of each coefficient (limb widths 22/21/21 for LIMBS = 3)
   for (int j = threadIdx.x; j < M; j += blockDim.x) {
-    double ab[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      uint64_t rem = g[j + h * M];
-      int64_t lv = 0;
-      for (int t = 0; t <= (int)limb; ++t) {
-        int w = 64 / LIMBS + (t < 64 % LIMBS ? 1 : 0);
-        uint64_t mask = (1ull << w) - 1ull;
-        uint64_t vv = rem & mask;
-        int64_t sgn = (vv >= (1ull << (w - 1))) ? (int64_t)vv - (int64_t)(1ull << w) : (int64_t)vv;
-        lv = sgn;
-        rem = (rem - (uint64_t)sgn) >> w;
-      }
-      ab[h] = (double)lv;
-    }
     // z_j = (a + i b) * zeta^j ; store at bit-reversed position for the DIT passes
-    ddc z{dd_from(ab[0]), dd_from(ab[1])};
+    ddc z{dd_from(limb_value<LIMBS>(g[j], limb)), dd_from(limb_value<LIMBS>(g[j + M], limb))};
     z = ddc_mul(z, zeta_t[j]);
     const int r = (int)(__builtin_bitreverse32((uint32_t)j) >> (32 - LOGM));
     buf[r] = z;
   }
   __syncthreads();
-  // radix-2 DIT, natural output, forward sign
-  for (int h = 1; h < M; h <<= 1) {
-    for (int b = threadIdx.x; b < M / 2; b += blockDim.x) {
-      const int grp = b / h, pos = b % h;
-      const int i0 = grp * 2 * h + pos, i1 = i0 + h;
-      const ddc w = tw_t[pos * (M / (2 * h))];
-      const ddc x0 = buf[i0];
-      const ddc x1 = ddc_mul(buf[i1], w);
-      buf[i0] = {dd_add(x0.re, x1.re), dd_add(x0.im, x1.im)};
-      buf[i1] = {dd_add(x0.re, dd_neg(x1.re)), dd_add(x0.im, dd_neg(x1.im))};
-    }
-    __syncthreads();
-  }
-  // scatter into the PBS kernel's register layout, scaled by 1/M (exact power of two)
   const uint32_t q = (uint32_t)(L - 1) - v;
-  cplx* d = dest + ((((i * K1 + col) * LIMBS + limb) * RQ) + row * L + q) * (uint64_t)M;
-  const double scale = 1.0 / (double)M;
-  for (int e = threadIdx.x; e < M; e += blockDim.x) {
-    const int lane = e & 63, slot = e >> 6;
-    const int f = fft512_freq(lane, slot);
-    const ddc x = buf[f];
-    d[e] = {(x.re.hi + x.re.lo) * scale, (x.im.hi + x.im.lo) * scale};
+  dd_fft_scatter<M>(buf, tw_t, dest + ((((i * K1 + col) * LIMBS + limb) * RQ) + row * L + q) * (uint64_t)M);
+}
+
+// N = 2048, k = 1, l = 1 (pbs2048.hip).  Block = (i, limb, col, row, sub, parity), in the order
+// of the output layout [n][limb][col][row][sub][parity][512]: the parity half p(u) = g[2u + par]
+// of key polynomial g (row, col) times 2^{12 sub} (mod 2^64), limb `limb`, as an N = 1024
+// negacyclic polynomial: folded, twisted, transformed exactly like the N = 1024 key.
+template <int LIMBS>
+__global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__ dest, const uint64_t* __restrict__ src,
+                                                             const ddc* __restrict__ zeta_t,
+                                                             const ddc* __restrict__ tw_t) {
+  constexpr int M = 512, LOGM = 9;
+  __shared__ ddc buf[M];
+  const uint64_t blk = blockIdx.x;
+  const uint32_t par = (uint32_t)(blk & 1), sub = (uint32_t)((blk >> 1) & 1);
+  const uint32_t row = (uint32_t)((blk >> 2) & 1), col = (uint32_t)((blk >> 3) & 1);
+  const uint32_t limb = (uint32_t)((blk >> 4) % LIMBS);
+  const uint64_t i = (blk >> 4) / LIMBS;
+  const uint64_t* g = src + (i * 4 + row * 2 + col) * 2048;  // [n][l = 1][row][col][N]
+  const int shift = (int)sub * PBS2_SUB_BITS;
+  for (int j = threadIdx.x; j < M; j += blockDim.x) {
+    const uint64_t p0 = g[2 * j + par] << shift, p1 = g[2 * (j + M) + par] << shift;
+    ddc z{dd_from(limb_value<LIMBS>(p0, limb)), dd_from(limb_value<LIMBS>(p1, limb))};
+    z = ddc_mul(z, zeta_t[j]);
+    const int r = (int)(__builtin_bitreverse32((uint32_t)j) >> (32 - LOGM));
+    buf[r] = z;
   }
+  __syncthreads();
+  dd_fft_scatter<M>(buf, tw_t, dest + blk * M);
 }
 
 template <int N, int K, int L, int LIMBS>
@@ -165,19 +197,30 @@ static void make_tables(uint32_t N, std::vector<ddc>& zeta, std::vector<ddc>& tw
 }
 
 int convert_bsk_launch(const ConvertArgs& a) {
-  if (!(a.N == 1024 && a.k == 1 && a.limbs == 3 && a.level >= 1 && a.level <= 3)) {
+  const bool n1024 = a.N == 1024 && a.k == 1 && a.limbs == 3 && a.level >= 1 && a.level <= 3;
+  const bool n2048 = a.N == 2048 && a.k == 1 && a.limbs == (uint32_t)PBS2_LIMBS && a.level == 1;
+  if (!n1024 && !n2048) {
     set_error("unsupported BSK conversion parameters: N=%u k=%u level=%u limbs=%u", a.N, a.k, a.level, a.limbs);
     return -2;
   }
   std::vector<ddc> zeta, tw;
-  make_tables(a.N, zeta, tw);
+  make_tables(1024, zeta, tw);  // both paths transform N = 1024 negacyclic polynomials
   ddc *dz = nullptr, *dt = nullptr;
   CHIP_CHECK(hipMallocAsync((void**)&dz, zeta.size() * sizeof(ddc), a.stream));
   CHIP_CHECK(hipMallocAsync((void**)&dt, tw.size() * sizeof(ddc), a.stream));
   CHIP_CHECK(hipMemcpyAsync(dz, zeta.data(), zeta.size() * sizeof(ddc), hipMemcpyHostToDevice, a.stream));
   CHIP_CHECK(hipMemcpyAsync(dt, tw.data(), tw.size() * sizeof(ddc), hipMemcpyHostToDevice, a.stream));
-  int rc;
-  switch (a.level) {
+  int rc = 0;
+  if (n2048) {
+    const uint64_t blocks = (uint64_t)a.n * PBS2_LIMBS * 4 * PBS2_SUBS * 2;
+    hipLaunchKernelGGL((convert_bsk2048_kernel<PBS2_LIMBS>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
+                       reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      set_error("convert launch failed: %s", hipGetErrorString(e));
+      rc = -1;
+    }
+  } else switch (a.level) {
     case 1: rc = launch_convert<1024, 1, 1, 3>(a, dz, dt); break;
     case 2: rc = launch_convert<1024, 1, 2, 3>(a, dz, dt); break;
     default: rc = launch_convert<1024, 1, 3, 3>(a, dz, dt); break;

@@ -1,0 +1,46 @@
+// kernel_util.hpp — device helpers shared by the PBS kernels (pbs.hip, pbs2048.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+namespace chip {
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// bits(v + 1.5 * 2^52) = bits(1.5 * 2^52) + round(v) for |v| < 2^51
+constexpr double RND_MAGIC = 6755399441055744.0;
+constexpr uint64_t RND_MAGIC_BITS = 0x4338000000000000ull;
+
+// Workgroup barrier for the two waves of a ciphertext: LDS writes drained, compiler fence,
+// no vmcnt drain (key loads may stay in flight).
+__device__ __forceinline__ void pair_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Diagnostic cycle stamps (STAMPS builds only; never in the product kernel).
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+constexpr int NSTAMP = 8;  // rot+decomp, fwd+xchg, mac+vmcnt, y-xchg, inv+recomb, ring barrier, total, steps
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <int N_WAIT>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N_WAIT >= 0 && N_WAIT < 64, "vmcnt range");
+  // gfx9 encoding: vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt_hi[15:14]
+  __builtin_amdgcn_s_waitcnt((N_WAIT & 15) | (7 << 4) | (15 << 8) | ((N_WAIT >> 4) << 14));
+}
+
+}  // namespace chip

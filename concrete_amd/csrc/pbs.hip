@@ -31,29 +31,14 @@
 
 #include "common.hpp"
 #include "fft512.hpp"
+#include "kernel_util.hpp"
 #include "pbs.hpp"
 
 namespace chip {
 
-// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
-template <int B, int E, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (B < E) {
-    f(std::integral_constant<int, B>{});
-    static_for<B + 1, E>(f);
-  }
-}
-
-// bits(v + 1.5 * 2^52) = bits(1.5 * 2^52) + round(v) for |v| < 2^51
-constexpr double RND_MAGIC = 6755399441055744.0;
-constexpr uint64_t RND_MAGIC_BITS = 0x4338000000000000ull;
 // sum over limbs of RND_MAGIC_BITS << shift(limb), LIMBS = 3 (shifts 0, 22, 43)
 constexpr uint64_t MAGIC_ALL = RND_MAGIC_BITS + (RND_MAGIC_BITS << 22) + (RND_MAGIC_BITS << 43);
 constexpr int limb_shift(int li) { return li * 21 + (li > 0 ? 1 : 0); }
-
-// Workgroup barrier for the two waves of a ciphertext: LDS writes drained, compiler fence,
-// no vmcnt drain (key loads may stay in flight).
-__device__ __forceinline__ void pair_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 #ifndef DIAG_NOMAC
 #define DIAG_NOMAC 0  // diagnostic builds only: skip the key MAC (wrong results)
@@ -68,25 +53,6 @@ __device__ __forceinline__ void xchg_barrier() { asm volatile("s_waitcnt lgkmcnt
 #else
 __device__ __forceinline__ void xchg_barrier() { pair_barrier(); }
 #endif
-
-// Diagnostic cycle stamps (STAMPS builds only; never in the product kernel).
-__device__ __forceinline__ uint64_t stamp() {
-  uint64_t t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-constexpr int NSTAMP = 8;  // rot+decomp, fwd+xchg, mac+vmcnt, y-xchg, inv+recomb, ring barrier, total, steps
-
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-
-template <int N_WAIT>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N_WAIT >= 0 && N_WAIT < 64, "vmcnt range");
-  // gfx9 encoding: vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt_hi[15:14]
-  __builtin_amdgcn_s_waitcnt((N_WAIT & 15) | (7 << 4) | (15 << 8) | ((N_WAIT >> 4) << 14));
-}
 
 template <int L, bool RESID, bool STAMPS, bool STATE32>
 __global__ void __launch_bounds__(PBS_PAIRS * 128, 2)
@@ -479,6 +445,7 @@ static int launch_pair(const PbsArgs& a) {
 }
 
 int pbs_launch(const PbsArgs& a) {
+  if (a.N == 2048) return pbs2048_launch(a);
   if (a.N == 1024 && a.k == 1 && a.limbs == 3) {
     switch (a.level) {
       case 1: return launch_pair<1>(a);

@@ -16,15 +16,30 @@ constexpr size_t pbs1024_pair_lds_bytes(int level) {
   return PBS1024_TABLE_BYTES + 2 * PBS_PAIRS * PBS1024_XCH_SLOTS * 16 + 3 * (size_t)level * 512 * 16;
 }
 
+// N = 2048 kernel geometry (pbs2048.hip): four waves per ciphertext (one per even/odd half of
+// each GLWE polynomial), PBS2_CTS ciphertexts per workgroup, a ring of 16 KB key groups.
+constexpr int PBS2_CTS = 2;
+constexpr int PBS2_RING_SLOTS = 4;
+constexpr int PBS2_RING_DIST = 3;
+constexpr int PBS2_LIMBS = 4;     // 16-bit key limbs
+constexpr int PBS2_SUBS = 2;      // balanced 12-bit sub-digits per decomposition digit
+constexpr int PBS2_SUB_BITS = 12;
+constexpr size_t pbs2048_lds_bytes() {
+  return PBS1024_TABLE_BYTES + 4 * PBS2_CTS * PBS1024_XCH_SLOTS * 16 + (size_t)PBS2_RING_SLOTS * 1024 * 16;
+}
+
 // Number of exact limbs of the key polynomial for a parameter set.
 inline uint32_t default_limbs(uint32_t N, uint32_t level, uint32_t base_log) {
   (void)level;
   (void)base_log;
-  return N <= 1024 ? 3u : 6u;
+  return N <= 1024 ? 3u : (uint32_t)PBS2_LIMBS;
 }
 
-// Size in bytes of the device Fourier bootstrapping key (complex f64 per limb, N/2 per poly).
+// Size in bytes of the device Fourier bootstrapping key.
+//   N = 1024: [n][col][limb][row*l + q][512] complex f64
+//   N = 2048 (l = 1): [n][limb][col][row][sub][parity][512] complex f64 (pbs2048.hip)
 inline uint64_t fourier_bsk_bytes(uint32_t n, uint32_t k, uint32_t level, uint32_t N, uint32_t limbs) {
+  if (N == 2048) return (uint64_t)n * limbs * (k + 1) * (k + 1) * PBS2_SUBS * 2 * 512 * 16ull * level;
   return (uint64_t)n * level * (k + 1) * (k + 1) * limbs * (N / 2) * 16ull;
 }
 
@@ -42,6 +57,7 @@ struct PbsArgs {
 };
 
 int pbs_launch(const PbsArgs& a);
+int pbs2048_launch(const PbsArgs& a);  // pbs2048.hip
 
 struct ConvertArgs {
   hipStream_t stream;

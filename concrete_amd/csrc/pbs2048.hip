@@ -1,0 +1,315 @@
+// pbs2048.hip — batched classic PBS for N = 2048, k = 1, l = 1 (BASELINE.json configs[3],
+// "cfg4": n = 742, logB = 23) on CDNA4 (gfx950).
+//
+// Same semantics as pbs.hip (concrete-cpu c_api/bootstrap.rs:347-414 -> tfhe 0.10
+// blind_rotate_assign + sample extract; restated in oracle/tfhe_oracle.c:ora_pbs), same exact
+// arithmetic, re-planned for the larger ring:
+//
+// * Even/odd split.  With Z = X^2, a(X) = a_e(Z) + X a_o(Z) and
+//       a * b mod (X^2048 + 1) = (a_e b_e + Z a_o b_o) + X (a_e b_o + a_o b_e),
+//   where every product is negacyclic in Z modulo Z^1024 + 1: the N = 1024 product of pbs.hip
+//   (512-point folded, twisted transform, fft512.hpp).  Multiplying by Z is pointwise
+//   multiplication by the evaluation point alpha_k = exp(i pi (1 - 4k) / 1024) of frequency k.
+// * Sub-digits.  A 23-bit digit d is split exactly into balanced 12-bit parts,
+//   d = d_lo + 2^12 d_hi, and the key holds the limbs of both g and 2^12 g (mod 2^64), so every
+//   product is (|sub-digit| <= 2^11) x (16-bit limb): 4 limbs keep the certified error < 1/2.
+//
+// Mapping: four waves per ciphertext; wave v = 2c + p owns the parity-p half of GLWE polynomial c
+// (16 u64 per lane, lane t holds coefficient 2(t + 64m) + p), runs the forward transforms of its
+// own sub-digit polynomials, keeps frequency slots k2 in {2v, 2v + 1} of all of them (the rest
+// goes to its three partners through LDS), does the key MAC for all four outputs on its quarter
+// of the frequencies, trades quarters back and runs the inverse transforms of its own output.
+// PBS2_CTS ciphertexts per workgroup share a ring of 16 KB key groups filled by LDS-DMA.
+#include "common.hpp"
+#include "fft512.hpp"
+#include "kernel_util.hpp"
+#include "pbs.hpp"
+
+namespace chip {
+
+constexpr uint64_t P2_MAGIC_ALL =
+    RND_MAGIC_BITS + (RND_MAGIC_BITS << 16) + (RND_MAGIC_BITS << 32) + (RND_MAGIC_BITS << 48);
+
+template <bool RESID>
+__global__ void __launch_bounds__(PBS2_CTS * 256, 2)
+pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx,
+                    const uint64_t* __restrict__ luts, const uint64_t* __restrict__ lut_idx,
+                    const uint64_t* __restrict__ in, const uint64_t* __restrict__ in_idx,
+                    const cplx* __restrict__ fbsk, uint32_t n, uint32_t base_log, uint32_t num_samples,
+                    unsigned long long* __restrict__ resid_out) {
+  constexpr int N = 2048, LOG2_2N = 12, K1 = 2;
+  constexpr int NW = 4 * PBS2_CTS;                          // waves per workgroup
+  constexpr int GROUP = 2 * 512;                            // (limb, col, row, sub): parity e and o spectra
+  constexpr int NGRP = PBS2_LIMBS * K1 * K1 * PBS2_SUBS;    // ring groups per CMUX step
+  constexpr int PER_I = NGRP * GROUP;                       // complex values per Fourier GGSW
+  constexpr int RS = PBS2_RING_SLOTS, DIST = PBS2_RING_DIST;
+  constexpr int GLDS = GROUP / 64 / NW;                     // 1 KB LDS-DMA pieces per wave per group
+  constexpr int XS = (int)PBS1024_XCH_SLOTS;
+  static_assert(GROUP % (64 * NW) == 0 && DIST < RS, "ring geometry");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  cplx* T1 = reinterpret_cast<cplx*>(smem);
+  cplx* T2 = T1 + 512;
+  cplx* xch_all = T2 + 64;                // NW x XS: transpose scratch and mailboxes
+  cplx* ring = xch_all + NW * XS;         // RS x GROUP key ring
+
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int ctl = w >> 2;            // ciphertext within the workgroup
+  const int v = w & 3;               // virtual polynomial = frequency quarter
+  const int c = v >> 1, par = v & 1;
+  const uint32_t s = blockIdx.x * PBS2_CTS + ctl;
+  const bool active = s < num_samples;
+  cplx* xch = xch_all + w * XS;
+  uint64_t* xch64 = reinterpret_cast<uint64_t*>(xch);
+  const cplx* ctx = xch_all + ctl * 4 * XS;  // the four scratches of this ciphertext
+
+  const uint64_t total_groups = (uint64_t)n * NGRP;
+  auto issue_group = [&](uint64_t g) {
+    const uint64_t i = g / NGRP;
+    const int r = (int)(g % NGRP);
+    const cplx* src = fbsk + i * (uint64_t)PER_I + r * GROUP;
+    cplx* dst = ring + (int)(g % RS) * GROUP;
+#pragma unroll
+    for (int j = 0; j < GLDS; ++j) {
+      const int piece = w * GLDS + j;
+      __builtin_amdgcn_global_load_lds(src + piece * 64 + lane, (lds_ptr_t)(dst + piece * 64), 16, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int g = 0; g < DIST; ++g)
+    if ((uint64_t)g < total_groups) issue_group(g);
+
+  build_fft512_tables(T1, T2, threadIdx.x, NW * 64);
+  __syncthreads();
+  const Fft512Tables T{T1, T2};
+
+  const uint64_t* lwe = in + (active ? (in_idx ? in_idx[s] : s) : 0) * (uint64_t)(n + 1);
+  const uint64_t* lut = luts + (active && lut_idx ? lut_idx[s] : 0ull) * (uint64_t)(K1 * N);
+
+  // acc_c = LUT_c * X^{-ms(b)}; this wave holds coefficients 2(lane + 64 m) + par of polynomial c
+  uint64_t A[16];
+  {
+    const uint32_t bt = active ? modswitch(lwe[n], LOG2_2N) : 0u;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const uint32_t src = (uint32_t)(2 * (lane + 64 * m) + par + bt) & (2 * N - 1);
+      const uint64_t val = active ? lut[c * N + (src & (N - 1))] : 0ull;
+      A[m] = src < N ? val : 0ull - val;
+    }
+  }
+
+  // evaluation points of my two frequency slots (multiplication by Z = X^2)
+  cplx alpha[2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int k = fft512_freq(lane, 2 * v + jj);
+    const int num = (1 - 4 * k) & 2047;  // in units of pi / 1024
+    double sn, cs;
+    sincospi((double)num / 1024.0, &sn, &cs);
+    alpha[jj] = {cs, sn};
+  }
+
+  const int nrep = 64 - (int)base_log;
+  const int logB = (int)base_log;
+  double max_resid = 0.0;
+
+  uint64_t a_next = active ? lwe[0] : 0ull;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t ai = a_next;
+    if (i + 1 < n) a_next = active ? lwe[i + 1] : 0ull;
+    const uint32_t at = modswitch(ai, LOG2_2N);
+    // uniform across the ciphertext's four waves; skipping waves still join every barrier
+    const bool work = ai != 0ull && at != 0u;
+
+    // ---- ct1 = X^{at} acc - acc: the source coefficient may sit in the other parity's wave --
+    uint32_t st[16];
+    if (work) {
+#pragma unroll
+      for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = A[m];
+    }
+    pair_barrier();
+    if (work) {
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const uint32_t sp = (uint32_t)(2 * (lane + 64 * m) + par - (int)at) & (2 * N - 1);
+        const uint32_t sj = sp & (N - 1);
+        const uint64_t* box = reinterpret_cast<const uint64_t*>(ctx + (c * 2 + (int)(sj & 1)) * XS);
+        const uint64_t rv = box[sj >> 1];
+        st[m] = (uint32_t)decomp_init((sp < N ? rv : 0ull - rv) - A[m], nrep);
+      }
+    }
+    pair_barrier();  // every wave has read its sources: scratches are free again
+
+    // ---- one decomposition level, two sub-digit polynomials, forward transforms ----------
+    // X[vv][sub][jj]: spectrum of sub-digit polynomial (virtual poly vv = 2 row + parity) at
+    // frequency slot 2v + jj
+    cplx X[4][PBS2_SUBS][2];
+    int32_t dlo[16], dhi[16];
+    if (work) {
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const int32_t d = decomp_next_t(st[m], logB);
+        const int32_t lo = ((d + (1 << (PBS2_SUB_BITS - 1))) & ((1 << PBS2_SUB_BITS) - 1)) - (1 << (PBS2_SUB_BITS - 1));
+        dlo[m] = lo;
+        dhi[m] = (d - lo) >> PBS2_SUB_BITS;  // exact: d - lo is a multiple of 2^12
+      }
+    }
+#pragma unroll
+    for (int sub = 0; sub < PBS2_SUBS; ++sub) {
+      if (work) {
+        cplx vv8[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+          vv8[m] = sub == 0 ? cplx{(double)dlo[m], (double)dlo[m + 8]} : cplx{(double)dhi[m], (double)dhi[m + 8]};
+        fft512_fwd(vv8, xch, T, lane);
+#pragma unroll
+        for (int k2 = 0; k2 < 8; ++k2) xch[k2 * 64 + lane] = vv8[k2];
+      }
+      pair_barrier();
+      if (work) {
+#pragma unroll
+        for (int vv = 0; vv < 4; ++vv)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) X[vv][sub][jj] = ctx[vv * XS + (2 * v + jj) * 64 + lane];
+      }
+      pair_barrier();
+    }
+
+    // ---- per limb: MAC for the four outputs on my quarter, trade quarters, inverse ---------
+    static_for<0, PBS2_LIMBS>([&](auto LI) __attribute__((always_inline)) {
+      constexpr int li = decltype(LI)::value;
+      cplx Y[2][2][2];  // [col][parity][slot]
+      cplx P[2][2];     // [col][slot]: sum of odd x odd products, times alpha at the end
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          Y[cc][0][jj] = Y[cc][1][jj] = P[cc][jj] = {0.0, 0.0};
+        }
+#pragma unroll
+      for (int cc = 0; cc < K1; ++cc) {
+#pragma unroll
+        for (int row = 0; row < K1; ++row) {
+#pragma unroll
+          for (int sub = 0; sub < PBS2_SUBS; ++sub) {
+            const uint64_t g = (uint64_t)i * NGRP + ((li * K1 + cc) * K1 + row) * PBS2_SUBS + sub;
+            if (g + DIST - 1 < total_groups) wait_vmcnt<GLDS * (DIST - 1)>();
+            else wait_vmcnt<0>();
+            pair_barrier();  // group g landed for every wave; everyone is done with group g - 1
+            if (g + DIST < total_groups) issue_group(g + DIST);
+            if (work) {
+              const cplx* G = ring + (int)(g % RS) * GROUP + (2 * v) * 64 + lane;
+#pragma unroll
+              for (int jj = 0; jj < 2; ++jj) {
+                const cplx ge = G[jj * 64], go = G[512 + jj * 64];
+                const cplx xe = X[2 * row][sub][jj], xo = X[2 * row + 1][sub][jj];
+                // (a_e b_e + Z a_o b_o) and (a_e b_o + a_o b_e)
+                Y[cc][0][jj].re = __builtin_fma(xe.re, ge.re, __builtin_fma(-xe.im, ge.im, Y[cc][0][jj].re));
+                Y[cc][0][jj].im = __builtin_fma(xe.re, ge.im, __builtin_fma(xe.im, ge.re, Y[cc][0][jj].im));
+                P[cc][jj].re = __builtin_fma(xo.re, go.re, __builtin_fma(-xo.im, go.im, P[cc][jj].re));
+                P[cc][jj].im = __builtin_fma(xo.re, go.im, __builtin_fma(xo.im, go.re, P[cc][jj].im));
+                Y[cc][1][jj].re = __builtin_fma(xe.re, go.re, __builtin_fma(-xe.im, go.im, Y[cc][1][jj].re));
+                Y[cc][1][jj].im = __builtin_fma(xe.re, go.im, __builtin_fma(xe.im, go.re, Y[cc][1][jj].im));
+                Y[cc][1][jj].re = __builtin_fma(xo.re, ge.re, __builtin_fma(-xo.im, ge.im, Y[cc][1][jj].re));
+                Y[cc][1][jj].im = __builtin_fma(xo.re, ge.im, __builtin_fma(xo.im, ge.re, Y[cc][1][jj].im));
+              }
+            }
+          }
+        }
+      }
+      cplx V[8];
+      if (work) {
+#pragma unroll
+        for (int cc = 0; cc < K1; ++cc)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) Y[cc][0][jj] = cadd(Y[cc][0][jj], cmul(P[cc][jj], alpha[jj]));
+        // my quarter of every output: mailbox slot (output vo, slot jj)
+#pragma unroll
+        for (int vo = 0; vo < 4; ++vo)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) xch[(vo * 2 + jj) * 64 + lane] = Y[vo >> 1][vo & 1][jj];
+      }
+      pair_barrier();
+      if (work) {
+#pragma unroll
+        for (int vv = 0; vv < 4; ++vv)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) V[2 * vv + jj] = ctx[vv * XS + (v * 2 + jj) * 64 + lane];
+      }
+      pair_barrier();
+      if (work) {
+        fft512_inv(V, xch, T, lane);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          const double tr = V[m].re + RND_MAGIC, ti = V[m].im + RND_MAGIC;
+          if constexpr (RESID) {
+            max_resid = fmax(max_resid, fabs(V[m].re - (tr - RND_MAGIC)));
+            max_resid = fmax(max_resid, fabs(V[m].im - (ti - RND_MAGIC)));
+          }
+          if constexpr (li == 0) {
+            A[m] += (uint64_t)__double_as_longlong(tr) - P2_MAGIC_ALL;
+            A[m + 8] += (uint64_t)__double_as_longlong(ti) - P2_MAGIC_ALL;
+          } else {
+            A[m] += (uint64_t)__double_as_longlong(tr) << (16 * li);
+            A[m + 8] += (uint64_t)__double_as_longlong(ti) << (16 * li);
+          }
+        }
+      }
+    });
+  }
+
+  // ---- sample extract (nth = 0): out[j] = -A_0[N - j] (j > 0), A_0[0]; body B[0] ---------
+  uint64_t* o = out + (active ? (out_idx ? out_idx[s] : s) : 0) * (uint64_t)(N + 1);
+  if (!active) {
+  } else if (c == 0) {
+    // N - j has the parity of j: each half reverses its own coefficients
+#pragma unroll
+    for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = A[m];
+    wave_lds_fence();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int uj = lane + 64 * m;
+      const int j = 2 * uj + par;
+      const int u = par == 0 ? ((1024 - uj) & 1023) : 1023 - uj;
+      const uint64_t val = xch64[u];
+      o[j] = j == 0 ? val : 0ull - val;
+    }
+  } else if (par == 0 && lane == 0) {
+    o[N] = A[0];
+  }
+
+  if constexpr (RESID) {
+    for (int off = 32; off > 0; off >>= 1) max_resid = fmax(max_resid, __shfl_xor(max_resid, off));
+    if (lane == 0 && active && resid_out) atomicMax(resid_out, (unsigned long long)__double_as_longlong(max_resid));
+  }
+}
+
+template <bool RESID>
+static int launch2048_t(const PbsArgs& a) {
+  const size_t lds = pbs2048_lds_bytes();
+  auto kern = pbs2048_quad_kernel<RESID>;
+  CHIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const uint32_t blocks = (a.num_samples + PBS2_CTS - 1) / PBS2_CTS;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(PBS2_CTS * 256), lds, a.stream, a.out, a.out_idx, a.luts, a.lut_idx,
+                     a.in, a.in_idx, reinterpret_cast<const cplx*>(a.fbsk), a.n, a.base_log, a.num_samples, a.resid);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("pbs launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+int pbs2048_launch(const PbsArgs& a) {
+  if (!(a.N == 2048 && a.k == 1 && a.level == 1 && a.limbs == (uint32_t)PBS2_LIMBS && a.base_log >= 1 &&
+        a.base_log <= 2 * PBS2_SUB_BITS)) {
+    set_error("unsupported PBS parameters: N=%u k=%u level=%u base_log=%u limbs=%u", a.N, a.k, a.level, a.base_log,
+              a.limbs);
+    return -2;
+  }
+  if (a.num_samples == 0) return 0;
+  return a.resid ? launch2048_t<true>(a) : launch2048_t<false>(a);
+}
+
+}  // namespace chip

@@ -93,8 +93,36 @@ class Params:
 
 # BASELINE.json configs[1] (cfg2) and configs[3] (cfg4); KS params from SURVEY.md §8.
 CFG2 = Params(n=630, k=1, N=1024, l=3, logB=7, ks_l=4, ks_logB=3, limbs=3)
-CFG4 = Params(n=742, k=1, N=2048, l=1, logB=23, ks_l=5, ks_logB=3, limbs=6)
+CFG4 = Params(n=742, k=1, N=2048, l=1, logB=23, ks_l=5, ks_logB=3, limbs=8)  # 8 limbs: certified bound 0.16
 SMALL = Params(n=16, k=1, N=256, l=3, logB=7, ks_l=4, ks_logB=3, limbs=3)
+
+
+def limbs_for(N: int) -> int:
+    """Key limbs the oracle's certified FFT path needs (fft_error_bound < 1/2): 3 at N = 1024
+    (l = 3, logB = 7), 8 at N = 2048 (l = 1, logB = 23)."""
+    return 3 if N <= 1024 else 8
+
+
+def gpu2048_error_bound(fbsk_gpu: np.ndarray) -> float:
+    """Certified bound on |x - round(x)| for the GPU's N = 2048 scheme (concrete_amd/csrc/
+    pbs2048.hip): even/odd halves as N = 1024 negacyclic products, 12-bit
+    sub-digits (|d| <= 2^11) x 16-bit key limbs, 8 products per output, plus the rounding of the
+    pointwise multiplication by alpha_k.  fbsk_gpu: the device key (f64 view, scaled by 1/512)."""
+    M = 512
+    u = 2.0 ** -53
+    logM = 9.0
+    eta = u + 4.0 * u / (1.0 - 4.0 * u) * (np.sqrt(2.0) + u)
+    gamma = logM * eta / (1.0 - logM * eta)
+    f = fbsk_gpu.reshape(-1, 2)
+    maxG = float(np.max(np.hypot(f[:, 0], f[:, 1]))) * M
+    dnorm = np.sqrt(1024.0) * 2.0 ** 11
+    terms = 8.0
+    main = terms * dnorm * maxG * (4.0 * gamma + 3.0 * u) * 1.0001
+    # alpha * P: |P_k| <= 4 * (512 sqrt2 2^11) * maxG / 512, complex-multiply error <= 2 sqrt2 u |P_k|,
+    # summed over the 512 frequencies of the unnormalised inverse transform
+    alpha_term = M * 2.0 * np.sqrt(2.0) * u * 4.0 * np.sqrt(2.0) * 2.0 ** 11 * maxG
+    max_out = terms * 1024.0 * 2.0 ** 11 * 2.0 ** 15
+    return float(main + alpha_term + 4.0 * u * max_out)
 
 
 def bsk_std_torus(p: Params) -> float:

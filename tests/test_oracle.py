@@ -329,3 +329,26 @@ def test_pbs_output_noise_matches_model(oracle):
     model = NM.variance_blind_rotate(p.n, p.k, p.N, p.logB, p.l, 64, 53, var_bsk, exact=True)
     # 48 samples: the sample variance is within a factor ~2 of the model with overwhelming probability
     assert model / 3 < emp < model * 3, (emp, model)
+
+
+def test_cfg4_shape_fft_equals_karatsuba(oracle):
+    """N = 2048, l = 1, logB = 23 (BASELINE configs[3]) with the oracle's 8-limb FFT path: its
+    certified bound is < 1/2 and it agrees bit-for-bit with the integer Karatsuba product."""
+    from dataclasses import replace
+    p = replace(oracle.CFG4, n=10)
+    assert p.limbs == oracle.limbs_for(p.N) == 8
+    lwe = oracle.binary_key(p.n, 1)
+    glwe = oracle.binary_key(p.big_n, 2)
+    bsk = oracle.keygen_bsk(p, lwe, glwe, 3, std=2.0 ** -45)
+    f = oracle.bsk_to_fourier(p, bsk)
+    assert oracle.fft_error_bound(p, f) < 0.5
+    width = 5
+    table = np.arange(32, dtype=np.uint64)[::-1].copy()
+    acc = oracle.trivial_glwe(p, oracle.expand_lut(table, p.N, width))
+    msgs = np.array([0, 1, 17, 31])
+    cts = oracle.lwe_encrypt_batch(lwe, [oracle.encode(int(m), width) for m in msgs], p.n, 2.0 ** -30, 7)
+    r_fft, _ = oracle.pbs_batch(p, cts, acc[None, :], fbsk=f, mode=oracle.MODE_FFT)
+    r_kar, _ = oracle.pbs_batch(p, cts, acc[None, :], bsk=bsk, mode=1)
+    assert np.array_equal(r_fft, r_kar)
+    dec = oracle.lwe_decrypt_batch(glwe, r_fft, p.big_n)
+    assert [oracle.decode(int(d), width) for d in dec] == [int(table[m]) for m in msgs]

@@ -96,6 +96,57 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Register-only transpose of lane bits 3..5 with the element index (the "hi" transpose of both
+// directions: lane (h, lo) element b  ->  lane (b, lo) element h), done as three butterfly
+// swaps with cross-lane moves instead of an LDS round trip:
+//   lane bit 5 <-> element bit 2: v_permlane32_swap (upper half of v[e] <-> lower half of v[e|4])
+//   lane bit 4 <-> element bit 1: v_permlane16_swap (odd rows of v[e] <-> even rows of v[e|2])
+//   lane bit 3 <-> element bit 0: DPP row_shr:8 / row_shl:8 under a bank mask (v[e] <-> v[e|1])
+__device__ __forceinline__ void swap32(uint32_t& a, uint32_t& b) {
+  auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+  a = r[0];
+  b = r[1];
+}
+__device__ __forceinline__ void swap16(uint32_t& a, uint32_t& b) {
+  auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+  a = r[0];
+  b = r[1];
+}
+__device__ __forceinline__ void swap8(uint32_t& a, uint32_t& b) {
+  // a keeps lanes with bit 3 = 0 and takes b's (lane - 8) where bit 3 = 1; b the converse
+  const uint32_t na = (uint32_t)__builtin_amdgcn_update_dpp((int)a, (int)b, 0x118, 0xF, 0xC, false);
+  const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp((int)b, (int)a, 0x108, 0xF, 0x3, false);
+  a = na;
+  b = nb;
+}
+template <int MODE>
+__device__ __forceinline__ void swap_cplx(cplx& x, cplx& y) {
+  uint32_t xa[4], ya[4];
+  const uint64_t x0 = (uint64_t)__double_as_longlong(x.re), x1 = (uint64_t)__double_as_longlong(x.im);
+  const uint64_t y0 = (uint64_t)__double_as_longlong(y.re), y1 = (uint64_t)__double_as_longlong(y.im);
+  xa[0] = (uint32_t)x0, xa[1] = (uint32_t)(x0 >> 32), xa[2] = (uint32_t)x1, xa[3] = (uint32_t)(x1 >> 32);
+  ya[0] = (uint32_t)y0, ya[1] = (uint32_t)(y0 >> 32), ya[2] = (uint32_t)y1, ya[3] = (uint32_t)(y1 >> 32);
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    if constexpr (MODE == 32) swap32(xa[d], ya[d]);
+    else if constexpr (MODE == 16) swap16(xa[d], ya[d]);
+    else swap8(xa[d], ya[d]);
+  }
+  x.re = __longlong_as_double((long long)(((uint64_t)xa[1] << 32) | xa[0]));
+  x.im = __longlong_as_double((long long)(((uint64_t)xa[3] << 32) | xa[2]));
+  y.re = __longlong_as_double((long long)(((uint64_t)ya[1] << 32) | ya[0]));
+  y.im = __longlong_as_double((long long)(((uint64_t)ya[3] << 32) | ya[2]));
+}
+__device__ __forceinline__ void xpose_hi(cplx (&v)[8]) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) swap_cplx<32>(v[e], v[e | 4]);
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    if (!(e & 2)) swap_cplx<16>(v[e], v[e | 2]);
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) swap_cplx<8>(v[e], v[e | 1]);
+}
+
 // psi^m = exp(i pi m / 16), m = 0..7 (correctly rounded)
 __device__ __forceinline__ cplx psi_pow(int m) {
   constexpr double C[8] = {1.0,
@@ -167,13 +218,21 @@ __device__ __forceinline__ void fwd_r2(cplx (&v)[8], const cplx* xch, int hi, in
   for (int e = 0; e < 8; ++e) v[e] = xch[xslot(hi, lo, e)];
 }
 
+#ifndef XPOSE_HI_REGS
+#define XPOSE_HI_REGS 1  // lane-bits-3..5 transposes with cross-lane moves instead of LDS
+#endif
+
 __device__ __forceinline__ void fft512_fwd(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane) {
   const int hi = lane >> 3, lo = lane & 7;
   fwd_p1(v, T, lane);
+#if XPOSE_HI_REGS
+  xpose_hi(v);
+#else
   fwd_w1(v, xch, hi, lo);
   wave_lds_fence();
   fwd_r1(v, xch, hi, lo);
   wave_lds_fence();
+#endif
   fwd_p2(v, T, lo);
   fwd_w2(v, xch, hi, lo);
   wave_lds_fence();
@@ -260,10 +319,14 @@ __device__ __forceinline__ void fft512_inv(cplx (&v)[8], cplx* xch, const Fft512
   inv_r1(v, xch, hi, lo);
   wave_lds_fence();
   inv_p2(v, T, hi, lo);
+#if XPOSE_HI_REGS
+  xpose_hi(v);
+#else
   inv_w2(v, xch, hi, lo);
   wave_lds_fence();
   inv_r2(v, xch, hi, lo);
   wave_lds_fence();
+#endif
   inv_p3(v);
 }
 

@@ -309,10 +309,16 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
                   wave_lds_fence();
                   inv_r1(vp, xch, hi, lo);
                   inv_p2(vp, T, hi, lo);
+#if XPOSE_HI_REGS
+                  xpose_hi(vp);
+                  inv_p3(vp);
+                  recombine(vp, std::integral_constant<int, li - 1>{});
+#else
                   wave_lds_fence();
                   inv_w2(vp, xch, hi, lo);
+#endif
                   wave_lds_fence();
-                } else if (win == 1) {
+                } else if (win == 1 && !XPOSE_HI_REGS) {
                   cplx vp[8];
                   wave_lds_fence();
                   inv_r2(vp, xch, hi, lo);

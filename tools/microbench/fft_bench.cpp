@@ -18,7 +18,9 @@ template <int MODE>
 __device__ __forceinline__ void fwd(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane) {
   const int hi = lane >> 3, lo = lane & 7;
   if constexpr (MODE != 2) fwd_p1(v, T, lane);
-  if constexpr (MODE != 1) {
+  if constexpr (MODE == 4) {
+    xpose_hi(v);
+  } else if constexpr (MODE != 1) {
     fwd_w1(v, xch, hi, lo);
     wave_lds_fence();
     fwd_r1(v, xch, hi, lo);
@@ -44,7 +46,9 @@ __device__ __forceinline__ void inv(cplx (&v)[8], cplx* xch, const Fft512Tables&
     wave_lds_fence();
   }
   if constexpr (MODE != 2) inv_p2(v, T, hi, lo);
-  if constexpr (MODE != 1) {
+  if constexpr (MODE == 4) {
+    xpose_hi(v);
+  } else if constexpr (MODE != 1) {
     inv_w2(v, xch, hi, lo);
     wave_lds_fence();
     inv_r2(v, xch, hi, lo);
@@ -145,6 +149,8 @@ __global__ void __launch_bounds__(NWAVES * 64) kern(double* out, unsigned long l
   if (lane == 0) cyc[blockIdx.x * NWAVES + w] = (unsigned long long)(c1 - c0);
 }
 
+static double* ref_out = nullptr;  // outputs of the last MODE 0 run
+
 template <int MODE, int NWAVES>
 void run(const char* name) {
   auto K = MODE == 3 ? kern2<NWAVES> : kern<MODE == 3 ? 0 : MODE, NWAVES>;
@@ -167,6 +173,21 @@ void run(const char* name) {
   hipEventSynchronize(e1);
   float ms;
   hipEventElapsedTime(&ms, e0, e1);
+  // correctness: modes 0 and 4 compute the same transforms (bit-identical outputs)
+  if (MODE == 0 || MODE == 4) {
+    size_t cnt = (size_t)ncu * NWAVES * 64;
+    double* hv = (double*)malloc(cnt * sizeof(double));
+    hipMemcpy(hv, out, cnt * sizeof(double), hipMemcpyDeviceToHost);
+    if (MODE == 0) {
+      free(ref_out);
+      ref_out = hv;
+    } else {
+      size_t bad = 0;
+      for (size_t i = 0; i < cnt; ++i) bad += hv[i] != ref_out[i];
+      printf("  register-transpose results identical to LDS transposes: %s (%zu mismatches)\n", bad ? "NO" : "yes", bad);
+      free(hv);
+    }
+  }
   unsigned long long* h = (unsigned long long*)malloc(ncu * NWAVES * sizeof(unsigned long long));
   hipMemcpy(h, cyc, ncu * NWAVES * sizeof(unsigned long long), hipMemcpyDeviceToHost);
   double avg = 0;
@@ -182,7 +203,9 @@ void run(const char* name) {
 
 int main() {
   run<0, 4>("full");
+  run<4, 4>("full, hi transposes in regs");
   run<0, 8>("full");
+  run<4, 8>("full, hi transposes in regs");
   run<1, 4>("butterflies only");
   run<1, 8>("butterflies only");
   run<2, 4>("transposes only");

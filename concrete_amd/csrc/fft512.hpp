@@ -161,8 +161,14 @@ __device__ __forceinline__ cplx psi_pow(int m) {
 }
 
 // LDS tables shared by the workgroup:
-//   T1[k0 * 64 + t] = zeta^t * w512^{t k0}      (512 entries)
-//   T2[k1 * 8 + t0] = w64^{t0 k1}               (64 entries, symmetric in (k1, t0))
+//   T1[k0 * T1_STRIDE + t] = zeta^t * w512^{t k0}   (8 rows of 64, padded to 72 entries)
+//   T2[k1 * 8 + t0] = w64^{t0 k1}                   (64 entries, symmetric in (k1, t0))
+// The row padding makes the inverse pass-2 read T1[hi * 72 + 8 t1 + lo] conflict-free on the
+// ds_read_b128 lane groups (2-way with a 64 stride); the forward read T1[k0 * 72 + lane] stays
+// contiguous.  The inverse pass-1 read uses T2's symmetry, T2[t0 * 8 + lo], for the same reason
+// (T2[lo * 8 + t0] is 4-way conflicted).
+constexpr int T1_STRIDE = 72;
+constexpr int FFT512_TABLE_ENTRIES = 8 * T1_STRIDE + 64;
 struct Fft512Tables {
   const cplx* T1;
   const cplx* T2;
@@ -175,7 +181,7 @@ __device__ __forceinline__ void build_fft512_tables(cplx* T1, cplx* T2, int tid,
     // angle / pi = t / 1024 - 2 t k0 / 512, reduced mod 2
     const int num = (t - 4 * ((t * k0) & 511)) & 2047;  // in units of pi / 1024
     sincospi((double)num / 1024.0, &s, &c);
-    T1[e] = {c, s};
+    T1[k0 * T1_STRIDE + t] = {c, s};
   }
   for (int e = tid; e < 64; e += nthreads) {
     const int k1 = e >> 3, t0 = e & 7;
@@ -192,7 +198,7 @@ __device__ __forceinline__ void fwd_p1(cplx (&v)[8], const Fft512Tables& T, int 
   for (int m = 1; m < 8; ++m) v[m] = cmul(v[m], psi_pow(m));
   dft8<false>(v);
 #pragma unroll
-  for (int k0 = 0; k0 < 8; ++k0) v[k0] = cmul(v[k0], T.T1[k0 * 64 + lane]);
+  for (int k0 = 0; k0 < 8; ++k0) v[k0] = cmul(v[k0], T.T1[k0 * T1_STRIDE + lane]);
 }
 // transpose 1: writer lane (t1 = hi, t0 = lo) element k0 ; reader lane (k0 = hi, t0 = lo) element t1
 __device__ __forceinline__ void fwd_w1(const cplx (&v)[8], cplx* xch, int hi, int lo) {
@@ -280,7 +286,7 @@ __device__ __forceinline__ void fft512_fwd2(cplx (&a)[8], cplx (&b)[8], cplx* xc
 __device__ __forceinline__ void inv_p1(cplx (&v)[8], const Fft512Tables& T, int lo) {
   dft8<true>(v);  // over k2 -> t0 ; lane (k0 = hi, k1 = lo)
 #pragma unroll
-  for (int t0 = 1; t0 < 8; ++t0) v[t0] = cmulc(v[t0], T.T2[lo * 8 + t0]);
+  for (int t0 = 1; t0 < 8; ++t0) v[t0] = cmulc(v[t0], T.T2[t0 * 8 + lo]);
 }
 // transpose 2': writer lane (k0, k1) element t0 ; reader lane (k0 = hi, t0 = lo) element k1
 __device__ __forceinline__ void inv_w1(const cplx (&v)[8], cplx* xch, int hi, int lo) {
@@ -294,7 +300,7 @@ __device__ __forceinline__ void inv_r1(cplx (&v)[8], const cplx* xch, int hi, in
 __device__ __forceinline__ void inv_p2(cplx (&v)[8], const Fft512Tables& T, int hi, int lo) {
   dft8<true>(v);  // over k1 -> t1 ; lane (k0 = hi, t0 = lo)
 #pragma unroll
-  for (int t1 = 0; t1 < 8; ++t1) v[t1] = cmulc(v[t1], T.T1[hi * 64 + 8 * t1 + lo]);
+  for (int t1 = 0; t1 < 8; ++t1) v[t1] = cmulc(v[t1], T.T1[hi * T1_STRIDE + 8 * t1 + lo]);
 }
 // transpose 1': writer lane (k0 = hi, t0 = lo) element t1 ; reader lane (t1 = hi, t0 = lo) element k0
 __device__ __forceinline__ void inv_w2(const cplx (&v)[8], cplx* xch, int hi, int lo) {

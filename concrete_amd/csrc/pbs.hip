@@ -73,7 +73,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cplx* T1 = reinterpret_cast<cplx*>(smem);
-  cplx* T2 = T1 + 512;
+  cplx* T2 = T1 + 8 * T1_STRIDE;
   cplx* xch_all = T2 + 64;                       // NW x PBS1024_XCH_SLOTS: transpose scratch,
   cplx* ring = xch_all + NW * PBS1024_XCH_SLOTS;  // also the mailbox; 3 x GROUP key ring
 

@@ -49,7 +49,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cplx* T1 = reinterpret_cast<cplx*>(smem);
-  cplx* T2 = T1 + 512;
+  cplx* T2 = T1 + 8 * T1_STRIDE;
   cplx* xch_all = T2 + 64;                // NW x XS: transpose scratch and mailboxes
   cplx* ring = xch_all + NW * XS;         // RS x GROUP key ring
 

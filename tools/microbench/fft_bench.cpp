@@ -91,7 +91,7 @@ template <int NWAVES>
 __global__ void __launch_bounds__(NWAVES * 64) kern2(double* out, unsigned long long* cyc) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cplx* T1 = reinterpret_cast<cplx*>(smem);
-  cplx* T2 = T1 + 512;
+  cplx* T2 = T1 + 8 * T1_STRIDE;
   cplx* xall = T2 + 64;
   build_fft512_tables(T1, T2, threadIdx.x, NWAVES * 64);
   __syncthreads();
@@ -124,7 +124,7 @@ template <int MODE, int NWAVES>
 __global__ void __launch_bounds__(NWAVES * 64) kern(double* out, unsigned long long* cyc) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cplx* T1 = reinterpret_cast<cplx*>(smem);
-  cplx* T2 = T1 + 512;
+  cplx* T2 = T1 + 8 * T1_STRIDE;
   cplx* xall = T2 + 64;
   build_fft512_tables(T1, T2, threadIdx.x, NWAVES * 64);
   __syncthreads();
@@ -155,7 +155,7 @@ template <int MODE, int NWAVES>
 void run(const char* name) {
   auto K = MODE == 3 ? kern2<NWAVES> : kern<MODE == 3 ? 0 : MODE, NWAVES>;
   int ncu = 256;
-  size_t lds = (512 + 64) * 16 + NWAVES * 576 * 16;
+  size_t lds = FFT512_TABLE_ENTRIES * 16 + NWAVES * 576 * 16;
   // pad LDS so that exactly one workgroup fits per CU
   size_t lds_req = lds < 90 * 1024 ? 90 * 1024 : lds;
   double* out;

@@ -50,6 +50,22 @@ SIGNATURES = {
     "concrete_hip_bsk_generate": (None, [vp, vp, vp, u64, u64, u64, u64, u64, dbl, u64]),
     "concrete_hip_ksk_generate": (None, [vp, vp, vp, u64, u64, u64, u64, dbl, u64]),
     "concrete_hip_encode_expand_lut": (None, [vp, u64, vp, u64, u32, i32]),
+    # Part 4: runtime glue (memref descriptors expanded: allocated, aligned, offset, sizes, strides)
+    "concrete_hip_keyset_create": (vp, []),
+    "concrete_hip_keyset_destroy": (None, [vp]),
+    "concrete_hip_keyset_add_bsk": (i32, [vp, u32, vp, u32, u32, u32, u32, u32]),
+    "concrete_hip_keyset_add_ksk": (i32, [vp, u32, vp, u32, u32, u32, u32]),
+    "concrete_hip_keyset_set_devices": (i32, [vp, vp, u32]),
+    "memref_keyswitch_lwe_hip_u64": (None, [vp, vp, u64, u64, u64, vp, vp, u64, u64, u64, u32, u32, u32, u32, u32, vp]),
+    "memref_bootstrap_lwe_hip_u64": (None, [vp, vp, u64, u64, u64, vp, vp, u64, u64, u64, vp, vp, u64, u64, u64,
+                                            u32, u32, u32, u32, u32, u32, vp]),
+    "memref_batched_keyswitch_lwe_hip_u64": (None, [vp, vp, u64, u64, u64, u64, u64, vp, vp, u64, u64, u64, u64, u64,
+                                                    u32, u32, u32, u32, u32, vp]),
+    "memref_batched_bootstrap_lwe_hip_u64": (None, [vp, vp, u64, u64, u64, u64, u64, vp, vp, u64, u64, u64, u64, u64,
+                                                    vp, vp, u64, u64, u64, u32, u32, u32, u32, u32, u32, vp]),
+    "memref_batched_mapped_bootstrap_lwe_hip_u64": (None, [vp, vp, u64, u64, u64, u64, u64, vp, vp, u64, u64, u64, u64,
+                                                           u64, vp, vp, u64, u64, u64, u64, u64, u32, u32, u32, u32,
+                                                           u32, u32, vp]),
 }
 
 _lib = None

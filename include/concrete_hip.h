@@ -140,6 +140,67 @@ void concrete_hip_ksk_generate(uint64_t *ksk, const uint64_t *sk_in, const uint6
 void concrete_hip_encode_expand_lut(uint64_t *out, uint64_t out_size, const uint64_t *in, uint64_t in_size,
                                     uint32_t out_message_bits, int is_signed);
 
+/* ------------------------------------------------------------------------------------------
+ * Part 4: circuit-facing runtime glue (SURVEY.md §8b layer B2).  Mirrors of the runtime's
+ * memref wrappers (compiler include/concretelang/Runtime/wrappers.h:240-300, implementation
+ * lib/Runtime/wrappers.cpp:88-363) over an opaque keyset handle instead of the C++
+ * RuntimeContext (include/concretelang/Runtime/context.h:42-145): MLIR memref descriptors
+ * expanded as (allocated, aligned, offset, sizes..., strides...), host memory in and out, the
+ * same shape assertions (violations abort), trivial GLWE accumulators built from the LUT
+ * (wrappers.cpp:199-209), one LUT per sample for the mapped form (wrappers.cpp:317-325).
+ * Differences by design: device keys are converted once per keyset and device and reused
+ * across calls (the reference re-converts per RuntimeContext, ServerLib.cpp:579); a keyset may
+ * list several devices, across which every batched call is sharded in contiguous slices
+ * (the reference's direct route is "TODO: Multi GPU", wrappers.cpp:176-177), the converted key
+ * reaching the other devices by peer copy.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct concrete_hip_keyset concrete_hip_keyset;
+concrete_hip_keyset *concrete_hip_keyset_create(void);
+void concrete_hip_keyset_destroy(concrete_hip_keyset *ks);
+/* standard-domain keys (host buffers, copied): BSK [n][l][k+1][k+1][N], KSK [n_in][l][n_out+1] */
+int concrete_hip_keyset_add_bsk(concrete_hip_keyset *ks, uint32_t bsk_index, const uint64_t *bsk, uint32_t input_lwe_dim,
+                                uint32_t glwe_dim, uint32_t level, uint32_t base_log, uint32_t poly_size);
+int concrete_hip_keyset_add_ksk(concrete_hip_keyset *ks, uint32_t ksk_index, const uint64_t *ksk, uint32_t level,
+                                uint32_t base_log, uint32_t input_lwe_dim, uint32_t output_lwe_dim);
+/* devices the batched calls shard across (default: device 0); entries may repeat */
+int concrete_hip_keyset_set_devices(concrete_hip_keyset *ks, const uint32_t *devices, uint32_t count);
+
+void memref_keyswitch_lwe_hip_u64(uint64_t *out_allocated, uint64_t *out_aligned, uint64_t out_offset,
+                                  uint64_t out_size, uint64_t out_stride, uint64_t *ct0_allocated,
+                                  uint64_t *ct0_aligned, uint64_t ct0_offset, uint64_t ct0_size, uint64_t ct0_stride,
+                                  uint32_t level, uint32_t base_log, uint32_t input_lwe_dim,
+                                  uint32_t output_lwe_dim, uint32_t ksk_index, concrete_hip_keyset *context);
+void memref_bootstrap_lwe_hip_u64(uint64_t *out_allocated, uint64_t *out_aligned, uint64_t out_offset,
+                                  uint64_t out_size, uint64_t out_stride, uint64_t *ct0_allocated,
+                                  uint64_t *ct0_aligned, uint64_t ct0_offset, uint64_t ct0_size, uint64_t ct0_stride,
+                                  uint64_t *tlu_allocated, uint64_t *tlu_aligned, uint64_t tlu_offset,
+                                  uint64_t tlu_size, uint64_t tlu_stride, uint32_t input_lwe_dim, uint32_t poly_size,
+                                  uint32_t level, uint32_t base_log, uint32_t glwe_dim, uint32_t bsk_index,
+                                  concrete_hip_keyset *context);
+void memref_batched_keyswitch_lwe_hip_u64(uint64_t *out_allocated, uint64_t *out_aligned, uint64_t out_offset,
+                                          uint64_t out_size0, uint64_t out_size1, uint64_t out_stride0,
+                                          uint64_t out_stride1, uint64_t *ct0_allocated, uint64_t *ct0_aligned,
+                                          uint64_t ct0_offset, uint64_t ct0_size0, uint64_t ct0_size1,
+                                          uint64_t ct0_stride0, uint64_t ct0_stride1, uint32_t level,
+                                          uint32_t base_log, uint32_t input_lwe_dim, uint32_t output_lwe_dim,
+                                          uint32_t ksk_index, concrete_hip_keyset *context);
+void memref_batched_bootstrap_lwe_hip_u64(uint64_t *out_allocated, uint64_t *out_aligned, uint64_t out_offset,
+                                          uint64_t out_size0, uint64_t out_size1, uint64_t out_stride0,
+                                          uint64_t out_stride1, uint64_t *ct0_allocated, uint64_t *ct0_aligned,
+                                          uint64_t ct0_offset, uint64_t ct0_size0, uint64_t ct0_size1,
+                                          uint64_t ct0_stride0, uint64_t ct0_stride1, uint64_t *tlu_allocated,
+                                          uint64_t *tlu_aligned, uint64_t tlu_offset, uint64_t tlu_size,
+                                          uint64_t tlu_stride, uint32_t input_lwe_dim, uint32_t poly_size,
+                                          uint32_t level, uint32_t base_log, uint32_t glwe_dim, uint32_t bsk_index,
+                                          concrete_hip_keyset *context);
+void memref_batched_mapped_bootstrap_lwe_hip_u64(
+    uint64_t *out_allocated, uint64_t *out_aligned, uint64_t out_offset, uint64_t out_size0, uint64_t out_size1,
+    uint64_t out_stride0, uint64_t out_stride1, uint64_t *ct0_allocated, uint64_t *ct0_aligned, uint64_t ct0_offset,
+    uint64_t ct0_size0, uint64_t ct0_size1, uint64_t ct0_stride0, uint64_t ct0_stride1, uint64_t *tlu_allocated,
+    uint64_t *tlu_aligned, uint64_t tlu_offset, uint64_t tlu_size0, uint64_t tlu_size1, uint64_t tlu_stride0,
+    uint64_t tlu_stride1, uint32_t input_lwe_dim, uint32_t poly_size, uint32_t level, uint32_t base_log,
+    uint32_t glwe_dim, uint32_t bsk_index, concrete_hip_keyset *context);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,6 +66,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", type=int, default=8, help="rows checked bit-exactly against the oracle (rank 0)")
+    ap.add_argument("--no-ks", action="store_true", help="skip the secondary keyswitch measurement")
     return ap.parse_args()
 
 
@@ -149,6 +150,37 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall, kern_ms = float(t[0]), float(t[1])
 
+    # ---- secondary row: batched keyswitch kN -> n of this batch, after the PBS
+    ks_res = None
+    if not args.no_ks:
+        ksk = B.ksk_generate(p, glwe_sk, lwe_sk, 6)
+        d_ksk = B.to_device(ksk, dev)
+        d_small = torch.empty((args.batch, p.n + 1), dtype=torch.int64, device=dev)
+        for _ in range(max(1, args.warmup)):
+            B.keyswitch(p, d_ksk, d_out, out=d_small)
+        torch.cuda.synchronize()
+        kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        for a_, b_ in kev:
+            a_.record()
+            B.keyswitch(p, d_ksk, d_out, out=d_small)
+            b_.record()
+        torch.cuda.synchronize()
+        ks_ms = float(np.mean([a_.elapsed_time(b_) for a_, b_ in kev]))
+        ks_bytes = 8 * (p.ksk_len + p.lwe_out_size + p.lwe_in_size)
+        ks_rate = args.batch / (ks_ms * 1e-3)
+        ks_res = {"metric": f"KS/sec per GPU at kN={p.big_n} -> n={p.n}, l={p.ks_level} logB={p.ks_base_log}",
+                  "value": round(ks_rate, 1), "unit": "KS/s", "kernel_ms": round(ks_ms, 4),
+                  "roofline": {"bound": "hbm", "achieved": round(ks_bytes * ks_rate / 1e9, 1), "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": round(ks_bytes * ks_rate / 1e9 / HBM_PEAK_GBS, 4),
+                               "bytes_per_ks": ks_bytes}}
+        if rank == 0 and args.verify:
+            from oracle import pyoracle as O
+            op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, ks_l=p.ks_level, ks_logB=p.ks_base_log)
+            rows = B.to_host(d_out[: args.verify])
+            ks_res["bitexact"] = bool(np.array_equal(B.to_host(d_small[: args.verify]),
+                                                     O.keyswitch_batch(op, rows, ksk)))
+        del d_ksk, d_small
+
     # ---- final gather of the output rows onto rank 0 (outside the timed PBS region)
     t_gather = 0.0
     if world > 1:
@@ -217,6 +249,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_src": traffic_src,
                          "kernel_ms": round(kern_ms, 3), "bytes_per_pbs": bytes_per_pbs},
             "cpu_baseline": cpu,
+            "secondary": {"keyswitch": ks_res},
             "checks": {"decrypt_ok": f"{ok_all}/{args.batch * world}", "bitexact_rows": args.verify,
                        "bitexact": bitexact},
         }

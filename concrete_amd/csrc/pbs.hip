@@ -47,12 +47,32 @@ constexpr int limb_shift(int li) { return li * 21 + (li > 0 ? 1 : 0); }
 #define FWD_BATCH 1  // forward transforms software-pipelined together (1 or 2; 2 spills at l = 3)
 #endif
 
-// Barrier of the half-spectrum exchanges (DIAG_NOXBAR: timing-only builds without it)
-#ifdef DIAG_NOXBAR
-__device__ __forceinline__ void xchg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-#else
-__device__ __forceinline__ void xchg_barrier() { pair_barrier(); }
+#ifndef PAIR_FLAGS
+#define PAIR_FLAGS 1  // half-spectrum exchanges synchronise the two waves of a pair only
 #endif
+
+// Synchronisation point of the half-spectrum exchanges.  PAIR_FLAGS: a pair-local barrier on
+// LDS counters — each wave publishes how many sync points it has passed and waits for its
+// partner to reach the same count — so the other pairs of the workgroup are not held up.
+// Only LDS traffic is drained (lgkmcnt), never the key DMA (no release fence: that would add
+// vmcnt(0)).  LDS operations are coherent across the waves of a CU.
+// (DIAG_NOXBAR: timing-only builds without any exchange synchronisation.)
+__device__ __forceinline__ void xchg_barrier(uint32_t* flags, int w, uint32_t& cnt) {
+#if defined(DIAG_NOXBAR)
+  (void)flags, (void)w, (void)cnt;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#elif PAIR_FLAGS
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  ++cnt;
+  __hip_atomic_store(&flags[w], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (__hip_atomic_load(&flags[w ^ 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < cnt)
+    __builtin_amdgcn_s_sleep(1);
+  asm volatile("" ::: "memory");
+#else
+  (void)flags, (void)w, (void)cnt;
+  pair_barrier();
+#endif
+}
 
 template <int L, bool RESID, bool STAMPS, bool STATE32>
 __global__ void __launch_bounds__(PBS_PAIRS * 128, 2)
@@ -76,6 +96,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   cplx* T2 = T1 + 8 * T1_STRIDE;
   cplx* xch_all = T2 + 64;                       // NW x PBS1024_XCH_SLOTS: transpose scratch,
   cplx* ring = xch_all + NW * PBS1024_XCH_SLOTS;  // also the mailbox; 3 x GROUP key ring
+  uint32_t* pflags = reinterpret_cast<uint32_t*>(ring + 3 * GROUP);  // NW pair-sync counters
 
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = w & 1;  // polynomial = frequency half
@@ -108,6 +129,8 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   if (total_groups > 1) issue_group(1);
 
   build_fft512_tables(T1, T2, threadIdx.x, PBS_PAIRS * 128);
+  if (lane == 0) pflags[w] = 0u;
+  uint32_t pcnt = 0;
   __syncthreads();
   const Fft512Tables T{T1, T2};
 
@@ -208,7 +231,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             }
         }
       }
-      xchg_barrier();
+      xchg_barrier(pflags, w, pcnt);
       if (work) {
         if (h == 0) {
 #pragma unroll
@@ -222,7 +245,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             for (int j = 0; j < 4; ++j) X[0][q0 + t][j] = partnerbox[(t * 4 + j) * 64 + lane];
         }
       }
-      xchg_barrier();  // partner has read my mailbox: my scratch is free again
+      xchg_barrier(pflags, w, pcnt);  // partner has read my mailbox: my scratch is free again
     }
     if constexpr (STAMPS) {
       uint64_t t = stamp();
@@ -347,7 +370,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         acc_t[2] += t - tp;
         tp = t;
       }
-      xchg_barrier();
+      xchg_barrier(pflags, w, pcnt);
       cplx vp[8];
       if (work) {
         if (h == 0) {
@@ -364,7 +387,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
           }
         }
       }
-      xchg_barrier();  // partner has read my mailbox: my scratch is free again
+      xchg_barrier(pflags, w, pcnt);  // partner has read my mailbox: my scratch is free again
       if constexpr (STAMPS) {
         uint64_t t = stamp();
         acc_t[3] += t - tp;

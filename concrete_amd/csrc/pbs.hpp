@@ -13,7 +13,8 @@ constexpr size_t PBS1024_TABLE_BYTES = (8 * 72 + 64) * 16;  // FFT512_TABLE_ENTR
 constexpr int PBS_PAIRS = 4;                // ciphertexts (wave pairs) per workgroup
 constexpr size_t PBS1024_XCH_SLOTS = 576;  // >= XCH_SLOTS (fft512.hpp), 16-B slots per wave
 constexpr size_t pbs1024_pair_lds_bytes(int level) {
-  return PBS1024_TABLE_BYTES + 2 * PBS_PAIRS * PBS1024_XCH_SLOTS * 16 + 3 * (size_t)level * 512 * 16;
+  return PBS1024_TABLE_BYTES + 2 * PBS_PAIRS * PBS1024_XCH_SLOTS * 16 + 3 * (size_t)level * 512 * 16 +
+         2 * PBS_PAIRS * 4;  // + pair-sync counters
 }
 
 // N = 2048 kernel geometry (pbs2048.hip): four waves per ciphertext (one per even/odd half of
@@ -25,7 +26,8 @@ constexpr int PBS2_LIMBS = 4;     // 16-bit key limbs
 constexpr int PBS2_SUBS = 2;      // balanced 12-bit sub-digits per decomposition digit
 constexpr int PBS2_SUB_BITS = 12;
 constexpr size_t pbs2048_lds_bytes() {
-  return PBS1024_TABLE_BYTES + 4 * PBS2_CTS * PBS1024_XCH_SLOTS * 16 + (size_t)PBS2_RING_SLOTS * 1024 * 16;
+  return PBS1024_TABLE_BYTES + 4 * PBS2_CTS * PBS1024_XCH_SLOTS * 16 + (size_t)PBS2_RING_SLOTS * 1024 * 16 +
+         4 * PBS2_CTS * 4;  // + per-wave sync counters
 }
 
 // Number of exact limbs of the key polynomial for a parameter set.

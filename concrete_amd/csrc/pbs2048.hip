@@ -30,6 +30,21 @@ namespace chip {
 constexpr uint64_t P2_MAGIC_ALL =
     RND_MAGIC_BITS + (RND_MAGIC_BITS << 16) + (RND_MAGIC_BITS << 32) + (RND_MAGIC_BITS << 48);
 
+// Synchronisation of the four waves of one ciphertext (the exchanges never involve the other
+// ciphertext of the workgroup): each wave publishes how many sync points it has passed and
+// waits until its three partners have reached the same count.  LDS traffic is drained, the
+// key DMA is not.
+__device__ __forceinline__ void quad_sync(uint32_t* flags, int ctl, int v, uint32_t& cnt) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  ++cnt;
+  __hip_atomic_store(&flags[ctl * 4 + v], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+  for (int o = 1; o < 4; ++o)
+    while (__hip_atomic_load(&flags[ctl * 4 + ((v + o) & 3)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < cnt)
+      __builtin_amdgcn_s_sleep(1);
+  asm volatile("" ::: "memory");
+}
+
 template <bool RESID>
 __global__ void __launch_bounds__(PBS2_CTS * 256, 2)
 pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx,
@@ -52,6 +67,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   cplx* T2 = T1 + 8 * T1_STRIDE;
   cplx* xch_all = T2 + 64;                // NW x XS: transpose scratch and mailboxes
   cplx* ring = xch_all + NW * XS;         // RS x GROUP key ring
+  uint32_t* qflags = reinterpret_cast<uint32_t*>(ring + RS * GROUP);  // NW sync counters
 
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -81,6 +97,8 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     if ((uint64_t)g < total_groups) issue_group(g);
 
   build_fft512_tables(T1, T2, threadIdx.x, NW * 64);
+  if (lane == 0) qflags[w] = 0u;
+  uint32_t qcnt = 0;
   __syncthreads();
   const Fft512Tables T{T1, T2};
 
@@ -128,7 +146,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
       for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = A[m];
     }
-    pair_barrier();
+    quad_sync(qflags, ctl, v, qcnt);
     if (work) {
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
@@ -139,7 +157,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         st[m] = (uint32_t)decomp_init((sp < N ? rv : 0ull - rv) - A[m], nrep);
       }
     }
-    pair_barrier();  // every wave has read its sources: scratches are free again
+    quad_sync(qflags, ctl, v, qcnt);  // every wave has read its sources: scratches are free again
 
     // ---- one decomposition level, two sub-digit polynomials, forward transforms ----------
     // X[vv][sub][jj]: spectrum of sub-digit polynomial (virtual poly vv = 2 row + parity) at
@@ -166,14 +184,14 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
         for (int k2 = 0; k2 < 8; ++k2) xch[k2 * 64 + lane] = vv8[k2];
       }
-      pair_barrier();
+      quad_sync(qflags, ctl, v, qcnt);
       if (work) {
 #pragma unroll
         for (int vv = 0; vv < 4; ++vv)
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) X[vv][sub][jj] = ctx[vv * XS + (2 * v + jj) * 64 + lane];
       }
-      pair_barrier();
+      quad_sync(qflags, ctl, v, qcnt);
     }
 
     // ---- per limb: MAC for the four outputs on my quarter, trade quarters, inverse ---------
@@ -230,14 +248,14 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) xch[(vo * 2 + jj) * 64 + lane] = Y[vo >> 1][vo & 1][jj];
       }
-      pair_barrier();
+      quad_sync(qflags, ctl, v, qcnt);
       if (work) {
 #pragma unroll
         for (int vv = 0; vv < 4; ++vv)
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) V[2 * vv + jj] = ctx[vv * XS + (v * 2 + jj) * 64 + lane];
       }
-      pair_barrier();
+      quad_sync(qflags, ctl, v, qcnt);
       if (work) {
         fft512_inv(V, xch, T, lane);
 #pragma unroll

@@ -24,6 +24,17 @@ constexpr uint64_t RND_MAGIC_BITS = 0x4338000000000000ull;
 // no vmcnt drain (key loads may stay in flight).
 __device__ __forceinline__ void pair_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Bounded spin on an LDS counter: returns once *ctr >= target.  The bound (~2^22 polls, far
+// beyond any legitimate wait) turns a synchronisation bug into wrong results instead of a hung
+// GPU.
+__device__ __forceinline__ void spin_until_ge(const uint32_t* ctr, uint32_t target) {
+  for (uint32_t it = 0; it < (1u << 22); ++it) {
+    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
+}
+
 // Diagnostic cycle stamps (STAMPS builds only; never in the product kernel).
 __device__ __forceinline__ uint64_t stamp() {
   uint64_t t;

@@ -65,9 +65,7 @@ __device__ __forceinline__ void xchg_barrier(uint32_t* flags, int w, uint32_t& c
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   ++cnt;
   __hip_atomic_store(&flags[w], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  while (__hip_atomic_load(&flags[w ^ 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < cnt)
-    __builtin_amdgcn_s_sleep(1);
-  asm volatile("" ::: "memory");
+  spin_until_ge(&flags[w ^ 1], cnt);
 #else
   (void)flags, (void)w, (void)cnt;
   pair_barrier();
@@ -354,6 +352,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             mac();
             inv_stage();
           }
+
         }
         if (work) {
           if (c == h) {

@@ -39,10 +39,7 @@ __device__ __forceinline__ void quad_sync(uint32_t* flags, int ctl, int v, uint3
   ++cnt;
   __hip_atomic_store(&flags[ctl * 4 + v], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
-  for (int o = 1; o < 4; ++o)
-    while (__hip_atomic_load(&flags[ctl * 4 + ((v + o) & 3)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < cnt)
-      __builtin_amdgcn_s_sleep(1);
-  asm volatile("" ::: "memory");
+  for (int o = 1; o < 4; ++o) spin_until_ge(&flags[ctl * 4 + ((v + o) & 3)], cnt);
 }
 
 template <bool RESID>

@@ -181,6 +181,19 @@ def main():
                                                      O.keyswitch_batch(op, rows, ksk)))
         del d_ksk, d_small
 
+    # ---- end-to-end including PCIe: host inputs -> H2D -> PBS -> D2H -> host outputs (DESIGN.md §6;
+    # never `value`, which is the device-resident rate)
+    h_in = torch.from_numpy(cts.view(np.int64)).pin_memory()
+    h_out = torch.empty((args.batch, p.lwe_out_size), dtype=torch.int64).pin_memory()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        d_in.copy_(h_in, non_blocking=True)
+        step()
+        h_out.copy_(d_out, non_blocking=True)
+    torch.cuda.synchronize()
+    e2e = args.batch * args.steps / (time.perf_counter() - t0)
+
     # ---- final gather of the output rows onto rank 0 (outside the timed PBS region)
     t_gather = 0.0
     if world > 1:
@@ -249,7 +262,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_src": traffic_src,
                          "kernel_ms": round(kern_ms, 3), "bytes_per_pbs": bytes_per_pbs},
             "cpu_baseline": cpu,
-            "secondary": {"keyswitch": ks_res},
+            "secondary": {"keyswitch": ks_res,
+                          "pcie_inclusive_pbs_per_s": round(e2e * world, 1)},
             "checks": {"decrypt_ok": f"{ok_all}/{args.batch * world}", "bitexact_rows": args.verify,
                        "bitexact": bitexact},
         }

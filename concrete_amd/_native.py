@@ -33,6 +33,10 @@ SIGNATURES = {
     "cuda_programmable_bootstrap_lwe_ciphertext_vector_64": (
         None, [vp, u32, vp, vp, vp, vp, vp, vp, vp, vp, u32, u32, u32, u32, u32, u32, u32, u32]),
     "cuda_keyswitch_lwe_ciphertext_vector_64": (None, [vp, u32, vp, vp, vp, vp, vp, u32, u32, u32, u32, u32]),
+    "cuda_add_lwe_ciphertext_vector_64": (None, [vp, u32, vp, vp, vp, u32, u32]),
+    "cuda_add_lwe_ciphertext_vector_plaintext_vector_64": (None, [vp, u32, vp, vp, vp, u32, u32]),
+    "cuda_mult_lwe_ciphertext_vector_cleartext_vector_64": (None, [vp, u32, vp, vp, vp, u32, u32]),
+    "cuda_negate_lwe_ciphertext_vector_64": (None, [vp, u32, vp, vp, u32, u32]),
     "concrete_hip_abi_version": (u32, []),
     "concrete_hip_last_error": (C.c_char_p, []),
     "concrete_hip_pbs_supported": (i32, [u32, u32, u32, u32]),

@@ -81,6 +81,24 @@ void cuda_keyswitch_lwe_ciphertext_vector_64(void *stream, uint32_t gpu_index, v
                                              uint32_t lwe_dimension_out, uint32_t base_log,
                                              uint32_t level_count, uint32_t num_samples);
 
+/* The four linear-operation vectors of the dataflow route (GPUDFG.cpp:1286-1289, 1344-1346,
+ * 1402-1404, 1445-1446): batch-major (count, lwe_dimension + 1) u64 ciphertexts, wrapping.
+ * plaintext/cleartext arrays hold one u64 per ciphertext. */
+void cuda_add_lwe_ciphertext_vector_64(void *stream, uint32_t gpu_index, void *lwe_array_out,
+                                       const void *lwe_array_in_1, const void *lwe_array_in_2,
+                                       uint32_t input_lwe_dimension, uint32_t input_lwe_ciphertext_count);
+void cuda_add_lwe_ciphertext_vector_plaintext_vector_64(void *stream, uint32_t gpu_index, void *lwe_array_out,
+                                                        const void *lwe_array_in, const void *plaintext_array_in,
+                                                        uint32_t input_lwe_dimension,
+                                                        uint32_t input_lwe_ciphertext_count);
+void cuda_mult_lwe_ciphertext_vector_cleartext_vector_64(void *stream, uint32_t gpu_index, void *lwe_array_out,
+                                                         const void *lwe_array_in, const void *cleartext_array_in,
+                                                         uint32_t input_lwe_dimension,
+                                                         uint32_t input_lwe_ciphertext_count);
+void cuda_negate_lwe_ciphertext_vector_64(void *stream, uint32_t gpu_index, void *lwe_array_out,
+                                          const void *lwe_array_in, uint32_t input_lwe_dimension,
+                                          uint32_t input_lwe_ciphertext_count);
+
 /* ------------------------------------------------------------------------------------------
  * Part 2: extensions (return 0 on success, < 0 on error; message via concrete_hip_last_error)
  * ------------------------------------------------------------------------------------------ */

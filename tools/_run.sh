@@ -2,6 +2,5 @@ set -e -o pipefail
 TAG=${1:-x}
 O=gpurun_out/$TAG; mkdir -p $O
 timeout -k 10 600 python -m pytest tests -m gpu -q -x > $O/pytest.log 2>&1
-timeout -k 10 300 python bench.py --no-cpu-baseline --no-ks > $O/bench.log 2>&1
-timeout -k 10 300 python bench.py --config cfg4 --no-cpu-baseline --no-ks > $O/bench4.log 2>&1
+timeout -k 10 300 python bench.py > $O/bench.log 2>&1
 echo done

@@ -83,10 +83,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # one process per GPU; CONCRETE_HIP_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
+    backend = os.environ.get("CONCRETE_HIP_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     p = B.CFG2 if args.config == "cfg2" else B.CFG4
     width = 3 if args.config == "cfg2" else 5

@@ -29,11 +29,23 @@ def shard_range(total: int, world: int, rank: int) -> tuple[int, int]:
     return start, count
 
 
+def _host_staged(t, group) -> bool:
+    """gloo collectives run on host tensors: device tensors are staged through host memory."""
+    import torch.distributed as dist
+
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
 def broadcast_key(key, src: int = 0, group=None):
     """Broadcast the device-format key tensor from `src` in place (one RCCL broadcast)."""
     import torch.distributed as dist
 
-    dist.broadcast(key, src=src, group=group)
+    if _host_staged(key, group):
+        h = key.cpu()
+        dist.broadcast(h, src=src, group=group)
+        key.copy_(h)
+    else:
+        dist.broadcast(key, src=src, group=group)
     return key
 
 
@@ -54,6 +66,9 @@ def gather_rows(rows, total: int, dst: int = 0, group=None):
     if rows.shape[0] != count:
         raise ValueError(f"rank {rank}: {rows.shape[0]} rows, shard is {count}")
     cap = shard_range(total, world, 0)[1]
+    device = rows.device
+    if _host_staged(rows, group):
+        rows = rows.cpu()
     buf = rows
     if count != cap:
         buf = torch.zeros((cap, width), dtype=rows.dtype, device=rows.device)
@@ -62,7 +77,7 @@ def gather_rows(rows, total: int, dst: int = 0, group=None):
     dist.gather(buf.contiguous(), gather_list=parts, dst=dst, group=group)
     if rank != dst:
         return None
-    out = torch.empty((total, width), dtype=rows.dtype, device=rows.device)
+    out = torch.empty((total, width), dtype=rows.dtype, device=device)
     for r in range(world):
         s, c = shard_range(total, world, r)
         out[s:s + c] = parts[r][:c]

@@ -1,6 +1,5 @@
 set -e -o pipefail
 TAG=${1:-x}
 O=gpurun_out/$TAG; mkdir -p $O
-timeout -k 10 600 python -m pytest tests -m gpu -q -x > $O/pytest.log 2>&1
-timeout -k 10 300 python bench.py > $O/bench.log 2>&1
+CONCRETE_HIP_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline --batch 1024 > $O/bench_n2.log 2>&1
 echo done

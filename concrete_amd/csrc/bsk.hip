@@ -75,9 +75,10 @@ __device__ __forceinline__ double limb_value(uint64_t rem, uint32_t limb) {
 }
 
 // In-LDS radix-2 DIT over buf (bit-reversed input, natural output, forward sign), then the
-// scatter into the PBS kernels' register layout (slot-major, fft512_freq order), scaled 1/M.
-template <int M>
-__device__ __forceinline__ void dd_fft_scatter(ddc* buf, const ddc* __restrict__ tw_t, cplx* __restrict__ d) {
+// scatter into the PBS kernels' register layout: element e = (slot, lane) holds frequency
+// fft512_freq(lane, slot), scaled 1/M, stored at dst(e).
+template <int M, class Dst>
+__device__ __forceinline__ void dd_fft_scatter(ddc* buf, const ddc* __restrict__ tw_t, Dst dst) {
   for (int h = 1; h < M; h <<= 1) {
     for (int b = threadIdx.x; b < M / 2; b += blockDim.x) {
       const int grp = b / h, pos = b % h;
@@ -95,7 +96,7 @@ __device__ __forceinline__ void dd_fft_scatter(ddc* buf, const ddc* __restrict__
     const int lane = e & 63, slot = e >> 6;
     const int f = fft512_freq(lane, slot);
     const ddc x = buf[f];
-    d[e] = {(x.re.hi + x.re.lo) * scale, (x.im.hi + x.im.lo) * scale};
+    *dst(e) = {(x.re.hi + x.re.lo) * scale, (x.im.hi + x.im.lo) * scale};
   }
 }
 
@@ -105,7 +106,7 @@ __global__ void __launch_bounds__(256) convert_bsk_kernel(cplx* __restrict__ des
                                                          const ddc* __restrict__ zeta_t, const ddc* __restrict__ tw_t,
                                                          uint32_t n) {
   constexpr int M = N / 2, LOGM = (M == 512 ? 9 : (M == 1024 ? 10 : (M == 256 ? 8 : 11)));
-  constexpr int K1 = K + 1, RQ = K1 * L;
+  constexpr int K1 = K + 1;
   __shared__ ddc buf[M];
   // block = (poly, limb); poly index in the standard layout
   const uint64_t blk = blockIdx.x;
@@ -125,8 +126,17 @@ __global__ void __launch_bounds__(256) convert_bsk_kernel(cplx* __restrict__ des
     buf[r] = z;
   }
   __syncthreads();
+  // layout [n][limb][co][ro][q][slot][lane] (pbs.hip): slots 0..3 of group (limb, co, ro) hold
+  // column co / row ro, slots 4..7 hold column 1 - co / row 1 - ro (K = 1), so each wave of a
+  // pair reads "own" and "other" spectra at fixed positions
+  static_assert(K1 == 2, "own/other key layout assumes k = 1");
   const uint32_t q = (uint32_t)(L - 1) - v;
-  dd_fft_scatter<M>(buf, tw_t, dest + ((((i * K1 + col) * LIMBS + limb) * RQ) + row * L + q) * (uint64_t)M);
+  cplx* base = dest + i * (uint64_t)(LIMBS * 4 * L * M);  // per GGSW: limbs x co x ro x levels
+  dd_fft_scatter<M>(buf, tw_t, [&](int e) {
+    const int slot = e >> 6, lane = e & 63;
+    const uint32_t co = slot < 4 ? col : 1u - col, ro = slot < 4 ? row : 1u - row;
+    return base + (((uint64_t)(limb * 2 + co) * 2 + ro) * L + q) * M + slot * 64 + lane;
+  });
 }
 
 // N = 2048, k = 1, l = 1 (pbs2048.hip).  Block = (i, limb, col, row, sub, parity), in the order
@@ -154,7 +164,7 @@ __global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__
     buf[r] = z;
   }
   __syncthreads();
-  dd_fft_scatter<M>(buf, tw_t, dest + blk * M);
+  dd_fft_scatter<M>(buf, tw_t, [&](int e) { return dest + blk * M + e; });
 }
 
 template <int N, int K, int L, int LIMBS>

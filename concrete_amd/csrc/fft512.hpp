@@ -61,9 +61,20 @@ __device__ __forceinline__ cplx mul_w83(cplx a) {
   else return {(a.im - a.re) * r, (-a.re - a.im) * r};
 }
 
+// Negate a complex value when `sign` is 1ull << 63 (sign-bit XOR on both parts, no branch).
+__device__ __forceinline__ cplx cneg_if(cplx a, uint64_t sign) {
+  return {__longlong_as_double((long long)((uint64_t)__double_as_longlong(a.re) ^ sign)),
+          __longlong_as_double((long long)((uint64_t)__double_as_longlong(a.im) ^ sign))};
+}
+
 // In-register 8-point DFT, natural order in and out: X[k] = sum_m x[m] w8^{+-mk}.
-template <bool INV>
-__device__ __forceinline__ void dft8(cplx (&v)[8]) {
+// Uniform relabelings used by the wave of a pair that owns the upper frequency half
+// (sign = 1ull << 63, else 0):
+//   OUT_XOR4: outputs permuted k -> k ^ 4 (negate b1, b3, b5, b7 before the last stage);
+//   IN_XOR4:  inputs given in order m ^ 4 (the DFT of the permuted input is (-1)^k X[k]:
+//             negate b4..b7, the terms of the odd outputs).
+template <bool INV, int RELABEL = 0>
+__device__ __forceinline__ void dft8(cplx (&v)[8], uint64_t sign = 0) {
   cplx a0 = cadd(v[0], v[4]), a4 = csub(v[0], v[4]);
   cplx a1 = cadd(v[1], v[5]), a5 = csub(v[1], v[5]);
   cplx a2 = cadd(v[2], v[6]), a6 = csub(v[2], v[6]);
@@ -75,6 +86,11 @@ __device__ __forceinline__ void dft8(cplx (&v)[8]) {
   cplx b1 = cadd(a1, a3), b3 = mul_mi<INV>(csub(a1, a3));
   cplx b4 = cadd(a4, a6), b6 = csub(a4, a6);
   cplx b5 = cadd(a5, a7), b7 = mul_mi<INV>(csub(a5, a7));
+  if constexpr (RELABEL == 1) {  // OUT_XOR4
+    b1 = cneg_if(b1, sign), b3 = cneg_if(b3, sign), b5 = cneg_if(b5, sign), b7 = cneg_if(b7, sign);
+  } else if constexpr (RELABEL == 2) {  // IN_XOR4
+    b4 = cneg_if(b4, sign), b5 = cneg_if(b5, sign), b6 = cneg_if(b6, sign), b7 = cneg_if(b7, sign);
+  }
   v[0] = cadd(b0, b1);
   v[4] = csub(b0, b1);
   v[2] = cadd(b2, b3);
@@ -228,7 +244,8 @@ __device__ __forceinline__ void fwd_r2(cplx (&v)[8], const cplx* xch, int hi, in
 #define XPOSE_HI_REGS 1  // lane-bits-3..5 transposes with cross-lane moves instead of LDS
 #endif
 
-__device__ __forceinline__ void fft512_fwd(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane) {
+__device__ __forceinline__ void fft512_fwd(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane,
+                                           uint64_t out_xor4 = 0) {
   const int hi = lane >> 3, lo = lane & 7;
   fwd_p1(v, T, lane);
 #if XPOSE_HI_REGS
@@ -244,7 +261,7 @@ __device__ __forceinline__ void fft512_fwd(cplx (&v)[8], cplx* xch, const Fft512
   wave_lds_fence();
   fwd_r2(v, xch, hi, lo);
   wave_lds_fence();
-  dft8<false>(v);
+  dft8<false, 1>(v, out_xor4);  // out_xor4 = 1 << 63: slots come out in order k2 ^ 4
 }
 
 // Two independent forward transforms through ONE scratch, software-pipelined: each
@@ -283,8 +300,8 @@ __device__ __forceinline__ void fft512_fwd2(cplx (&a)[8], cplx (&b)[8], cplx* xc
 // Inverse: v[k2] = Y[k0 + 8 k1 + 64 k2] in lane (k0, k1) -> v[m] = sum_k Y_k w^{-jk} * conj(zeta^j),
 // j = t + 64 m in lane t.  Stages: P1 | W1 R1 | P2 | W2 R2 | P3 (the kernel interleaves them
 // with other work, so each is callable on its own).
-__device__ __forceinline__ void inv_p1(cplx (&v)[8], const Fft512Tables& T, int lo) {
-  dft8<true>(v);  // over k2 -> t0 ; lane (k0 = hi, k1 = lo)
+__device__ __forceinline__ void inv_p1(cplx (&v)[8], const Fft512Tables& T, int lo, uint64_t in_xor4 = 0) {
+  dft8<true, 2>(v, in_xor4);  // over k2 -> t0 ; lane (k0 = hi, k1 = lo); in_xor4: inputs in k2 ^ 4 order
 #pragma unroll
   for (int t0 = 1; t0 < 8; ++t0) v[t0] = cmulc(v[t0], T.T2[t0 * 8 + lo]);
 }
@@ -317,9 +334,10 @@ __device__ __forceinline__ void inv_p3(cplx (&v)[8]) {
   for (int m = 1; m < 8; ++m) v[m] = cmulc(v[m], psi_pow(m));
 }
 
-__device__ __forceinline__ void fft512_inv(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane) {
+__device__ __forceinline__ void fft512_inv(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane,
+                                           uint64_t in_xor4 = 0) {
   const int hi = lane >> 3, lo = lane & 7;
-  inv_p1(v, T, lo);
+  inv_p1(v, T, lo, in_xor4);
   inv_w1(v, xch, hi, lo);
   wave_lds_fence();
   inv_r1(v, xch, hi, lo);

@@ -43,9 +43,6 @@ constexpr int limb_shift(int li) { return li * 21 + (li > 0 ? 1 : 0); }
 #ifndef DIAG_NOMAC
 #define DIAG_NOMAC 0  // diagnostic builds only: skip the key MAC (wrong results)
 #endif
-#ifndef FWD_BATCH
-#define FWD_BATCH 1  // forward transforms software-pipelined together (1 or 2; 2 spills at l = 3)
-#endif
 
 #ifndef PAIR_FLAGS
 #define PAIR_FLAGS 1  // half-spectrum exchanges synchronise the two waves of a pair only
@@ -80,8 +77,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
                     const cplx* __restrict__ fbsk, uint32_t n, uint32_t base_log, uint32_t num_samples,
                     unsigned long long* __restrict__ resid_out) {
   constexpr int K = 1, K1 = 2, N = 1024, LOG2_2N = 11, LIMBS = 3, RQ = K1 * L;
-  constexpr int SLICE = RQ * 512;            // complex values per (column, limb) key slice
-  constexpr int PER_I = K1 * LIMBS * SLICE;  // complex values per Fourier GGSW
+  constexpr int PER_I = K1 * LIMBS * RQ * 512;  // complex values per Fourier GGSW
   static_assert(XCH_SLOTS <= (int)PBS1024_XCH_SLOTS, "transpose scratch");
   constexpr int NW = 2 * PBS_PAIRS;           // waves per workgroup
   constexpr int GROUP = L * 512;              // complex values per ring group (one row of a slice)
@@ -98,6 +94,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = w & 1;  // polynomial = frequency half
+  const uint64_t hsign = (uint64_t)h << 63;  // sign mask of the k2 ^ 4 relabeling (h = 1)
   const int lane = threadIdx.x & 63;
   const uint32_t s = blockIdx.x * PBS_PAIRS + (w >> 1);
   const bool active = s < num_samples;
@@ -106,16 +103,15 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   cplx* mybox = xch;                                  // the half-spectrum mailbox is the
   const cplx* partnerbox = xch_all + (w ^ 1) * PBS1024_XCH_SLOTS;   // transpose scratch, between transforms
 
-  // ---- key ring: group g = (step g / NGRP, slice (g % NGRP) / 2, row g % 2) -> slot g % 3 ----
-  // slice order (c, li) = (0,0), (1,0), (0,1), (1,1), ... : both waves of a pair read the same
-  // slice at the same time (their own halves of its frequency slots)
+  // ---- key ring: group g = (step g / NGRP, limb, co, ro) -> slot g % 3 ---------------------
+  // Both waves of a pair read the same group at the same time, each its own half of the slots:
+  // group (li, co, ro) holds, for slots 0..3, column co / row ro and, for slots 4..7, column
+  // 1 - co / row 1 - ro, i.e. "own"/"other" relative to the reading wave (bsk.hip).
   const uint64_t total_groups = (uint64_t)n * NGRP;
   auto issue_group = [&](uint64_t g) {
     const uint64_t i = g / NGRP;
-    const int r = (int)(g % NGRP);
-    const int sl = r >> 1, row = r & 1;
-    const int c = sl % K1, li = sl / K1;
-    const cplx* src = fbsk + i * (uint64_t)PER_I + (c * LIMBS + li) * SLICE + row * GROUP;
+    const int r = (int)(g % NGRP);  // (limb, co, ro) in consumption order = storage order
+    const cplx* src = fbsk + i * (uint64_t)PER_I + r * GROUP;
     cplx* dst = ring + (int)(g % 3) * GROUP;
 #pragma unroll
     for (int j = 0; j < GLDS; ++j) {
@@ -191,57 +187,31 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     }
 
     // ---- forward transforms; keep my half of the slots, mail the other half -------------
-    // X[row][q][j]: digit spectrum (row, level q) at slot k2 = 4h + j.  Levels are transformed
-    // two at a time (software-pipelined through the one scratch), then both halves traded.
-    cplx X[K1][L][4];
+    // Xo[q][j] / Xp[q][j]: spectrum of my own / my partner's digit polynomial (level q) at
+    // frequency slot 4h + j.  The wave owning the upper half (h = 1) emits its spectrum in slot
+    // order k2 ^ 4, so every wave keeps v[0..3] and mails v[4..7]: no h-dependent registers.
+    cplx Xo[L][4], Xp[L][4];
 #pragma unroll
-    for (int q0 = 0; q0 < L; q0 += FWD_BATCH) {
-      const int NQ = (q0 + 1 < L) ? FWD_BATCH : 1;
+    for (int q = 0; q < L; ++q) {
       if (work) {
         // digits of level l - q (the decomposition iterator yields the least significant first)
-        cplx v[2][8];
+        cplx v[8];
+        int32_t d[16];
 #pragma unroll
-        for (int t = 0; t < NQ; ++t) {
-          int32_t d[16];
+        for (int m = 0; m < 16; ++m) d[m] = decomp_next_t(st[m], logB);
 #pragma unroll
-          for (int m = 0; m < 16; ++m) d[m] = decomp_next_t(st[m], logB);
+        for (int m = 0; m < 8; ++m) v[m] = {(double)d[m], (double)d[m + 8]};
+        fft512_fwd(v, xch, T, lane, hsign);
 #pragma unroll
-          for (int m = 0; m < 8; ++m) v[t][m] = {(double)d[m], (double)d[m + 8]};
-        }
-        if (NQ == 2) fft512_fwd2(v[0], v[1], xch, T, lane);
-        else fft512_fwd(v[0], xch, T, lane);
-        // (X is indexed by the uniform h through branches: a dynamic index would put X in scratch)
-        if (h == 0) {
-#pragma unroll
-          for (int t = 0; t < NQ; ++t)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              X[0][q0 + t][j] = v[t][j];
-              mybox[(t * 4 + j) * 64 + lane] = v[t][4 + j];
-            }
-        } else {
-#pragma unroll
-          for (int t = 0; t < NQ; ++t)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              X[1][q0 + t][j] = v[t][4 + j];
-              mybox[(t * 4 + j) * 64 + lane] = v[t][j];
-            }
+        for (int j = 0; j < 4; ++j) {
+          Xo[q][j] = v[j];
+          mybox[j * 64 + lane] = v[4 + j];
         }
       }
       xchg_barrier(pflags, w, pcnt);
       if (work) {
-        if (h == 0) {
 #pragma unroll
-          for (int t = 0; t < NQ; ++t)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) X[1][q0 + t][j] = partnerbox[(t * 4 + j) * 64 + lane];
-        } else {
-#pragma unroll
-          for (int t = 0; t < NQ; ++t)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) X[0][q0 + t][j] = partnerbox[(t * 4 + j) * 64 + lane];
-        }
+        for (int j = 0; j < 4; ++j) Xp[q][j] = partnerbox[j * 64 + lane];
       }
       xchg_barrier(pflags, w, pcnt);  // partner has read my mailbox: my scratch is free again
     }
@@ -280,14 +250,16 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     static_for<0, LIMBS>([&](auto LI) __attribute__((always_inline)) {
       constexpr int li = decltype(LI)::value;
       cplx Ymine[4];
+      // co / ro: my own (0) or my partner's (1) output polynomial / input row; group
+      // (li, co, ro) holds exactly those spectra for both halves (layout: bsk.hip)
 #pragma unroll
-      for (int c = 0; c < K1; ++c) {
+      for (int co = 0; co < K1; ++co) {
         cplx Y[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) Y[j] = {0.0, 0.0};
 #pragma unroll
-        for (int row = 0; row < K1; ++row) {
-          const uint64_t g = (uint64_t)i * NGRP + (li * K1 + c) * K1 + row;
+        for (int ro = 0; ro < K1; ++ro) {
+          const uint64_t g = (uint64_t)i * NGRP + (li * K1 + co) * K1 + ro;
           // group g landed for this wave's pieces (group g + 1 may stay in flight) ...
           if (g + 1 < total_groups) wait_vmcnt<GLDS>();
           else wait_vmcnt<0>();
@@ -315,7 +287,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                   const cplx gv = G[(q * 8 + j) * 64];
-                  const cplx x = X[row][q][j];
+                  const cplx x = ro == 0 ? Xo[q][j] : Xp[q][j];
                   Y[j].re = __builtin_fma(x.re, gv.re, __builtin_fma(-x.im, gv.im, Y[j].re));
                   Y[j].im = __builtin_fma(x.re, gv.im, __builtin_fma(x.im, gv.re, Y[j].im));
                 }
@@ -324,7 +296,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             // left the data in my scratch): pass 2 in window 0, pass 3 in window 1
             auto inv_stage = [&]() __attribute__((always_inline)) {
               if constexpr (li > 0) {
-                const int win = c * K1 + row;
+                const int win = co * K1 + ro;
                 if (win == 0) {
                   cplx vp[8];
                   wave_lds_fence();
@@ -355,7 +327,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 
         }
         if (work) {
-          if (c == h) {
+          if (co == 0) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) Ymine[j] = Y[j];
           } else {
@@ -370,20 +342,13 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         tp = t;
       }
       xchg_barrier(pflags, w, pcnt);
+      // my output polynomial's spectrum, slots in order k2 ^ 4h (undone by the inverse pass 1)
       cplx vp[8];
       if (work) {
-        if (h == 0) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            vp[j] = Ymine[j];
-            vp[4 + j] = partnerbox[j * 64 + lane];
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            vp[j] = partnerbox[j * 64 + lane];
-            vp[4 + j] = Ymine[j];
-          }
+        for (int j = 0; j < 4; ++j) {
+          vp[j] = Ymine[j];
+          vp[4 + j] = partnerbox[j * 64 + lane];
         }
       }
       xchg_barrier(pflags, w, pcnt);  // partner has read my mailbox: my scratch is free again
@@ -394,11 +359,11 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
       }
       if (work) {
         if constexpr (li == LIMBS - 1) {
-          fft512_inv(vp, xch, T, lane);
+          fft512_inv(vp, xch, T, lane, hsign);
           recombine(vp, LI);
         } else {
           // pass 1 now; passes 2 and 3 ride in the next limb's first two key windows
-          inv_p1(vp, T, lo);
+          inv_p1(vp, T, lo, hsign);
           inv_w1(vp, xch, hi, lo);
           wave_lds_fence();
         }

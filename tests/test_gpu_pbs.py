@@ -93,25 +93,29 @@ def run_oracle(oracle, S, cts, luts, lut_idx=None, in_idx=None, out_idx=None):
 
 def test_fourier_key_matches_oracle_transform(B, small, torch_cuda):
     """Device conversion (double-double FFT) == oracle extended-precision transform, reordered
-    into the kernel's (lane, slot) layout; both are within ~1 ulp of the exact spectrum."""
+    into the kernel's layout [n][limb][co][ro][q][slot][lane]: slots 0..3 of group (limb, co,
+    ro) hold column co / row ro, slots 4..7 column 1 - co / row 1 - ro; both transforms are
+    within ~1 ulp of the exact spectrum."""
     p = small.p
-    g = B.to_host(small.fbsk).view(np.float64).reshape(p.n, p.k + 1, 3, (p.k + 1) * p.level, 8, 64, 2)
-    o = small.fbsk_cpu.reshape(p.n, p.level, p.k + 1, p.k + 1, 3, 2, 512)
+    L = p.level
+    g = B.to_host(small.fbsk).view(np.float64).reshape(p.n, 3, 2, 2, L, 8, 64, 2)
+    o = small.fbsk_cpu.reshape(p.n, L, p.k + 1, p.k + 1, 3, 2, 512)
     lane = np.arange(64)
     slot = np.arange(8)
     K = (lane[None, :] >> 3) + 8 * (lane[None, :] & 7) + 64 * slot[:, None]  # (8, 64)
     maxrel = 0.0
-    for v in range(p.level):
-        for row in range(p.k + 1):
-            rq = row * p.level + (p.level - 1 - v)
-            for col in range(p.k + 1):
-                for li in range(3):
-                    ref_re = o[:, v, row, col, li, 0][:, K]
-                    ref_im = o[:, v, row, col, li, 1][:, K]
-                    got = g[:, col, li, rq]
-                    scale = np.max(np.abs(o[:, v, row, col, li]))
-                    err = max(np.max(np.abs(got[..., 0] - ref_re)), np.max(np.abs(got[..., 1] - ref_im)))
-                    maxrel = max(maxrel, err / scale)
+    for v in range(L):
+        q = L - 1 - v
+        for li in range(3):
+            for co in range(2):
+                for ro in range(2):
+                    for s0, (row, col) in ((slice(0, 4), (ro, co)), (slice(4, 8), (1 - ro, 1 - co))):
+                        ref_re = o[:, v, row, col, li, 0][:, K[s0]]
+                        ref_im = o[:, v, row, col, li, 1][:, K[s0]]
+                        got = g[:, li, co, ro, q, s0]
+                        scale = np.max(np.abs(o[:, v, row, col, li]))
+                        err = max(np.max(np.abs(got[..., 0] - ref_re)), np.max(np.abs(got[..., 1] - ref_im)))
+                        maxrel = max(maxrel, err / scale)
     assert maxrel < 4e-16, maxrel
 
 

@@ -44,6 +44,9 @@ constexpr int limb_shift(int li) { return li * 21 + (li > 0 ? 1 : 0); }
 #define DIAG_NOMAC 0  // diagnostic builds only: skip the key MAC (wrong results)
 #endif
 
+#ifndef FWD_XBATCH
+#define FWD_XBATCH 2  // forward levels traded per exchange (mailbox: 4 KB per level, <= 2)
+#endif
 #ifndef PAIR_FLAGS
 #define PAIR_FLAGS 1  // half-spectrum exchanges synchronise the two waves of a pair only
 #endif
@@ -191,27 +194,45 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     // frequency slot 4h + j.  The wave owning the upper half (h = 1) emits its spectrum in slot
     // order k2 ^ 4, so every wave keeps v[0..3] and mails v[4..7]: no h-dependent registers.
     cplx Xo[L][4], Xp[L][4];
+    // levels are traded in batches of up to FWD_XBATCH (one mailbox of 4 KB per level): the
+    // mailed halves of a batch wait in registers until its last transform is done
+    constexpr int XB = FWD_XBATCH;
 #pragma unroll
-    for (int q = 0; q < L; ++q) {
+    for (int q0 = 0; q0 < L; q0 += XB) {
+      const int nq = (q0 + XB <= L) ? XB : L - q0;
+      cplx out[XB][4];
       if (work) {
-        // digits of level l - q (the decomposition iterator yields the least significant first)
-        cplx v[8];
-        int32_t d[16];
 #pragma unroll
-        for (int m = 0; m < 16; ++m) d[m] = decomp_next_t(st[m], logB);
+        for (int t = 0; t < XB; ++t) {
+          if (t < nq) {
+            // digits of level l - q (the decomposition iterator yields the least significant first)
+            cplx v[8];
+            int32_t d[16];
 #pragma unroll
-        for (int m = 0; m < 8; ++m) v[m] = {(double)d[m], (double)d[m + 8]};
-        fft512_fwd(v, xch, T, lane, hsign);
+            for (int m = 0; m < 16; ++m) d[m] = decomp_next_t(st[m], logB);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          Xo[q][j] = v[j];
-          mybox[j * 64 + lane] = v[4 + j];
+            for (int m = 0; m < 8; ++m) v[m] = {(double)d[m], (double)d[m + 8]};
+            fft512_fwd(v, xch, T, lane, hsign);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              Xo[q0 + t][j] = v[j];
+              out[t][j] = v[4 + j];
+            }
+          }
         }
+#pragma unroll
+        for (int t = 0; t < XB; ++t)
+          if (t < nq)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) mybox[(t * 4 + j) * 64 + lane] = out[t][j];
       }
       xchg_barrier(pflags, w, pcnt);
       if (work) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) Xp[q][j] = partnerbox[j * 64 + lane];
+        for (int t = 0; t < XB; ++t)
+          if (t < nq)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) Xp[q0 + t][j] = partnerbox[(t * 4 + j) * 64 + lane];
       }
       xchg_barrier(pflags, w, pcnt);  // partner has read my mailbox: my scratch is free again
     }

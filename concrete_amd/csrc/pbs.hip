@@ -105,6 +105,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   uint64_t* xch64 = reinterpret_cast<uint64_t*>(xch);
   cplx* mybox = xch;                                  // the half-spectrum mailbox is the
   const cplx* partnerbox = xch_all + (w ^ 1) * PBS1024_XCH_SLOTS;   // transpose scratch, between transforms
+  cplx* partnermail = xch_all + (w ^ 1) * PBS1024_XCH_SLOTS;
 
   // ---- key ring: group g = (step g / NGRP, limb, co, ro) -> slot g % 3 ---------------------
   // Both waves of a pair read the same group at the same time, each its own half of the slots:
@@ -352,8 +353,10 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
             for (int j = 0; j < 4; ++j) Ymine[j] = Y[j];
           } else {
+            // straight into my partner's mailbox (its scratch has been idle since the key
+            // windows' workgroup barriers), so no "partner has read" sync is needed afterwards
 #pragma unroll
-            for (int j = 0; j < 4; ++j) mybox[j * 64 + lane] = Y[j];
+            for (int j = 0; j < 4; ++j) partnermail[j * 64 + lane] = Y[j];
           }
         }
       }
@@ -369,10 +372,12 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           vp[j] = Ymine[j];
-          vp[4 + j] = partnerbox[j * 64 + lane];
+          vp[4 + j] = mybox[j * 64 + lane];
         }
       }
-      xchg_barrier(pflags, w, pcnt);  // partner has read my mailbox: my scratch is free again
+      // no second sync: the only writes into my scratch by my partner are these Y mailboxes,
+      // one per limb, always behind key-window workgroup barriers (the forward exchange only
+      // reads the partner's scratch, under its own two syncs)
       if constexpr (STAMPS) {
         uint64_t t = stamp();
         acc_t[3] += t - tp;

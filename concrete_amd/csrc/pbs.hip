@@ -235,7 +235,9 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
             for (int j = 0; j < 4; ++j) Xp[q0 + t][j] = partnerbox[(t * 4 + j) * 64 + lane];
       }
-      xchg_barrier(pflags, w, pcnt);  // partner has read my mailbox: my scratch is free again
+      // partner has read my mailbox before my next transform writes the scratch; after the last
+      // batch the scratch is next written behind the key windows' workgroup barriers
+      if (q0 + XB < L) xchg_barrier(pflags, w, pcnt);
     }
     if constexpr (STAMPS) {
       uint64_t t = stamp();

@@ -76,6 +76,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   cplx* xch = xch_all + w * XS;
   uint64_t* xch64 = reinterpret_cast<uint64_t*>(xch);
   const cplx* ctx = xch_all + ctl * 4 * XS;  // the four scratches of this ciphertext
+  cplx* ctxw = xch_all + ctl * 4 * XS;
 
   const uint64_t total_groups = (uint64_t)n * NGRP;
   auto issue_group = [&](uint64_t g) {
@@ -188,7 +189,9 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) X[vv][sub][jj] = ctx[vv * XS + (2 * v + jj) * 64 + lane];
       }
-      quad_sync(qflags, ctl, v, qcnt);
+      // everyone has read my spectrum before my next transform writes the scratch; after the
+      // last sub-digit the scratches are next written behind the key windows' barriers
+      if (sub + 1 < PBS2_SUBS) quad_sync(qflags, ctl, v, qcnt);
     }
 
     // ---- per limb: MAC for the four outputs on my quarter, trade quarters, inverse ---------
@@ -239,20 +242,21 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         for (int cc = 0; cc < K1; ++cc)
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) Y[cc][0][jj] = cadd(Y[cc][0][jj], cmul(P[cc][jj], alpha[jj]));
-        // my quarter of every output: mailbox slot (output vo, slot jj)
+        // my quarter of output vo goes straight into wave vo's mailbox, slot pair (v, jj): every
+        // scratch has been idle since the key windows' workgroup barriers, and nobody writes it
+        // again before the next limb's windows, so one sync suffices
 #pragma unroll
         for (int vo = 0; vo < 4; ++vo)
 #pragma unroll
-          for (int jj = 0; jj < 2; ++jj) xch[(vo * 2 + jj) * 64 + lane] = Y[vo >> 1][vo & 1][jj];
+          for (int jj = 0; jj < 2; ++jj) ctxw[vo * XS + (v * 2 + jj) * 64 + lane] = Y[vo >> 1][vo & 1][jj];
       }
       quad_sync(qflags, ctl, v, qcnt);
       if (work) {
 #pragma unroll
         for (int vv = 0; vv < 4; ++vv)
 #pragma unroll
-          for (int jj = 0; jj < 2; ++jj) V[2 * vv + jj] = ctx[vv * XS + (v * 2 + jj) * 64 + lane];
+          for (int jj = 0; jj < 2; ++jj) V[2 * vv + jj] = xch[(vv * 2 + jj) * 64 + lane];
       }
-      quad_sync(qflags, ctl, v, qcnt);
       if (work) {
         fft512_inv(V, xch, T, lane);
 #pragma unroll

@@ -43,7 +43,7 @@ __device__ __forceinline__ uint64_t stamp() {
   __builtin_amdgcn_sched_barrier(0);
   return t;
 }
-constexpr int NSTAMP = 8;  // rot+decomp, fwd+xchg, mac+vmcnt, y-xchg, inv+recomb, ring barrier, total, steps
+constexpr int NSTAMP = 10;  // rot+decomp, fwd+xchg, mac, y-xchg, inv+recomb, ring barrier, total, steps, vmcnt, -
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 

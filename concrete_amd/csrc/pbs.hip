@@ -150,7 +150,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   const int nrep = 64 - L * (int)base_log;
   const int logB = (int)base_log;
   double max_resid = 0.0;
-  uint64_t acc_t[NSTAMP] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t acc_t[NSTAMP] = {};
   uint64_t t_begin = 0, tp = 0;
   if constexpr (STAMPS) t_begin = stamp();
 
@@ -158,6 +158,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   for (uint32_t i = 0; i < n; ++i) {
     const uint64_t ai = a_next;
     if (i + 1 < n) a_next = active ? lwe[i + 1] : 0ull;
+
     const uint32_t at = modswitch(ai, LOG2_2N);
     // tfhe skips a zero mask element; at == 0 gives X^0 acc - acc = 0 whose product is 0.
     // The condition depends only on the ciphertext (uniform across the pair); a skipping pair
@@ -284,12 +285,17 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
         for (int ro = 0; ro < K1; ++ro) {
           const uint64_t g = (uint64_t)i * NGRP + (li * K1 + co) * K1 + ro;
+          if constexpr (STAMPS) {
+            uint64_t t = stamp();
+            acc_t[2] += t - tp;
+            tp = t;
+          }
           // group g landed for this wave's pieces (group g + 1 may stay in flight) ...
           if (g + 1 < total_groups) wait_vmcnt<GLDS>();
           else wait_vmcnt<0>();
           if constexpr (STAMPS) {
             uint64_t t = stamp();
-            acc_t[2] += t - tp;
+            acc_t[8] += t - tp;
             tp = t;
           }
           // ... and for every wave's pieces; everyone is also done with group g - 1
@@ -306,15 +312,21 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
           if (work) {
             auto mac = [&]() __attribute__((always_inline)) {
               const cplx* G = ring + (int)(g % 3) * GROUP + (4 * h) * 64 + lane;
+              // all key values of the window first, then the FMAs
+              cplx gv[L][4];
 #pragma unroll
-              for (int q = 0; q < (DIAG_NOMAC ? 0 : L); ++q)
+              for (int q = 0; q < L; ++q)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) gv[q][j] = G[(q * 8 + j) * 64];
+#pragma unroll
+              for (int q = 0; q < (DIAG_NOMAC ? 0 : L); ++q) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                  const cplx gv = G[(q * 8 + j) * 64];
                   const cplx x = ro == 0 ? Xo[q][j] : Xp[q][j];
-                  Y[j].re = __builtin_fma(x.re, gv.re, __builtin_fma(-x.im, gv.im, Y[j].re));
-                  Y[j].im = __builtin_fma(x.re, gv.im, __builtin_fma(x.im, gv.re, Y[j].im));
+                  Y[j].re = __builtin_fma(x.re, gv[q][j].re, __builtin_fma(-x.im, gv[q][j].im, Y[j].re));
+                  Y[j].im = __builtin_fma(x.re, gv[q][j].im, __builtin_fma(x.im, gv[q][j].re, Y[j].im));
                 }
+              }
             };
             // deferred inverse transform of limb li - 1 (its pass 1 ran before this limb and
             // left the data in my scratch): pass 2 in window 0, pass 3 in window 1
@@ -348,6 +360,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             mac();
             inv_stage();
           }
+
 
         }
         if (work) {
@@ -459,7 +472,7 @@ template <int L>
 static int launch_pair(const PbsArgs& a) {
   if (a.num_samples == 0) return 0;
   // diagnostic: CONCRETE_HIP_PBS_STAMPS=1 runs the s_memtime-instrumented build; `resid` must then
-  // point at 2 * PBS_PAIRS * ceil(num_samples / PBS_PAIRS) * 8 u64 (per-wave cycle sums per phase)
+  // point at 2 * PBS_PAIRS * ceil(num_samples / PBS_PAIRS) * NSTAMP u64 (per-wave cycle sums)
   static const bool stamps = getenv("CONCRETE_HIP_PBS_STAMPS") && atoi(getenv("CONCRETE_HIP_PBS_STAMPS"));
   if (stamps) return launch_pair_t<L, true, true>(a);
   return a.resid ? launch_pair_t<L, true, false>(a) : launch_pair_t<L, false, false>(a);

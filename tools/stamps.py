@@ -13,16 +13,18 @@ rng = np.random.RandomState(0)
 cts = B.lwe_encrypt(lwe_sk, [B.encode(m, 3) for m in rng.randint(0, 8, nb)], p.n, B.secure_std(1, p.n), 5)
 acc = B.trivial_glwe(p, B.expand_lut(np.arange(8, dtype=np.uint64), p.N, 3))
 nw = 2 * ((nb + 3) // 4) * 4  # pair kernel: two waves per ciphertext, 4 pairs per workgroup
-buf = torch.zeros(nw * 8, dtype=torch.int64, device="cuda:0")
+NS = 10  # kernel_util.hpp NSTAMP
+buf = torch.zeros(nw * NS, dtype=torch.int64, device="cuda:0")
 d_in, d_lut = B.to_device(cts, "cuda:0"), B.to_device(acc[None, :], "cuda:0")
 B.pbs(p, fbsk, d_in, d_lut, resid=buf); torch.cuda.synchronize()
 buf.zero_()
 t0 = torch.cuda.Event(enable_timing=True); t1 = torch.cuda.Event(enable_timing=True)
 t0.record(); B.pbs(p, fbsk, d_in, d_lut, resid=buf); t1.record(); torch.cuda.synchronize()
-st = buf.cpu().numpy().reshape(nw, 8).astype(np.float64)
-names = ["rot+decomp", "fwd+xchg", "mac+vmcnt", "y-xchg", "inv+recomb", "ring-barrier", "total", "work_steps"]
+st = buf.cpu().numpy().reshape(nw, NS).astype(np.float64)
+names = ["rot+decomp", "fwd+xchg", "mac", "y-xchg", "inv+recomb", "ring-barrier", "total", "work_steps", "vmcnt-wait"]
 tot = st[:, 6].mean()
 print(f"kernel {t0.elapsed_time(t1):.2f} ms (stamp build), batch {nb}, mean wave cycles {tot:.3g} (memtime ticks)")
-for k, nme in enumerate(names[:6]):
+for k in (0, 1, 2, 8, 3, 4, 5):
+    nme = names[k]
     print(f"  {nme:14s} {st[:, k].mean() / tot * 100:6.1f} %   per step {st[:, k].mean() / p.n:9.0f}")
 print(f"  work steps {st[:, 7].mean():.1f}")

@@ -302,3 +302,25 @@ def test_keyswitch_bit_exact_and_chain(B, oracle, cfg2, torch_cuda):
         out = run_gpu(B, cfg2, small_cts, acc, torch_cuda)      # layer 2
         dec = B.lwe_decrypt(cfg2.glwe_sk, out, p.big_n)
         assert [B.decode(d, width) for d in dec] == c["expected"], c["description"]
+
+
+def test_configs2_total_batch_65536(B, oracle, cfg2, torch_cuda):
+    """BASELINE configs[2]'s whole batch (65,536 PBS) in one launch on one GPU: every sample
+    decrypts to LUT[m], 8 random rows bit-exact, outputs of identical inputs identical."""
+    width = 3
+    nb = 65536
+    rng = np.random.RandomState(21)
+    table = rng.randint(0, 8, size=8)
+    msgs = rng.randint(0, 8, size=nb)
+    cts = encrypt(B, cfg2, msgs, width, 2121)
+    cts[nb - 1] = cts[0]
+    msgs[nb - 1] = msgs[0]
+    acc = lut_acc(B, cfg2, table, width)
+    got = run_gpu(B, cfg2, cts, acc, torch_cuda)
+    dec = B.lwe_decrypt(cfg2.glwe_sk, got, cfg2.p.big_n)
+    bad = [s for s, (d, m) in enumerate(zip(dec, msgs)) if B.decode(d, width) != table[m]]
+    assert not bad, (len(bad), bad[:8])
+    assert np.array_equal(got[0], got[nb - 1])
+    pick = rng.choice(nb, size=8, replace=False)
+    ref = run_oracle(oracle, cfg2, cts[pick], acc)
+    assert np.array_equal(got[pick], ref)

@@ -171,6 +171,11 @@ def _gpu_index(device) -> int:
     return torch.device(device).index or 0
 
 
+def pbs_supported(p: PbsParams) -> bool:
+    """Whether the kernels take this parameter set (and compute it exactly: pbs.hpp)."""
+    return bool(_native.lib().concrete_hip_pbs_supported(p.k, p.N, p.level, p.base_log))
+
+
 def fourier_bsk_bytes(p: PbsParams) -> int:
     return int(_native.lib().concrete_hip_fourier_bsk_size_bytes(p.n, p.k, p.level, p.N))
 

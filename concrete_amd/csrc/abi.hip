@@ -41,7 +41,7 @@ static void set_device(uint32_t gpu) { CHIP_CHECK(hipSetDevice((int)gpu)); }
 
 static bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
   if (k != 1 || base_log < 1) return false;
-  if (N == 1024) return level >= 1 && level <= 3 && base_log <= 30 && level * base_log < 64;
+  if (N == 1024) return pbs1024_exact(k, level, base_log);
   // N = 2048: one level whose digit splits into two 12-bit sub-digits (pbs2048.hip)
   if (N == 2048) return level == 1 && base_log <= 2 * PBS2_SUB_BITS;
   return false;

@@ -454,8 +454,12 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 template <int L, bool RESID, bool STAMPS>
 static int launch_pair_t(const PbsArgs& a) {
   const size_t lds = pbs1024_pair_lds_bytes(L);
-  auto kern = L * a.base_log <= 31 ? pbs1024_pair_kernel<L, RESID, STAMPS, true>
-                                   : pbs1024_pair_kernel<L, RESID, STAMPS, false>;
+  // the exactness gate (pbs1024_exact) keeps l * logB <= 27: the decomposer state fits 32 bits
+  if (!pbs1024_exact(1, L, a.base_log)) {
+    set_error("pbs: N=1024 l=%d logB=%u is outside the exact range", L, a.base_log);
+    return -2;
+  }
+  auto kern = pbs1024_pair_kernel<L, RESID, STAMPS, true>;
   CHIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const uint32_t blocks = (a.num_samples + PBS_PAIRS - 1) / PBS_PAIRS;
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(PBS_PAIRS * 128), lds, a.stream, a.out, a.out_idx, a.luts, a.lut_idx,

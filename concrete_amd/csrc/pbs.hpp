@@ -37,6 +37,15 @@ inline uint32_t default_limbs(uint32_t N, uint32_t level, uint32_t base_log) {
   return N <= 1024 ? 3u : (uint32_t)PBS2_LIMBS;
 }
 
+// N = 1024 exactness gate.  The 3-limb product's certified rounding bound grows with the number
+// of digit rows (k+1)l and the digit magnitude 2^(logB-1): measured on random keys it is
+// 0.044 at l=3/logB=7 (cfg2) and ~0.22-0.24 at (k+1) l 2^logB = 4096 (oracle fft_error_bound;
+// DESIGN.md §3).  Sets beyond that could round a coefficient the wrong way, so they are refused.
+inline bool pbs1024_exact(uint32_t k, uint32_t level, uint32_t base_log) {
+  return level >= 1 && level <= 3 && base_log >= 1 && base_log <= 11 &&
+         ((uint64_t)(k + 1) * level << base_log) <= 4096ull;
+}
+
 // Size in bytes of the device Fourier bootstrapping key.
 //   N = 1024: [n][col][limb][row*l + q][512] complex f64
 //   N = 2048 (l = 1): [n][limb][col][row][sub][parity][512] complex f64 (pbs2048.hip)

@@ -150,6 +150,28 @@ def test_pbs_bit_exact_cfg2(B, oracle, cfg2, torch_cuda):
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
 
 
+@pytest.mark.parametrize("level,base_log", [(1, 11), (1, 5), (2, 10), (2, 6), (3, 9), (3, 3)])
+def test_pbs_bit_exact_other_decompositions(B, oracle, torch_cuda, level, base_log):
+    """The L = 1 / 2 / 3 kernel instantiations across the exact range of the gate
+    ((k+1) l 2^logB <= 4096, pbs.hpp pbs1024_exact), each against the oracle bit for bit."""
+    p = replace(B.CFG2, n=16, level=level, base_log=base_log)
+    assert B.pbs_supported(p)
+    S = Setup(B, oracle, torch_cuda, p, 3000 + 10 * level + base_log)
+    width = 2
+    rng = np.random.RandomState(base_log)
+    table = rng.randint(0, 4, size=4)
+    msgs = rng.randint(0, 4, size=40)
+    cts = encrypt(B, S, msgs, width, 41, std=2.0 ** -25)
+    acc = lut_acc(B, S, table, width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    assert np.array_equal(got, run_oracle(oracle, S, cts, acc))
+    bound = oracle.fft_error_bound(S.op, S.fbsk_cpu)
+    assert resid < bound < 0.5, (resid, bound)
+    if level * base_log >= 15:  # coarser decompositions do not decrypt (approximation noise)
+        dec = B.lwe_decrypt(S.glwe_sk, got, p.big_n)
+        assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+
+
 def test_pbs_edge_inputs(B, oracle, small, torch_cuda):
     """Zero mask elements (tfhe skip rule), mask elements whose modulus switch is 0 or 2N-1,
     body near 2^64 (modulus switch wraps to 2N), all-zero and all-ones ciphertexts."""

@@ -25,6 +25,12 @@ def test_abi_version_and_queries():
     assert L.concrete_hip_abi_version() == 1
     assert L.concrete_hip_pbs_supported(1, 1024, 3, 7) == 1
     assert L.concrete_hip_pbs_supported(1, 1024, 3, 30) == 0  # l * logB >= 64
+    # the exactness gate: (k+1) l 2^logB <= 4096 (3-limb rounding bound < 1/4)
+    assert L.concrete_hip_pbs_supported(1, 1024, 3, 9) == 1
+    assert L.concrete_hip_pbs_supported(1, 1024, 3, 10) == 0
+    assert L.concrete_hip_pbs_supported(1, 1024, 2, 10) == 1
+    assert L.concrete_hip_pbs_supported(1, 1024, 1, 11) == 1
+    assert L.concrete_hip_pbs_supported(1, 1024, 1, 15) == 0
     assert L.concrete_hip_pbs_supported(2, 1024, 3, 7) == 0
     assert L.concrete_hip_bsk_limbs(1024, 3, 7) == 3
     p = B.CFG2

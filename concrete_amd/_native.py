@@ -41,6 +41,8 @@ SIGNATURES = {
     "concrete_hip_last_error": (C.c_char_p, []),
     "concrete_hip_pbs_supported": (i32, [u32, u32, u32, u32]),
     "concrete_hip_bsk_limbs": (u32, [u32, u32, u32]),
+    "concrete_hip_bsk_format": (C.c_int, [u32, u32, u32, C.POINTER(u32), C.POINTER(u32)]),
+    "concrete_hip_generic_error_bound": (C.c_double, [u32, u32, u32, u32, C.c_double]),
     "concrete_hip_fourier_bsk_size_bytes": (u64, [u32, u32, u32, u32]),
     "concrete_hip_convert_bsk": (i32, [vp, u32, vp, vp, i32, u32, u32, u32, u32]),
     "concrete_hip_pbs": (i32, [vp, u32, vp, vp, vp, vp, vp, vp, vp, u32, u32, u32, u32, u32, u32, vp]),

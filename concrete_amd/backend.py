@@ -176,6 +176,14 @@ def pbs_supported(p: PbsParams) -> bool:
     return bool(_native.lib().concrete_hip_pbs_supported(p.k, p.N, p.level, p.base_log))
 
 
+def bsk_format(p: PbsParams) -> tuple[int, int, int]:
+    """Device key format of (k, N, l): (kind, limbs, limb bits); kind 1 / 2 = the N = 1024 /
+    2048 kernels' layouts, 3 = the general path (pbs_generic.hip), 0 = unsupported."""
+    limbs, bits = C.c_uint32(0), C.c_uint32(0)
+    kind = _native.lib().concrete_hip_bsk_format(p.k, p.N, p.level, C.byref(limbs), C.byref(bits))
+    return int(kind), int(limbs.value), int(bits.value)
+
+
 def fourier_bsk_bytes(p: PbsParams) -> int:
     return int(_native.lib().concrete_hip_fourier_bsk_size_bytes(p.n, p.k, p.level, p.N))
 

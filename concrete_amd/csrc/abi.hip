@@ -39,13 +39,6 @@ static std::unordered_map<const void*, KeyEntry> g_keys;
 
 static void set_device(uint32_t gpu) { CHIP_CHECK(hipSetDevice((int)gpu)); }
 
-static bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
-  if (k != 1 || base_log < 1) return false;
-  if (N == 1024) return pbs1024_exact(k, level, base_log);
-  // N = 2048: one level whose digit splits into two 12-bit sub-digits (pbs2048.hip)
-  if (N == 2048) return level == 1 && base_log <= 2 * PBS2_SUB_BITS;
-  return false;
-}
 
 }  // namespace chip
 
@@ -137,13 +130,28 @@ int concrete_hip_pbs_supported(uint32_t glwe_dim, uint32_t polynomial_size, uint
 }
 
 uint32_t concrete_hip_bsk_limbs(uint32_t polynomial_size, uint32_t level_count, uint32_t base_log) {
-  return default_limbs(polynomial_size, level_count, base_log);
+  (void)base_log;
+  return default_limbs(1, polynomial_size, level_count);
+}
+
+int concrete_hip_bsk_format(uint32_t glwe_dim, uint32_t polynomial_size, uint32_t level_count, uint32_t* limbs,
+                            uint32_t* limb_bits) {
+  const KeyFormat f = key_format(glwe_dim, polynomial_size, level_count);
+  if (limbs) *limbs = f.limbs;
+  if (limb_bits) *limb_bits = f.bits;
+  return (int)f.kind;
+}
+
+double concrete_hip_generic_error_bound(uint32_t glwe_dim, uint32_t polynomial_size, uint32_t level_count,
+                                        uint32_t base_log, double max_key_spectrum) {
+  const KeyFormat f = key_format(glwe_dim, polynomial_size, level_count);
+  if (f.kind != KeyKind::GENERIC) return -1.0;
+  return generic_error_bound(glwe_dim, polynomial_size, level_count, base_log, f.bits, max_key_spectrum);
 }
 
 uint64_t concrete_hip_fourier_bsk_size_bytes(uint32_t input_lwe_dim, uint32_t glwe_dim, uint32_t level_count,
                                              uint32_t polynomial_size) {
-  return fourier_bsk_bytes(input_lwe_dim, glwe_dim, level_count, polynomial_size,
-                           default_limbs(polynomial_size, level_count, 0));
+  return fourier_bsk_bytes(input_lwe_dim, glwe_dim, level_count, polynomial_size);
 }
 
 int concrete_hip_convert_bsk(void* stream, uint32_t gpu_index, void* dest_fourier, const void* src,
@@ -153,7 +161,7 @@ int concrete_hip_convert_bsk(void* stream, uint32_t gpu_index, void* dest_fourie
     set_error("convert_bsk: null pointer");
     return -1;
   }
-  if (!pbs_params_ok(glwe_dim, polynomial_size, level_count, 1)) {
+  if (key_format(glwe_dim, polynomial_size, level_count).kind == KeyKind::NONE) {
     set_error("convert_bsk: unsupported parameters k=%u N=%u level=%u", glwe_dim, polynomial_size, level_count);
     return -2;
   }
@@ -169,7 +177,7 @@ int concrete_hip_convert_bsk(void* stream, uint32_t gpu_index, void* dest_fourie
     src_dev = (const uint64_t*)tmp;
   }
   ConvertArgs a{s, dest_fourier, src_dev, input_lwe_dim, glwe_dim, level_count, polynomial_size,
-                default_limbs(polynomial_size, level_count, 0)};
+                default_limbs(glwe_dim, polynomial_size, level_count)};
   int rc = convert_bsk_launch(a);
   if (tmp) CHIP_CHECK(hipFreeAsync(tmp, s));
   return rc;
@@ -208,7 +216,7 @@ int concrete_hip_pbs(void* stream, uint32_t gpu_index, uint64_t* lwe_array_out, 
             polynomial_size,
             base_log,
             level_count,
-            default_limbs(polynomial_size, level_count, base_log),
+            default_limbs(glwe_dimension, polynomial_size, level_count),
             num_samples,
             (unsigned long long*)resid_bits};
   return pbs_launch(a);
@@ -272,7 +280,7 @@ void scratch_cuda_programmable_bootstrap_64(void* stream, uint32_t gpu_index, in
                                             uint32_t level_count, uint32_t input_lwe_ciphertext_count,
                                             bool allocate_gpu_memory) {
   (void)input_lwe_ciphertext_count;
-  if (!pbs_params_ok(glwe_dimension, polynomial_size, level_count, 1)) {
+  if (key_format(glwe_dimension, polynomial_size, level_count).kind == KeyKind::NONE) {
     set_error("scratch: unsupported parameters k=%u N=%u level=%u", glwe_dimension, polynomial_size, level_count);
     die("scratch_cuda_programmable_bootstrap_64");
   }

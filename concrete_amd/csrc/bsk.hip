@@ -207,6 +207,7 @@ static void make_tables(uint32_t N, std::vector<ddc>& zeta, std::vector<ddc>& tw
 }
 
 int convert_bsk_launch(const ConvertArgs& a) {
+  if (key_format(a.k, a.N, a.level).kind == KeyKind::GENERIC) return convert_bsk_generic_launch(a);
   const bool n1024 = a.N == 1024 && a.k == 1 && a.limbs == 3 && a.level >= 1 && a.level <= 3;
   const bool n2048 = a.N == 2048 && a.k == 1 && a.limbs == (uint32_t)PBS2_LIMBS && a.level == 1;
   if (!n1024 && !n2048) {

@@ -483,8 +483,10 @@ static int launch_pair(const PbsArgs& a) {
 }
 
 int pbs_launch(const PbsArgs& a) {
-  if (a.N == 2048) return pbs2048_launch(a);
-  if (a.N == 1024 && a.k == 1 && a.limbs == 3) {
+  const KeyKind kind = key_format(a.k, a.N, a.level).kind;
+  if (kind == KeyKind::GENERIC) return pbs_generic_launch(a);
+  if (kind == KeyKind::N2048) return pbs2048_launch(a);
+  if (kind == KeyKind::N1024 && a.limbs == 3) {
     switch (a.level) {
       case 1: return launch_pair<1>(a);
       case 2: return launch_pair<2>(a);

@@ -30,12 +30,27 @@ constexpr size_t pbs2048_lds_bytes() {
          4 * PBS2_CTS * 4;  // + per-wave sync counters
 }
 
+// Device key formats.  N1024 / N2048: the hand-tuned kernels' layouts (pbs.hip, pbs2048.hip);
+// GENERIC: pbs_generic.hip, L balanced limbs of `bits` bits for any k <= GEN_MAX_K and
+// N = 256 .. 16384.  The format depends on (k, N, l) only: the runtime's key conversion call
+// carries no base_log (context.h:106-109).
+enum class KeyKind { NONE, N1024, N2048, GENERIC };
+struct KeyFormat {
+  KeyKind kind;
+  uint32_t limbs, bits;
+};
+constexpr int GEN_MAX_K = 8;       // GLWE dimension
+constexpr int GEN_MAX_LIMBS = 8;   // key limbs
+constexpr int GEN_MAX_TERMS = 24; // (k+1) * l * sub-digits per slot product
+KeyFormat key_format(uint32_t k, uint32_t N, uint32_t level);                              // pbs_generic.hip
+bool generic_pbs_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log);            // pbs_generic.hip
+uint32_t generic_limb_bits(uint32_t k, uint32_t N, uint32_t level);                        // pbs_generic.hip
+double generic_error_bound(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log, uint32_t bits,
+                           double maxG);                                                   // pbs_generic.hip
+uint64_t generic_scratch_bytes_per_sample(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log);
+
 // Number of exact limbs of the key polynomial for a parameter set.
-inline uint32_t default_limbs(uint32_t N, uint32_t level, uint32_t base_log) {
-  (void)level;
-  (void)base_log;
-  return N <= 1024 ? 3u : (uint32_t)PBS2_LIMBS;
-}
+inline uint32_t default_limbs(uint32_t k, uint32_t N, uint32_t level) { return key_format(k, N, level).limbs; }
 
 // N = 1024 exactness gate.  The 3-limb product's certified rounding bound grows with the number
 // of digit rows (k+1)l and the digit magnitude 2^(logB-1): measured on random keys it is
@@ -46,12 +61,30 @@ inline bool pbs1024_exact(uint32_t k, uint32_t level, uint32_t base_log) {
          ((uint64_t)(k + 1) * level << base_log) <= 4096ull;
 }
 
+// Whether a (k, N, l, logB) PBS runs, exactly, on one of the kernels.
+inline bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
+  const KeyFormat f = key_format(k, N, level);
+  switch (f.kind) {
+    case KeyKind::N1024: return pbs1024_exact(k, level, base_log);
+    // one level whose digit splits into two 12-bit sub-digits (pbs2048.hip)
+    case KeyKind::N2048: return base_log >= 1 && base_log <= 2 * PBS2_SUB_BITS;
+    case KeyKind::GENERIC: return generic_pbs_ok(k, N, level, base_log);
+    default: return false;
+  }
+}
+
 // Size in bytes of the device Fourier bootstrapping key.
-//   N = 1024: [n][col][limb][row*l + q][512] complex f64
-//   N = 2048 (l = 1): [n][limb][col][row][sub][parity][512] complex f64 (pbs2048.hip)
-inline uint64_t fourier_bsk_bytes(uint32_t n, uint32_t k, uint32_t level, uint32_t N, uint32_t limbs) {
-  if (N == 2048) return (uint64_t)n * limbs * (k + 1) * (k + 1) * PBS2_SUBS * 2 * 512 * 16ull * level;
-  return (uint64_t)n * level * (k + 1) * (k + 1) * limbs * (N / 2) * 16ull;
+//   N1024:   [n][col][limb][row*l + q][512] complex f64
+//   N2048:   [n][limb][col][row][sub][parity][512] complex f64 (pbs2048.hip)
+//   GENERIC: [n][col][limb][row][q][N/2] complex f64 (pbs_generic.hip)
+inline uint64_t fourier_bsk_bytes(uint32_t n, uint32_t k, uint32_t level, uint32_t N) {
+  const KeyFormat f = key_format(k, N, level);
+  switch (f.kind) {
+    case KeyKind::N2048: return (uint64_t)n * f.limbs * (k + 1) * (k + 1) * PBS2_SUBS * 2 * 512 * 16ull * level;
+    case KeyKind::N1024:
+    case KeyKind::GENERIC: return (uint64_t)n * level * (k + 1) * (k + 1) * f.limbs * (N / 2) * 16ull;
+    default: return 0;
+  }
 }
 
 struct PbsArgs {
@@ -68,7 +101,8 @@ struct PbsArgs {
 };
 
 int pbs_launch(const PbsArgs& a);
-int pbs2048_launch(const PbsArgs& a);  // pbs2048.hip
+int pbs2048_launch(const PbsArgs& a);         // pbs2048.hip
+int pbs_generic_launch(const PbsArgs& a);     // pbs_generic.hip
 
 struct ConvertArgs {
   hipStream_t stream;
@@ -77,6 +111,7 @@ struct ConvertArgs {
   uint32_t n, k, level, N, limbs;
 };
 int convert_bsk_launch(const ConvertArgs& a);
+int convert_bsk_generic_launch(const ConvertArgs& a);  // pbs_generic.hip
 
 struct KsArgs {
   hipStream_t stream;

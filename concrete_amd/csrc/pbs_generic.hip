@@ -1,0 +1,593 @@
+// pbs_generic.hip — batched PBS for the general parameter sets of the concrete optimizer
+// (SURVEY.md §8f item 4): GLWE dimension k >= 1 and polynomial sizes N = 256 .. 16384, e.g.
+// the v0_last_128 table's 1-2 bit sets (k = 4..6, N = 256), 3 bits (k = 3, N = 512), 4 bits
+// (k = 2, N = 1024), 6-8 bits (k = 1, N = 4096 .. 16384; 8 bits: n = 1006, l = 2, logB = 15).
+//
+// Same semantics as pbs.hip / pbs2048.hip (concrete-cpu c_api/bootstrap.rs:347-414 -> tfhe 0.10
+// blind_rotate_assign + sample extract; oracle/tfhe_oracle.c:ora_pbs) and the same exactness
+// recipe: every digit x key product over Z_{2^64}[X]/(X^N+1) is evaluated as
+// exact integer convolutions with an f64 negacyclic FFT (M = N/2 complex points, folded
+// x_j + i x_{j+M}, twisted by zeta^j), whose certified rounding error stays below 1/2:
+//   * the key polynomial g is split into L balanced limbs of b bits, g = sum_j 2^{jb} g_j;
+//   * a decomposition digit wider than b bits is split into T balanced b-bit sub-digits,
+//     d = sum_t 2^{tb} s_t, so the product s_t * g_j lands on "slot" m = j + t: the slot sums
+//     Y_m = sum_t S_t * G_{m-t} are inverse-transformed once per slot (L per output
+//     polynomial; slots >= L vanish mod 2^64) and recombined as sum_m 2^{mb} round(y_m).
+//   b depends on (k, N, l) only, so the key format is fixed at conversion time (the runtime's
+//   conversion call carries no base_log); the PBS gate checks the bound for the actual logB.
+//
+// A GLWE accumulator at these sizes (up to 256 KB) does not fit a CU's LDS next to its
+// transforms, so the blind rotation runs as two batched launches per CMUX step:
+//   gen_mac_kernel   Y[ct][c][m] = sum_{r,q,t} X[ct][r][q][t] * G_i[c][m-t][r][q]   (each key
+//                    value read once per 16-ciphertext tile: HBM-bound on the X/Y spectra)
+//   gen_step_kernel  per (ciphertext, polynomial): inverse transforms of the L slots, exact
+//                    recombination into the accumulator, then the next step's rotation
+//                    X^{a_{i+1}} acc - acc, decomposition and forward transforms -> X.
+// Transforms are block-wide radix-4 Stockham FFTs in LDS (one polynomial per workgroup).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "common.hpp"
+#include "fft512.hpp"
+#include "kernel_util.hpp"
+#include "pbs.hpp"
+
+namespace chip {
+
+// ------------------------------------------------------------------------------------------
+// key format and exactness gate (host)
+// ------------------------------------------------------------------------------------------
+
+// Rounding bound of one slot of the product (oracle ora_fft_error_bound): R
+// products of a digit polynomial (||d||_2 <= sqrt(N) 2^(dbits-1)) with a key limb spectrum
+// (|G| <= maxG) through a forward transform, the pointwise product and an inverse transform
+// (Higham, Accuracy and Stability, Thm 24.2; gamma doubled for the radix-4 schedule), plus the
+// f64 key transform (||dG||_2 <= gamma ||g||_2, ||g||_2 <= sqrt(N) 2^(b-1)) and the final
+// rounding of the largest output.  maxG <= 0 selects the random-key estimate
+// 8 sqrt(M) 2^(b-1) sqrt(2) used by the gate; tests certify each key with its measured maxG
+// (oracle/pyoracle.py:generic_error_bound).
+double generic_error_bound(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log, uint32_t bits,
+                           double maxG) {
+  const double u = std::ldexp(1.0, -53);
+  const double M = N / 2.0;
+  const double logM = std::log2(M);
+  const double eta = u + 4.0 * u / (1.0 - 4.0 * u) * (std::sqrt(2.0) + u);
+  const double gamma = 2.0 * logM * eta / (1.0 - 2.0 * logM * eta);
+  const uint32_t T = (base_log + bits - 1) / bits;
+  const uint32_t dbits = base_log < bits ? base_log : bits;
+  const double R = (double)(k + 1) * level * T;
+  const double dnorm = std::sqrt((double)N) * std::ldexp(1.0, (int)dbits - 1);
+  const double gnorm = std::sqrt((double)N) * std::ldexp(1.0, (int)bits - 1);
+  if (maxG <= 0.0) maxG = 8.0 * std::sqrt(M) * std::ldexp(1.0, (int)bits - 1) * std::sqrt(2.0);
+  const double max_out = R * (double)N * std::ldexp(1.0, (int)dbits - 1) * std::ldexp(1.0, (int)bits - 1);
+  return R * dnorm * (maxG * (4.0 * gamma + 3.0 * u) + gamma * gnorm) * 1.0001 + 4.0 * u * max_out;
+}
+
+static bool generic_shape_ok(uint32_t k, uint32_t N, uint32_t level) {
+  if (k < 1 || k > (uint32_t)GEN_MAX_K || level < 1 || level > 16) return false;
+  return N >= 256 && N <= 16384 && (N & (N - 1)) == 0;
+}
+
+// Limb width b for (k, N, l): the widest b whose bound holds for digits of up to 2b bits
+// (T <= 2 sub-digits), which covers every logB the optimizer pairs with these sizes.
+uint32_t generic_limb_bits(uint32_t k, uint32_t N, uint32_t level) {
+  for (uint32_t b = 24; b >= 8; --b)
+    if (generic_error_bound(k, N, level, 2 * b, b, 0.0) < 0.25) return b;
+  return 0;
+}
+
+KeyFormat key_format(uint32_t k, uint32_t N, uint32_t level) {
+  if (k == 1 && N == 1024 && level >= 1 && level <= 3) return {KeyKind::N1024, 3, 22};
+  if (k == 1 && N == 2048 && level == 1) return {KeyKind::N2048, (uint32_t)PBS2_LIMBS, 16};
+  if (generic_shape_ok(k, N, level)) {
+    const uint32_t b = generic_limb_bits(k, N, level);
+    const uint32_t L = b ? (64 + b - 1) / b : 0;
+    if (b && L <= (uint32_t)GEN_MAX_LIMBS) return {KeyKind::GENERIC, L, b};
+  }
+  return {KeyKind::NONE, 0, 0};
+}
+
+bool generic_pbs_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
+  const KeyFormat f = key_format(k, N, level);
+  if (f.kind != KeyKind::GENERIC || base_log < 1 || (uint64_t)level * base_log > 64) return false;
+  const uint32_t T = (base_log + f.bits - 1) / f.bits;
+  if ((k + 1) * level * T > (uint32_t)GEN_MAX_TERMS) return false;
+  return generic_error_bound(k, N, level, base_log, f.bits, 0.0) < 0.25;
+}
+
+namespace gen {
+
+// ------------------------------------------------------------------------------------------
+// block FFT (LDS, in place, radix-4 Stockham passes + one radix-2 pass when log2 M is odd)
+// ------------------------------------------------------------------------------------------
+template <int M>
+struct Geo {
+  static constexpr int THREADS = M >= 512 ? M / 8 : (M >= 256 ? 64 : M / 4);
+  static constexpr int VPT = M / THREADS;  // complex values per thread
+  static constexpr int LOG = M == 128 ? 7 : M == 256 ? 8 : M == 512 ? 9 : M == 1024 ? 10 : M == 2048 ? 11
+                           : M == 4096 ? 12 : 13;
+  static_assert((1 << LOG) == M, "M");
+  static_assert(VPT % 4 == 0, "values per thread");
+};
+
+template <bool INV>
+__device__ __forceinline__ cplx twiddle(const cplx* W, int idx) {
+  const cplx w = W[idx];
+  return INV ? cplx{w.re, -w.im} : w;
+}
+
+// One Stockham pass of radix R at stride Ns (natural order in, natural order out).  Every
+// thread reads all its inputs before the barrier and writes after it, so the pass is in place.
+template <int M, int R, bool INV>
+__device__ __forceinline__ void stockham_pass(cplx* buf, const cplx* W, int tid, int Ns) {
+  constexpr int TH = Geo<M>::THREADS;
+  constexpr int NB = M / R / TH;  // butterflies per thread
+  static_assert(NB >= 1 && (M / R) % TH == 0, "pass split");
+  cplx v[NB][R];
+#pragma unroll
+  for (int s = 0; s < NB; ++s) {
+    const int j = tid + s * TH;
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[s][r] = buf[j + r * (M / R)];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < NB; ++s) {
+    const int j = tid + s * TH;
+    const int kk = j & (Ns - 1);
+    const int step = M / (Ns * R);
+#pragma unroll
+    for (int r = 1; r < R; ++r) v[s][r] = cmul(v[s][r], twiddle<INV>(W, kk * r * step));
+    if constexpr (R == 2) {
+      const cplx x0 = v[s][0], x1 = v[s][1];
+      v[s][0] = cadd(x0, x1);
+      v[s][1] = csub(x0, x1);
+    } else {
+      const cplx t0 = cadd(v[s][0], v[s][2]), t1 = csub(v[s][0], v[s][2]);
+      const cplx t2 = cadd(v[s][1], v[s][3]), t3 = mul_mi<INV>(csub(v[s][1], v[s][3]));
+      v[s][0] = cadd(t0, t2);
+      v[s][2] = csub(t0, t2);
+      v[s][1] = cadd(t1, t3);
+      v[s][3] = csub(t1, t3);
+    }
+    const int d = (j - kk) * R + kk;
+#pragma unroll
+    for (int r = 0; r < R; ++r) buf[d + r * Ns] = v[s][r];
+  }
+  __syncthreads();
+}
+
+// Unnormalised DFT of buf (M complex, natural order) in place: forward e^{-2 pi i jk/M},
+// inverse e^{+2 pi i jk/M}; W[j] = e^{-2 pi i j/M}.  Callers synchronise before the call.
+template <int M, bool INV>
+__device__ __forceinline__ void fft_block(cplx* buf, const cplx* W, int tid) {
+  int Ns = 1;
+  if constexpr (Geo<M>::LOG & 1) {
+    stockham_pass<M, 2, INV>(buf, W, tid, Ns);
+    Ns = 2;
+  }
+#pragma unroll 1
+  for (; Ns < M; Ns *= 4) stockham_pass<M, 4, INV>(buf, W, tid, Ns);
+}
+
+// tfhe SignedDecomposer::decompose_one_level on a 64-bit state (digits up to 64 bits)
+__device__ __forceinline__ int64_t decomp_next64(uint64_t& state, int logB) {
+  const uint64_t mask = logB >= 64 ? ~0ull : (1ull << logB) - 1ull;
+  const uint64_t res = state & mask;
+  state = logB >= 64 ? 0ull : state >> logB;
+  const uint64_t carry = (((res - 1ull) | state) & res) >> (logB - 1);
+  state += carry;
+  return (int64_t)(res - (logB >= 64 ? 0ull : carry << logB));
+}
+
+// ------------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------------
+struct StepArgs {
+  uint64_t* acc;       // [chunk][K1][N] accumulators
+  cplx* X;             // [chunk][K1 r][l q][T t][M] digit spectra
+  const cplx* Y;       // [chunk][K1 c][L m][M] slot spectra
+  const cplx* W;       // e^{-2 pi i j/M}
+  const cplx* Z;       // zeta^j = e^{i pi j/N}
+  const uint64_t* in;  // LWE inputs (rows of n+1)
+  const uint64_t* in_idx;
+  const uint64_t* luts;
+  const uint64_t* lut_idx;
+  unsigned long long* resid;
+  uint32_t base;   // first sample of the chunk
+  uint32_t count;  // samples in the chunk
+  uint32_t n, k, level, base_log, bits, limbs, subs;
+  uint32_t step;  // FRONT: the mask position whose rotation is prepared
+};
+
+enum { MODE_INIT = 1, MODE_BACK = 2, MODE_FRONT = 4 };
+
+template <int M, int MODE>
+__global__ void __launch_bounds__(Geo<M>::THREADS) gen_step_kernel(StepArgs a) {
+  constexpr int N = 2 * M, TH = Geo<M>::THREADS, VPT = Geo<M>::VPT, LOG2_2N = Geo<M>::LOG + 2;
+  __shared__ cplx buf[M];
+  const int tid = threadIdx.x;
+  const uint32_t K1 = a.k + 1;
+  const uint32_t ct = blockIdx.x / K1, c = blockIdx.x % K1;
+  if (ct >= a.count) return;
+  const uint32_t s = a.base + ct;
+  const uint64_t row = a.in_idx ? a.in_idx[s] : s;
+  const uint64_t* lwe = a.in + row * (uint64_t)(a.n + 1);
+  uint64_t* acc = a.acc + ((uint64_t)ct * K1 + c) * N;
+  // this thread's coefficients: j = tid + e TH (e < VPT) and j + M (element e + VPT)
+  auto coef = [&](int e) { return (uint32_t)(tid + (e % VPT) * TH + (e / VPT) * M); };
+  uint64_t A[2 * VPT];
+  double max_resid = 0.0;
+
+  if constexpr ((MODE & MODE_INIT) != 0) {
+    // acc_c = LUT_c * X^{-ms(b)} (blind_rotate_assign: polynomial_wrapping_monic_monomial_div)
+    const uint64_t* lut = a.luts + (a.lut_idx ? a.lut_idx[s] : 0ull) * (uint64_t)(K1 * N) + (uint64_t)c * N;
+    const uint32_t bt = modswitch(lwe[a.n], LOG2_2N);
+#pragma unroll
+    for (int e = 0; e < 2 * VPT; ++e) {
+      const uint32_t src = (coef(e) + bt) & (2 * N - 1);
+      const uint64_t v = lut[src & (N - 1)];
+      A[e] = src < (uint32_t)N ? v : 0ull - v;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 2 * VPT; ++e) A[e] = acc[coef(e)];
+  }
+
+  if constexpr ((MODE & MODE_BACK) != 0) {
+    // acc_c += sum_m 2^{m b} round(iFFT(Y_m) conj(zeta^j)); the key spectra carry the 1/M.
+    // bits(v + MAGIC) - MAGIC_BITS = round(v) mod 2^64 for |v| < 2^51 (either sign).
+    const cplx* Yc = a.Y + ((uint64_t)ct * K1 + c) * a.limbs * (uint64_t)M;
+#pragma unroll 1
+    for (uint32_t m = 0; m < a.limbs; ++m) {
+      const cplx* Ym = Yc + (uint64_t)m * M;
+#pragma unroll
+      for (int e = 0; e < VPT; ++e) buf[tid + e * TH] = Ym[tid + e * TH];
+      __syncthreads();
+      fft_block<M, true>(buf, a.W, tid);
+      const uint32_t sh = m * a.bits;
+#pragma unroll
+      for (int e = 0; e < VPT; ++e) {
+        const int j = tid + e * TH;
+        const cplx z = cmulc(buf[j], a.Z[j]);
+        const double tr = z.re + RND_MAGIC, ti = z.im + RND_MAGIC;
+        max_resid = fmax(max_resid, fmax(fabs(z.re - (tr - RND_MAGIC)), fabs(z.im - (ti - RND_MAGIC))));
+        if (sh < 64) {
+          A[e] += ((uint64_t)__double_as_longlong(tr) - RND_MAGIC_BITS) << sh;
+          A[e + VPT] += ((uint64_t)__double_as_longlong(ti) - RND_MAGIC_BITS) << sh;
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  if constexpr ((MODE & (MODE_BACK | MODE_INIT)) != 0) {
+#pragma unroll
+    for (int e = 0; e < 2 * VPT; ++e) acc[coef(e)] = A[e];
+  }
+
+  if constexpr ((MODE & MODE_FRONT) != 0) {
+    // ct1 = X^{ms(a_i)} acc - acc; balanced decomposition; b-bit sub-digits; forward transforms
+    const uint32_t at = modswitch(lwe[a.step], LOG2_2N);
+    uint64_t* accl = reinterpret_cast<uint64_t*>(buf);
+#pragma unroll
+    for (int e = 0; e < 2 * VPT; ++e) accl[coef(e)] = A[e];
+    __syncthreads();
+    const int nrep = 64 - (int)(a.level * a.base_log);
+#pragma unroll
+    for (int e = 0; e < 2 * VPT; ++e) {
+      const uint32_t src = (coef(e) - at) & (2 * N - 1);
+      const uint64_t rv = accl[src & (N - 1)];
+      const uint64_t x = (src < (uint32_t)N ? rv : 0ull - rv) - A[e];
+      A[e] = nrep > 0 ? decomp_init(x, nrep) : x;  // decomposer state (reuses A)
+    }
+    __syncthreads();
+    cplx* Xc = a.X + ((uint64_t)ct * K1 + c) * a.level * a.subs * (uint64_t)M;
+    const int logB = (int)a.base_log;
+    const int sb = (int)a.bits;
+    const uint64_t half = 1ull << (sb - 1);
+    const uint64_t bmask = (1ull << sb) - 1ull;
+#pragma unroll 1
+    for (uint32_t q = 0; q < a.level; ++q) {
+      int64_t D[2 * VPT];
+#pragma unroll
+      for (int e = 0; e < 2 * VPT; ++e) D[e] = decomp_next64(A[e], logB);
+#pragma unroll 1
+      for (uint32_t t = 0; t < a.subs; ++t) {
+#pragma unroll
+        for (int e = 0; e < VPT; ++e) {
+          int64_t s0 = D[e], s1 = D[e + VPT];
+          if (a.subs > 1) {  // balanced b-bit sub-digit, exact: D - s is a multiple of 2^b
+            s0 = (int64_t)(((uint64_t)D[e] + half) & bmask) - (int64_t)half;
+            s1 = (int64_t)(((uint64_t)D[e + VPT] + half) & bmask) - (int64_t)half;
+            D[e] = (D[e] - s0) >> sb;
+            D[e + VPT] = (D[e + VPT] - s1) >> sb;
+          }
+          const int j = tid + e * TH;
+          buf[j] = cmul(cplx{(double)s0, (double)s1}, a.Z[j]);
+        }
+        __syncthreads();
+        fft_block<M, false>(buf, a.W, tid);
+        cplx* dst = Xc + ((uint64_t)q * a.subs + t) * M;
+#pragma unroll
+        for (int e = 0; e < VPT; ++e) dst[tid + e * TH] = buf[tid + e * TH];
+        __syncthreads();
+      }
+    }
+  }
+
+  if constexpr ((MODE & MODE_BACK) != 0) {
+    if (a.resid) {
+      for (int off = 32; off > 0; off >>= 1) max_resid = fmax(max_resid, __shfl_xor(max_resid, off));
+      if ((tid & 63) == 0) atomicMax(a.resid, (unsigned long long)__double_as_longlong(max_resid));
+    }
+  }
+}
+
+// Y[ct][c][m][f] = sum over (r, q, t) with 0 <= m - t < L of X[ct][r][q][t][f] * G_i[c][m-t][r][q][f]
+struct MacArgs {
+  const cplx* X;
+  cplx* Y;
+  const cplx* G;  // Fourier key [n][K1 c][L lim][K1 r][l q][M]
+  uint32_t count, k, level, limbs, subs, M;
+  uint32_t i;  // GGSW index (LWE mask position)
+};
+constexpr int MAC_CTS = 16;  // ciphertexts per block (key values loaded once per tile)
+
+__global__ void __launch_bounds__(256) gen_mac_kernel(MacArgs a) {
+  const uint32_t f = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t K1 = a.k + 1, L = a.limbs, T = a.subs;
+  const uint32_t c = blockIdx.y / L, m = blockIdx.y % L;
+  const uint32_t terms = K1 * a.level * T;
+  const uint64_t M = a.M;
+  if (f >= M) return;
+  cplx kv[GEN_MAX_TERMS];
+#pragma unroll
+  for (int x = 0; x < GEN_MAX_TERMS; ++x) {
+    kv[x] = {0.0, 0.0};
+    if ((uint32_t)x < terms) {
+      const uint32_t t = x % T, rq = x / T;  // x = (r l + q) T + t
+      if (m >= t && m - t < L) kv[x] = a.G[((((uint64_t)a.i * K1 + c) * L + (m - t)) * K1 * a.level + rq) * M + f];
+    }
+  }
+  const uint32_t ct0 = blockIdx.z * MAC_CTS;
+  for (uint32_t ct = ct0; ct < ct0 + MAC_CTS && ct < a.count; ++ct) {
+    const cplx* Xct = a.X + (uint64_t)ct * terms * M + f;
+    cplx y = {0.0, 0.0};
+#pragma unroll
+    for (int x = 0; x < GEN_MAX_TERMS; ++x) {
+      if ((uint32_t)x < terms) {
+        const cplx xv = Xct[(uint64_t)x * M];
+        y.re = __builtin_fma(xv.re, kv[x].re, __builtin_fma(-xv.im, kv[x].im, y.re));
+        y.im = __builtin_fma(xv.re, kv[x].im, __builtin_fma(xv.im, kv[x].re, y.im));
+      }
+    }
+    a.Y[(((uint64_t)ct * K1 + c) * L + m) * M + f] = y;
+  }
+}
+
+// sample extract (nth = 0): out[r N + 0] = A_r[0], out[r N + j] = -A_r[N - j], out[k N] = B[0]
+__global__ void gen_extract_kernel(uint64_t* out, const uint64_t* out_idx, const uint64_t* acc, uint32_t base,
+                                   uint32_t count, uint32_t k, uint32_t N) {
+  const uint64_t width = (uint64_t)k * N + 1;
+  const uint64_t total = width * count;
+  for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < total; g += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t ct = (uint32_t)(g / width), e = (uint32_t)(g % width);
+    const uint32_t s = base + ct;
+    const uint64_t orow = out_idx ? out_idx[s] : s;
+    const uint64_t* A = acc + (uint64_t)ct * (k + 1) * N;
+    uint64_t v;
+    if (e == k * N) {
+      v = A[(uint64_t)k * N];
+    } else {
+      const uint32_t r = e / N, j = e % N;
+      const uint64_t x = A[(uint64_t)r * N + ((N - j) & (N - 1))];
+      v = j == 0 ? x : 0ull - x;
+    }
+    out[orow * width + e] = v;
+  }
+}
+
+// Fourier key: G[i][c][lim][r][q][f] = FFT(twist(limb_lim(std[i][l-1-q][r][c])))[f] / M
+template <int M>
+__global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, const uint64_t* src, const cplx* W,
+                                                                        const cplx* Z, uint32_t k, uint32_t level,
+                                                                        uint32_t bits, uint32_t limbs) {
+  constexpr int N = 2 * M, TH = Geo<M>::THREADS, VPT = Geo<M>::VPT;
+  __shared__ cplx buf[M];
+  const int tid = threadIdx.x;
+  const uint32_t K1 = k + 1;
+  // block = one standard polynomial [i][v][row r][col c] (concrete-cpu bootstrap.rs:417-429)
+  uint64_t p = blockIdx.x;
+  const uint32_t c = p % K1;
+  p /= K1;
+  const uint32_t r = p % K1;
+  p /= K1;
+  const uint32_t v = p % level;
+  const uint64_t i = p / level;
+  const uint32_t q = level - 1 - v;
+  const uint64_t* g = src + (uint64_t)blockIdx.x * N;
+  uint64_t gv[2 * VPT];
+#pragma unroll
+  for (int e = 0; e < 2 * VPT; ++e) gv[e] = g[tid + (e % VPT) * TH + (e / VPT) * M];
+  const uint64_t half = 1ull << (bits - 1);
+  const uint64_t bmask = (1ull << bits) - 1ull;
+  const double scale = 1.0 / (double)M;
+#pragma unroll 1
+  for (uint32_t lim = 0; lim < limbs; ++lim) {
+#pragma unroll
+    for (int e = 0; e < VPT; ++e) {
+      // balanced b-bit limb: g = sum_j 2^{jb} g_j mod 2^64, |g_j| <= 2^(b-1)
+      const int64_t s0 = (int64_t)((gv[e] + half) & bmask) - (int64_t)half;
+      const int64_t s1 = (int64_t)((gv[e + VPT] + half) & bmask) - (int64_t)half;
+      gv[e] = (gv[e] - (uint64_t)s0) >> bits;
+      gv[e + VPT] = (gv[e + VPT] - (uint64_t)s1) >> bits;
+      const int j = tid + e * TH;
+      buf[j] = cmul(cplx{(double)s0, (double)s1}, Z[j]);
+    }
+    __syncthreads();
+    fft_block<M, false>(buf, W, tid);
+    cplx* dst = G + ((((i * K1 + c) * limbs + lim) * K1 + r) * level + q) * (uint64_t)M;
+#pragma unroll
+    for (int e = 0; e < VPT; ++e) {
+      const cplx x = buf[tid + e * TH];
+      dst[tid + e * TH] = {x.re * scale, x.im * scale};
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+struct Tables {
+  cplx* W = nullptr;
+  cplx* Z = nullptr;
+};
+
+// W (e^{-2 pi i j/M}) and Z (zeta^j) for polynomial size N on the current device, built once in
+// long double (correctly rounded to f64) and kept for the life of the process.
+static Tables tables_for(uint32_t N) {
+  static std::mutex mu;
+  static std::map<std::pair<int, uint32_t>, Tables> cache;
+  int dev = 0;
+  CHIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find({dev, N});
+  if (it != cache.end()) return it->second;
+  const uint32_t M = N / 2;
+  const long double PI = 3.14159265358979323846264338327950288L;
+  std::vector<cplx> w(M), z(M);
+  for (uint32_t j = 0; j < M; ++j) {
+    const long double aw = -2.0L * PI * (long double)j / (long double)M;
+    const long double az = PI * (long double)j / (long double)N;
+    w[j] = {(double)cosl(aw), (double)sinl(aw)};
+    z[j] = {(double)cosl(az), (double)sinl(az)};
+  }
+  Tables t;
+  CHIP_CHECK(hipMalloc((void**)&t.W, M * sizeof(cplx)));
+  CHIP_CHECK(hipMalloc((void**)&t.Z, M * sizeof(cplx)));
+  CHIP_CHECK(hipMemcpy(t.W, w.data(), M * sizeof(cplx), hipMemcpyHostToDevice));
+  CHIP_CHECK(hipMemcpy(t.Z, z.data(), M * sizeof(cplx), hipMemcpyHostToDevice));
+  cache[{dev, N}] = t;
+  return t;
+}
+
+template <int M, int MODE>
+static void launch_step(const StepArgs& s, uint32_t K1, hipStream_t st) {
+  hipLaunchKernelGGL((gen_step_kernel<M, MODE>), dim3(s.count * K1), dim3(Geo<M>::THREADS), 0, st, s);
+}
+
+template <int MODE>
+static int step_dispatch(uint32_t N, const StepArgs& s, uint32_t K1, hipStream_t st) {
+  switch (N) {
+    case 256: launch_step<128, MODE>(s, K1, st); break;
+    case 512: launch_step<256, MODE>(s, K1, st); break;
+    case 1024: launch_step<512, MODE>(s, K1, st); break;
+    case 2048: launch_step<1024, MODE>(s, K1, st); break;
+    case 4096: launch_step<2048, MODE>(s, K1, st); break;
+    case 8192: launch_step<4096, MODE>(s, K1, st); break;
+    case 16384: launch_step<8192, MODE>(s, K1, st); break;
+    default: return -2;
+  }
+  return 0;
+}
+
+}  // namespace gen
+
+uint64_t generic_scratch_bytes_per_sample(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
+  const KeyFormat f = key_format(k, N, level);
+  if (f.kind != KeyKind::GENERIC) return 0;
+  const uint64_t K1 = k + 1, M = N / 2, T = (base_log + f.bits - 1) / f.bits;
+  return K1 * level * T * M * 16 + K1 * f.limbs * M * 16 + K1 * N * 8;
+}
+
+int pbs_generic_launch(const PbsArgs& a) {
+  using namespace gen;
+  if (a.num_samples == 0) return 0;
+  if (!generic_pbs_ok(a.k, a.N, a.level, a.base_log)) {
+    set_error("pbs: k=%u N=%u level=%u base_log=%u outside the generic path's exact range", a.k, a.N, a.level,
+              a.base_log);
+    return -2;
+  }
+  const KeyFormat fmt = key_format(a.k, a.N, a.level);
+  const uint32_t K1 = a.k + 1, M = a.N / 2, L = fmt.limbs, b = fmt.bits;
+  const uint32_t T = (a.base_log + b - 1) / b;
+  const Tables tb = tables_for(a.N);
+  const uint64_t per_ct = generic_scratch_bytes_per_sample(a.k, a.N, a.level, a.base_log);
+  const uint64_t budget = 2ull << 30;
+  const uint32_t chunk = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(a.num_samples, 65536),
+                                                      std::max<uint64_t>(1, budget / per_ct));
+  void* scratch = nullptr;
+  CHIP_CHECK(hipMallocAsync(&scratch, per_ct * chunk, a.stream));
+  cplx* X = reinterpret_cast<cplx*>(scratch);
+  cplx* Y = X + (uint64_t)chunk * K1 * a.level * T * M;
+  uint64_t* acc = reinterpret_cast<uint64_t*>(Y + (uint64_t)chunk * K1 * L * M);
+  int rc = 0;
+  for (uint32_t base = 0; base < a.num_samples && rc == 0; base += chunk) {
+    const uint32_t cnt = std::min(chunk, a.num_samples - base);
+    StepArgs s{acc,  X,   Y,   tb.W, tb.Z,    a.in,       a.in_idx, a.luts, a.lut_idx, a.resid,
+               base, cnt, a.n, a.k,  a.level, a.base_log, b,        L,      T,         0};
+    rc = step_dispatch<MODE_INIT | MODE_FRONT>(a.N, s, K1, a.stream);
+    MacArgs m{X, Y, reinterpret_cast<const cplx*>(a.fbsk), cnt, a.k, a.level, L, T, M, 0};
+    const dim3 mg((M + 255) / 256, K1 * L, (cnt + MAC_CTS - 1) / MAC_CTS);
+    for (uint32_t i = 0; i < a.n && rc == 0; ++i) {
+      m.i = i;
+      hipLaunchKernelGGL(gen_mac_kernel, mg, dim3(256), 0, a.stream, m);
+      s.step = i + 1;
+      rc = i + 1 < a.n ? step_dispatch<MODE_BACK | MODE_FRONT>(a.N, s, K1, a.stream)
+                       : step_dispatch<MODE_BACK>(a.N, s, K1, a.stream);
+    }
+    const uint64_t total = ((uint64_t)a.k * a.N + 1) * cnt;
+    const uint32_t eb = (uint32_t)std::min<uint64_t>((total + 255) / 256, 65535);
+    hipLaunchKernelGGL(gen_extract_kernel, dim3(eb), dim3(256), 0, a.stream, a.out, a.out_idx, acc, base, cnt, a.k,
+                       a.N);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      set_error("generic pbs launch failed: %s", hipGetErrorString(e));
+      rc = -1;
+    }
+  }
+  CHIP_CHECK(hipFreeAsync(scratch, a.stream));
+  return rc;
+}
+
+int convert_bsk_generic_launch(const ConvertArgs& a) {
+  using namespace gen;
+  const KeyFormat fmt = key_format(a.k, a.N, a.level);
+  if (fmt.kind != KeyKind::GENERIC) {
+    set_error("generic BSK conversion: unsupported k=%u N=%u level=%u", a.k, a.N, a.level);
+    return -2;
+  }
+  const Tables tb = tables_for(a.N);
+  const uint64_t blocks = (uint64_t)a.n * a.level * (a.k + 1) * (a.k + 1);
+  if (blocks == 0) return 0;
+  cplx* G = reinterpret_cast<cplx*>(a.dest);
+#define GEN_CONV(MM)                                                                                        \
+  hipLaunchKernelGGL(gen_convert_kernel<MM>, dim3((uint32_t)blocks), dim3(Geo<MM>::THREADS), 0, a.stream, G, \
+                     a.src_dev, tb.W, tb.Z, a.k, a.level, fmt.bits, fmt.limbs)
+  switch (a.N) {
+    case 256: GEN_CONV(128); break;
+    case 512: GEN_CONV(256); break;
+    case 1024: GEN_CONV(512); break;
+    case 2048: GEN_CONV(1024); break;
+    case 4096: GEN_CONV(2048); break;
+    case 8192: GEN_CONV(4096); break;
+    case 16384: GEN_CONV(8192); break;
+    default: set_error("generic BSK conversion: N=%u", a.N); return -2;
+  }
+#undef GEN_CONV
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("generic convert launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+}  // namespace chip

@@ -112,6 +112,15 @@ int concrete_hip_pbs_supported(uint32_t glwe_dim, uint32_t polynomial_size, uint
                                uint32_t base_log);
 /* number of exact key limbs the device format uses for these parameters */
 uint32_t concrete_hip_bsk_limbs(uint32_t polynomial_size, uint32_t level_count, uint32_t base_log);
+/* device key format of (k, N, l): 0 unsupported, 1 / 2 the N = 1024 / 2048 (k = 1) kernels' layouts,
+ * 3 the general path (pbs_generic.hip); *limbs balanced key limbs of *limb_bits bits each */
+int concrete_hip_bsk_format(uint32_t glwe_dim, uint32_t polynomial_size, uint32_t level_count, uint32_t *limbs,
+                            uint32_t *limb_bits);
+/* rounding-error bound of the general path's exact product for a key whose largest
+ * limb-spectrum magnitude is max_key_spectrum (<= 0: the random-key estimate the gate uses);
+ * -1 when (k, N, l) is not on the general path */
+double concrete_hip_generic_error_bound(uint32_t glwe_dim, uint32_t polynomial_size, uint32_t level_count,
+                                        uint32_t base_log, double max_key_spectrum);
 /* bytes of the device (Fourier, exact-limb) bootstrapping key */
 uint64_t concrete_hip_fourier_bsk_size_bytes(uint32_t input_lwe_dim, uint32_t glwe_dim, uint32_t level_count,
                                              uint32_t polynomial_size);

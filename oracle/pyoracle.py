@@ -125,6 +125,32 @@ def gpu2048_error_bound(fbsk_gpu: np.ndarray) -> float:
     return float(main + alpha_term + 4.0 * u * max_out)
 
 
+def generic_error_bound(k: int, N: int, l: int, logB: int, bits: int, fbsk_gpu=None) -> float:
+    """Certified bound on |x - round(x)| for the GPU's general path (concrete_amd/csrc/
+    pbs_generic.hip:generic_error_bound): R = (k+1) l T products per slot of a
+    digit (or b-bit sub-digit) polynomial with a b-bit key-limb spectrum through radix-4
+    forward/inverse transforms (gamma doubled), plus the f64 key transform and the final
+    rounding.  fbsk_gpu: the device key (f64 view, spectra scaled by 1/M) -> measured max|G|;
+    None -> the random-key estimate the kernel's gate uses."""
+    u = 2.0 ** -53
+    M = N / 2.0
+    logM = np.log2(M)
+    eta = u + 4.0 * u / (1.0 - 4.0 * u) * (np.sqrt(2.0) + u)
+    gamma = 2.0 * logM * eta / (1.0 - 2.0 * logM * eta)
+    T = -(-logB // bits)
+    dbits = min(logB, bits)
+    R = (k + 1) * l * T
+    dnorm = np.sqrt(N) * 2.0 ** (dbits - 1)
+    gnorm = np.sqrt(N) * 2.0 ** (bits - 1)
+    if fbsk_gpu is None:
+        maxG = 8.0 * np.sqrt(M) * 2.0 ** (bits - 1) * np.sqrt(2.0)
+    else:
+        f = np.asarray(fbsk_gpu, dtype=np.float64).reshape(-1, 2)
+        maxG = float(np.max(np.hypot(f[:, 0], f[:, 1]))) * M
+    max_out = R * N * 2.0 ** (dbits - 1) * 2.0 ** (bits - 1)
+    return float(R * dnorm * (maxG * (4.0 * gamma + 3.0 * u) + gamma * gnorm) * 1.0001 + 4.0 * u * max_out)
+
+
 def bsk_std_torus(p: Params) -> float:
     return 2.0 ** lib().ora_secure_log2_std(p.k, p.N)
 

@@ -78,3 +78,30 @@ def test_encode_decode_match_oracle(oracle):
             e = B.encode(m, width)
             assert int(e) == int(oracle.encode(m, width))
             assert B.decode(e, width) == oracle.decode(e, width) == m
+
+
+def test_key_formats_and_exact_range():
+    """Host-side key-format selection and exactness gate (pbs.hpp:key_format, pbs_generic.hip):
+    the two hand-tuned layouts for cfg2/cfg4, the general path for the optimizer's other rows
+    (v0_last_128 1..8-bit sets), and refusal where the certified bound would not hold."""
+    import ctypes as C
+
+    from concrete_amd import _native
+    L = _native.lib()
+
+    def fmt(k, N, l):
+        a, b = C.c_uint32(), C.c_uint32()
+        return L.concrete_hip_bsk_format(k, N, l, C.byref(a), C.byref(b)), a.value, b.value
+
+    assert fmt(1, 1024, 3) == (1, 3, 22)
+    assert fmt(1, 2048, 1) == (2, 4, 16)
+    for k, N, l, logB in [(5, 256, 1, 15), (6, 256, 1, 18), (3, 512, 1, 18), (2, 1024, 1, 23), (1, 4096, 1, 22),
+                          (1, 8192, 1, 22), (1, 16384, 2, 15), (1, 2048, 2, 10)]:
+        kind, limbs, bits = fmt(k, N, l)
+        assert kind == 3 and limbs * bits >= 64, (k, N, l)
+        assert L.concrete_hip_pbs_supported(k, N, l, logB) == 1, (k, N, l, logB)
+        assert 0 < L.concrete_hip_generic_error_bound(k, N, l, logB, 0.0) < 0.25
+        assert L.concrete_hip_fourier_bsk_size_bytes(10, k, l, N) == 10 * l * (k + 1) ** 2 * limbs * (N // 2) * 16
+    assert fmt(1, 32768, 2)[0] == 0
+    assert L.concrete_hip_pbs_supported(1, 32768, 2, 15) == 0
+    assert L.concrete_hip_pbs_supported(1, 4096, 1, 40) == 0

@@ -31,7 +31,8 @@ def test_abi_version_and_queries():
     assert L.concrete_hip_pbs_supported(1, 1024, 2, 10) == 1
     assert L.concrete_hip_pbs_supported(1, 1024, 1, 11) == 1
     assert L.concrete_hip_pbs_supported(1, 1024, 1, 15) == 0
-    assert L.concrete_hip_pbs_supported(2, 1024, 3, 7) == 0
+    assert L.concrete_hip_pbs_supported(2, 1024, 3, 7) == 1  # k = 2: the general path
+    assert L.concrete_hip_pbs_supported(1, 32768, 1, 7) == 0
     assert L.concrete_hip_bsk_limbs(1024, 3, 7) == 3
     p = B.CFG2
     # n * l * (k+1)^2 * LIMBS * N/2 complex f64
@@ -42,7 +43,7 @@ def test_abi_version_and_queries():
 def test_status_codes_without_device():
     L = _native.lib()
     # unsupported parameters are rejected before any device call
-    rc = L.concrete_hip_pbs(None, 0, 1, None, 1, None, 1, None, 1, 630, 2, 1024, 7, 3, 4, None)
+    rc = L.concrete_hip_pbs(None, 0, 1, None, 1, None, 1, None, 1, 630, 1, 32768, 7, 3, 4, None)
     assert rc == -2 and b"unsupported" in L.concrete_hip_last_error()
     rc = L.concrete_hip_pbs(None, 0, None, None, None, None, None, None, None, 630, 1, 1024, 7, 3, 4, None)
     assert rc == -1

@@ -55,8 +55,9 @@ def pmc_traffic(batch: int, config: str):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=("cfg2", "cfg4"), default="cfg2",
-                    help="cfg2: N=1024 n=630 l=3 logB=7 (the metric's config); cfg4: N=2048 n=742 l=1 logB=23")
+    ap.add_argument("--config", choices=("cfg2", "cfg4") + tuple(f"opt{b}" for b in range(1, 9)), default="cfg2",
+                    help="cfg2: N=1024 n=630 l=3 logB=7 (the metric's config); cfg4: N=2048 n=742 l=1 logB=23; "
+                         "optB: the optimizer's B-bit row of v0_last_128 (backend.OPTIMIZER_SETS)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=4096, help="PBS per GPU per step")
@@ -94,10 +95,14 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    p = B.CFG2 if args.config == "cfg2" else B.CFG4
-    width = 3 if args.config == "cfg2" else 5
+    if args.config.startswith("opt"):
+        width = int(args.config[3:])
+        p = B.OPTIMIZER_SETS[width]
+    else:
+        p = B.CFG2 if args.config == "cfg2" else B.CFG4
+        width = 3 if args.config == "cfg2" else 5
     if not args.cpu_sample:
-        args.cpu_sample = 4096 if args.config == "cfg2" else 1024
+        args.cpu_sample = {"cfg2": 4096, "cfg4": 1024}.get(args.config, 32 if p.N <= 1024 else 16 if p.N <= 4096 else 2)
     # ---- keys: deterministic synthetic keyset (product keygen); device key on rank 0 -> RCCL bcast
     lwe_sk = B.binary_key(p.n, 1)
     glwe_sk = B.binary_key(p.big_n, 2)
@@ -231,22 +236,31 @@ def main():
         traffic, traffic_src = pmc_traffic(args.batch, args.config)
         if args.verify or not args.no_cpu_baseline:
             from oracle import pyoracle as O  # checker / CPU baseline only
-            op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, limbs=O.limbs_for(p.N))
+            opt = args.config.startswith("opt")
             if bsk is None:
                 bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 3)
-            fcpu = O.bsk_to_fourier(op, bsk)
+            if opt:
+                # optimizer rows: the oracle's pure-integer Karatsuba product (exact for every row;
+                # its limb-FFT path is tuned to cfg2/cfg4), on the standard key
+                op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
+                kw = {"bsk": bsk, "mode": O.MODE_KARATSUBA}
+                desc = "pure-integer Karatsuba restatement"
+            else:
+                op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, limbs=O.limbs_for(p.N))
+                kw = {"fbsk": O.bsk_to_fourier(op, bsk)}
+                desc = f"exact-limb f64 FFT restatement, {op.limbs} limbs"
             if args.verify:
-                ref, _ = O.pbs_batch(op, cts[: args.verify], acc[None, :], fbsk=fcpu, nthreads=args.cpu_threads)
+                ref, _ = O.pbs_batch(op, cts[: args.verify], acc[None, :], nthreads=args.cpu_threads, **kw)
                 bitexact = bool(np.array_equal(ref, out[: args.verify]))
             if not args.no_cpu_baseline:
                 sample = cts[: args.cpu_sample]
                 t1 = time.perf_counter()
-                O.pbs_batch(op, sample, acc[None, :], fbsk=fcpu, nthreads=args.cpu_threads)
+                O.pbs_batch(op, sample, acc[None, :], nthreads=args.cpu_threads, **kw)
                 dt = time.perf_counter() - t1
                 cpu = {"value": round(len(sample) / dt, 2), "unit": "PBS/s", "cores": args.cpu_threads,
                        "kind": "port",
-                       "sample": f"{len(sample)} PBS of the same {args.config} workload (exact-limb f64 FFT "
-                                 f"restatement, {op.limbs} limbs, OpenMP over ciphertexts), {dt:.2f} s wall"}
+                       "sample": f"{len(sample)} PBS of the same {args.config} workload ({desc}, OpenMP over "
+                                 f"ciphertexts), {dt:.2f} s wall"}
         result = {
             "metric": METRIC if args.config == "cfg2" else f"PBS/sec (whole node) at N={p.N} batch={args.batch}",
             "value": round(value, 1),

@@ -63,6 +63,20 @@ class PbsParams:
 CFG2 = PbsParams(n=630, k=1, N=1024, level=3, base_log=7, ks_level=4, ks_base_log=3)
 CFG4 = PbsParams(n=742, k=1, N=2048, level=1, base_log=23, ks_level=5, ks_base_log=3)
 
+# The concrete optimizer's 128-bit parameter rows at log norm2 = 0 (compilers/concrete-optimizer/
+# v0-parameters/ref/v0_last_128: k, log2 N, n, br_l, br_b, ks_l, ks_b), keyed by message bits.
+# All but 5 bits run on the general path (pbs_generic.hip).
+OPTIMIZER_SETS = {
+    1: PbsParams(n=592, k=5, N=256, level=1, base_log=15, ks_level=3, ks_base_log=3),
+    2: PbsParams(n=700, k=5, N=256, level=1, base_log=15, ks_level=3, ks_base_log=4),
+    3: PbsParams(n=722, k=3, N=512, level=1, base_log=18, ks_level=3, ks_base_log=4),
+    4: PbsParams(n=801, k=2, N=1024, level=1, base_log=23, ks_level=3, ks_base_log=4),
+    5: PbsParams(n=783, k=1, N=2048, level=1, base_log=23, ks_level=5, ks_base_log=3),
+    6: PbsParams(n=880, k=1, N=4096, level=1, base_log=22, ks_level=4, ks_base_log=4),
+    7: PbsParams(n=915, k=1, N=8192, level=1, base_log=22, ks_level=6, ks_base_log=3),
+    8: PbsParams(n=1006, k=1, N=16384, level=2, base_log=15, ks_level=5, ks_base_log=4),
+}
+
 
 def _ptr(a) -> int:
     if a is None:

@@ -46,7 +46,8 @@ namespace chip {
 // Rounding bound of one slot of the product (oracle ora_fft_error_bound): R
 // products of a digit polynomial (||d||_2 <= sqrt(N) 2^(dbits-1)) with a key limb spectrum
 // (|G| <= maxG) through a forward transform, the pointwise product and an inverse transform
-// (Higham, Accuracy and Stability, Thm 24.2; gamma doubled for the radix-4 schedule), plus the
+// (Higham, Accuracy and Stability, Thm 24.2, twiddle error mu = 5u for the two-level twiddle
+// tables; gamma doubled for the radix-4 schedule), plus the
 // f64 key transform (||dG||_2 <= gamma ||g||_2, ||g||_2 <= sqrt(N) 2^(b-1)) and the final
 // rounding of the largest output.  maxG <= 0 selects the random-key estimate
 // 8 sqrt(M) 2^(b-1) sqrt(2) used by the gate; tests certify each key with its measured maxG
@@ -56,7 +57,9 @@ double generic_error_bound(uint32_t k, uint32_t N, uint32_t level, uint32_t base
   const double u = std::ldexp(1.0, -53);
   const double M = N / 2.0;
   const double logM = std::log2(M);
-  const double eta = u + 4.0 * u / (1.0 - 4.0 * u) * (std::sqrt(2.0) + u);
+  // twiddles are products of two correctly rounded table entries: |error| <= mu = 5u
+  const double mu = 5.0 * u;
+  const double eta = mu + 4.0 * u / (1.0 - 4.0 * u) * (std::sqrt(2.0) + mu);
   const double gamma = 2.0 * logM * eta / (1.0 - 2.0 * logM * eta);
   const uint32_t T = (base_log + bits - 1) / bits;
   const uint32_t dbits = base_log < bits ? base_log : bits;
@@ -107,18 +110,31 @@ namespace gen {
 // ------------------------------------------------------------------------------------------
 template <int M>
 struct Geo {
-  static constexpr int THREADS = M >= 512 ? M / 8 : (M >= 256 ? 64 : M / 4);
-  static constexpr int VPT = M / THREADS;  // complex values per thread
+  static constexpr int THREADS = M >= 512 ? M / 8 : (M >= 256 ? 64 : M / 4);  // per polynomial
+  static constexpr int VPT = M / THREADS;                  // complex values per thread
+  static constexpr int PPB = THREADS >= 256 ? 1 : 256 / THREADS;  // polynomials per workgroup
+  static constexpr int BLOCK = THREADS * PPB;
   static constexpr int LOG = M == 128 ? 7 : M == 256 ? 8 : M == 512 ? 9 : M == 1024 ? 10 : M == 2048 ? 11
                            : M == 4096 ? 12 : 13;
   static_assert((1 << LOG) == M, "M");
   static_assert(VPT % 4 == 0, "values per thread");
 };
 
+// Twiddle e^{-+2 pi i idx/M} from two LDS tables: W[j] = Wlo[j mod TW_LO] * Whi[j / TW_LO]
+// (W points at Wlo; Whi follows it).
+constexpr int TW_LO = 128;
 template <bool INV>
 __device__ __forceinline__ cplx twiddle(const cplx* W, int idx) {
-  const cplx w = W[idx];
+  const cplx w = cmul(W[idx & (TW_LO - 1)], W[TW_LO + (idx >> 7)]);
   return INV ? cplx{w.re, -w.im} : w;
+}
+static_assert(TW_LO == 128, "twiddle split");
+
+// stage the two-level twiddle tables of size M into LDS (tw: TW_LO + max(1, M / TW_LO) entries)
+template <int M>
+__device__ __forceinline__ void load_twiddles(cplx* tw, const cplx* Wlo, const cplx* Whi, int t, int nt) {
+  constexpr int NHI = M / TW_LO > 1 ? M / TW_LO : 1;
+  for (int e = t; e < TW_LO + NHI; e += nt) tw[e] = e < TW_LO ? Wlo[e] : Whi[e - TW_LO];
 }
 
 // One Stockham pass of radix R at stride Ns (natural order in, natural order out).  Every
@@ -192,7 +208,8 @@ struct StepArgs {
   uint64_t* acc;       // [chunk][K1][N] accumulators
   cplx* X;             // [chunk][K1 r][l q][T t][M] digit spectra
   const cplx* Y;       // [chunk][K1 c][L m][M] slot spectra
-  const cplx* W;       // e^{-2 pi i j/M}
+  const cplx* Wlo;     // e^{-2 pi i j/M}, j < TW_LO
+  const cplx* Whi;     // e^{-2 pi i j TW_LO/M}
   const cplx* Z;       // zeta^j = e^{i pi j/N}
   const uint64_t* in;  // LWE inputs (rows of n+1)
   const uint64_t* in_idx;
@@ -208,15 +225,23 @@ struct StepArgs {
 enum { MODE_INIT = 1, MODE_BACK = 2, MODE_FRONT = 4 };
 
 template <int M, int MODE>
-__global__ void __launch_bounds__(Geo<M>::THREADS) gen_step_kernel(StepArgs a) {
+__global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
   constexpr int N = 2 * M, TH = Geo<M>::THREADS, VPT = Geo<M>::VPT, LOG2_2N = Geo<M>::LOG + 2;
-  __shared__ cplx buf[M];
-  const int tid = threadIdx.x;
+  constexpr int PPB = Geo<M>::PPB;
+  __shared__ cplx lds[PPB * M + TW_LO + (M / TW_LO > 1 ? M / TW_LO : 1)];
+  cplx* W = lds + PPB * M;
+  load_twiddles<M>(W, a.Wlo, a.Whi, threadIdx.x, Geo<M>::BLOCK);
+  __syncthreads();
+  // polynomial group g of this workgroup: (ciphertext, GLWE polynomial) = divmod(poly, k + 1).
+  // Groups past the batch keep taking part in the workgroup barriers of the transforms.
+  const int g = threadIdx.x / TH, tid = threadIdx.x % TH;
+  cplx* buf = lds + g * M;
   const uint32_t K1 = a.k + 1;
-  const uint32_t ct = blockIdx.x / K1, c = blockIdx.x % K1;
-  if (ct >= a.count) return;
+  const uint64_t poly = (uint64_t)blockIdx.x * PPB + g;
+  const bool live = poly < (uint64_t)a.count * K1;
+  const uint32_t ct = live ? (uint32_t)(poly / K1) : 0u, c = (uint32_t)(poly % K1);
   const uint32_t s = a.base + ct;
-  const uint64_t row = a.in_idx ? a.in_idx[s] : s;
+  const uint64_t row = live ? (a.in_idx ? a.in_idx[s] : s) : 0ull;
   const uint64_t* lwe = a.in + row * (uint64_t)(a.n + 1);
   uint64_t* acc = a.acc + ((uint64_t)ct * K1 + c) * N;
   // this thread's coefficients: j = tid + e TH (e < VPT) and j + M (element e + VPT)
@@ -226,17 +251,18 @@ __global__ void __launch_bounds__(Geo<M>::THREADS) gen_step_kernel(StepArgs a) {
 
   if constexpr ((MODE & MODE_INIT) != 0) {
     // acc_c = LUT_c * X^{-ms(b)} (blind_rotate_assign: polynomial_wrapping_monic_monomial_div)
-    const uint64_t* lut = a.luts + (a.lut_idx ? a.lut_idx[s] : 0ull) * (uint64_t)(K1 * N) + (uint64_t)c * N;
-    const uint32_t bt = modswitch(lwe[a.n], LOG2_2N);
+    const uint64_t* lut =
+        a.luts + (live && a.lut_idx ? a.lut_idx[s] : 0ull) * (uint64_t)(K1 * N) + (uint64_t)c * N;
+    const uint32_t bt = live ? modswitch(lwe[a.n], LOG2_2N) : 0u;
 #pragma unroll
     for (int e = 0; e < 2 * VPT; ++e) {
       const uint32_t src = (coef(e) + bt) & (2 * N - 1);
-      const uint64_t v = lut[src & (N - 1)];
+      const uint64_t v = live ? lut[src & (N - 1)] : 0ull;
       A[e] = src < (uint32_t)N ? v : 0ull - v;
     }
   } else {
 #pragma unroll
-    for (int e = 0; e < 2 * VPT; ++e) A[e] = acc[coef(e)];
+    for (int e = 0; e < 2 * VPT; ++e) A[e] = live ? acc[coef(e)] : 0ull;
   }
 
   if constexpr ((MODE & MODE_BACK) != 0) {
@@ -247,9 +273,9 @@ __global__ void __launch_bounds__(Geo<M>::THREADS) gen_step_kernel(StepArgs a) {
     for (uint32_t m = 0; m < a.limbs; ++m) {
       const cplx* Ym = Yc + (uint64_t)m * M;
 #pragma unroll
-      for (int e = 0; e < VPT; ++e) buf[tid + e * TH] = Ym[tid + e * TH];
+      for (int e = 0; e < VPT; ++e) buf[tid + e * TH] = live ? Ym[tid + e * TH] : cplx{0.0, 0.0};
       __syncthreads();
-      fft_block<M, true>(buf, a.W, tid);
+      fft_block<M, true>(buf, W, tid);
       const uint32_t sh = m * a.bits;
 #pragma unroll
       for (int e = 0; e < VPT; ++e) {
@@ -267,13 +293,14 @@ __global__ void __launch_bounds__(Geo<M>::THREADS) gen_step_kernel(StepArgs a) {
   }
 
   if constexpr ((MODE & (MODE_BACK | MODE_INIT)) != 0) {
+    if (live)
 #pragma unroll
-    for (int e = 0; e < 2 * VPT; ++e) acc[coef(e)] = A[e];
+      for (int e = 0; e < 2 * VPT; ++e) acc[coef(e)] = A[e];
   }
 
   if constexpr ((MODE & MODE_FRONT) != 0) {
     // ct1 = X^{ms(a_i)} acc - acc; balanced decomposition; b-bit sub-digits; forward transforms
-    const uint32_t at = modswitch(lwe[a.step], LOG2_2N);
+    const uint32_t at = live ? modswitch(lwe[a.step], LOG2_2N) : 0u;
     uint64_t* accl = reinterpret_cast<uint64_t*>(buf);
 #pragma unroll
     for (int e = 0; e < 2 * VPT; ++e) accl[coef(e)] = A[e];
@@ -312,10 +339,11 @@ __global__ void __launch_bounds__(Geo<M>::THREADS) gen_step_kernel(StepArgs a) {
           buf[j] = cmul(cplx{(double)s0, (double)s1}, a.Z[j]);
         }
         __syncthreads();
-        fft_block<M, false>(buf, a.W, tid);
+        fft_block<M, false>(buf, W, tid);
         cplx* dst = Xc + ((uint64_t)q * a.subs + t) * M;
+        if (live)
 #pragma unroll
-        for (int e = 0; e < VPT; ++e) dst[tid + e * TH] = buf[tid + e * TH];
+          for (int e = 0; e < VPT; ++e) dst[tid + e * TH] = buf[tid + e * TH];
         __syncthreads();
       }
     }
@@ -324,7 +352,7 @@ __global__ void __launch_bounds__(Geo<M>::THREADS) gen_step_kernel(StepArgs a) {
   if constexpr ((MODE & MODE_BACK) != 0) {
     if (a.resid) {
       for (int off = 32; off > 0; off >>= 1) max_resid = fmax(max_resid, __shfl_xor(max_resid, off));
-      if ((tid & 63) == 0) atomicMax(a.resid, (unsigned long long)__double_as_longlong(max_resid));
+      if ((threadIdx.x & 63) == 0) atomicMax(a.resid, (unsigned long long)__double_as_longlong(max_resid));
     }
   }
 }
@@ -371,6 +399,66 @@ __global__ void __launch_bounds__(256) gen_mac_kernel(MacArgs a) {
   }
 }
 
+// Same product, one thread per (frequency, output polynomial c) computing all L slots: each X
+// value is read once per output polynomial instead of once per (polynomial, slot), and the
+// key values of the thread (L x K1 l) stay in registers across the ciphertext tile.
+template <int KL, int L, int T>
+__global__ void __launch_bounds__(256) gen_mac2_kernel(MacArgs a) {
+  const uint32_t f = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t c = blockIdx.y, K1 = a.k + 1;
+  const uint64_t M = a.M;
+  if (f >= M) return;
+  cplx kv[L][KL];
+#pragma unroll
+  for (int lim = 0; lim < L; ++lim)
+#pragma unroll
+    for (int rq = 0; rq < KL; ++rq) kv[lim][rq] = a.G[((((uint64_t)a.i * K1 + c) * L + lim) * KL + rq) * M + f];
+  const uint32_t ct0 = blockIdx.z * MAC_CTS;
+  for (uint32_t ct = ct0; ct < ct0 + MAC_CTS && ct < a.count; ++ct) {
+    const cplx* Xct = a.X + (uint64_t)ct * KL * T * M + f;
+    cplx xv[KL][T];
+#pragma unroll
+    for (int rq = 0; rq < KL; ++rq)
+#pragma unroll
+      for (int t = 0; t < T; ++t) xv[rq][t] = Xct[(uint64_t)(rq * T + t) * M];
+    cplx* Yct = a.Y + ((uint64_t)ct * K1 + c) * L * M + f;
+#pragma unroll
+    for (int m = 0; m < L; ++m) {
+      cplx y = {0.0, 0.0};
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        if (m - t < 0 || m - t >= L) continue;
+#pragma unroll
+        for (int rq = 0; rq < KL; ++rq) {
+          const cplx xg = xv[rq][t], g = kv[m - t][rq];
+          y.re = __builtin_fma(xg.re, g.re, __builtin_fma(-xg.im, g.im, y.re));
+          y.im = __builtin_fma(xg.re, g.im, __builtin_fma(xg.im, g.re, y.im));
+        }
+      }
+      Yct[(uint64_t)m * M] = y;
+    }
+  }
+}
+
+// launch the register-tiled product for (K1 l, L, T) when instantiated, else the generic one
+static bool launch_mac2(const MacArgs& m, uint32_t cnt, hipStream_t st) {
+  const uint32_t KL = (m.k + 1) * m.level;
+  const dim3 grid((m.M + 255) / 256, m.k + 1, (cnt + MAC_CTS - 1) / MAC_CTS);
+#define GEN_MAC2(KLv, Lv, Tv)                                                               \
+  if (KL == KLv && m.limbs == Lv && m.subs == Tv) {                                           \
+    hipLaunchKernelGGL((gen_mac2_kernel<KLv, Lv, Tv>), grid, dim3(256), 0, st, m);            \
+    return true;                                                                              \
+  }
+#define GEN_MAC2_L(KLv, Tv) GEN_MAC2(KLv, 4, Tv) GEN_MAC2(KLv, 5, Tv) GEN_MAC2(KLv, 6, Tv)
+  GEN_MAC2_L(2, 1) GEN_MAC2_L(2, 2) GEN_MAC2_L(3, 1) GEN_MAC2_L(3, 2) GEN_MAC2_L(4, 1) GEN_MAC2_L(4, 2)
+  GEN_MAC2_L(5, 1) GEN_MAC2_L(5, 2) GEN_MAC2_L(6, 1) GEN_MAC2_L(6, 2)
+  GEN_MAC2(7, 4, 1) GEN_MAC2(7, 5, 1) GEN_MAC2(7, 4, 2) GEN_MAC2(7, 5, 2)
+  GEN_MAC2(8, 4, 1) GEN_MAC2(8, 4, 2)
+#undef GEN_MAC2_L
+#undef GEN_MAC2
+  return false;
+}
+
 // sample extract (nth = 0): out[r N + 0] = A_r[0], out[r N + j] = -A_r[N - j], out[k N] = B[0]
 __global__ void gen_extract_kernel(uint64_t* out, const uint64_t* out_idx, const uint64_t* acc, uint32_t base,
                                    uint32_t count, uint32_t k, uint32_t N) {
@@ -395,11 +483,14 @@ __global__ void gen_extract_kernel(uint64_t* out, const uint64_t* out_idx, const
 
 // Fourier key: G[i][c][lim][r][q][f] = FFT(twist(limb_lim(std[i][l-1-q][r][c])))[f] / M
 template <int M>
-__global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, const uint64_t* src, const cplx* W,
-                                                                        const cplx* Z, uint32_t k, uint32_t level,
-                                                                        uint32_t bits, uint32_t limbs) {
+__global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, const uint64_t* src, const cplx* Wlo,
+                                                                        const cplx* Whi, const cplx* Z, uint32_t k,
+                                                                        uint32_t level, uint32_t bits, uint32_t limbs) {
   constexpr int N = 2 * M, TH = Geo<M>::THREADS, VPT = Geo<M>::VPT;
-  __shared__ cplx buf[M];
+  __shared__ cplx buf[M + TW_LO + (M / TW_LO > 1 ? M / TW_LO : 1)];
+  cplx* W = buf + M;
+  load_twiddles<M>(W, Wlo, Whi, threadIdx.x, TH);
+  __syncthreads();
   const int tid = threadIdx.x;
   const uint32_t K1 = k + 1;
   // block = one standard polynomial [i][v][row r][col c] (concrete-cpu bootstrap.rs:417-429)
@@ -415,14 +506,16 @@ __global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, c
   uint64_t gv[2 * VPT];
 #pragma unroll
   for (int e = 0; e < 2 * VPT; ++e) gv[e] = g[tid + (e % VPT) * TH + (e / VPT) * M];
-  const uint64_t half = 1ull << (bits - 1);
-  const uint64_t bmask = (1ull << bits) - 1ull;
   const double scale = 1.0 / (double)M;
 #pragma unroll 1
   for (uint32_t lim = 0; lim < limbs; ++lim) {
+    // balanced limbs: g = sum_j 2^{jb} g_j mod 2^64, |g_j| <= 2^(b-1); the top limb only matters
+    // mod 2^(64 - (L-1) b), so it is balanced in that width (no DC offset in its spectrum)
+    const uint32_t w = lim + 1 < limbs ? bits : 64 - (limbs - 1) * bits;
+    const uint64_t half = 1ull << (w - 1);
+    const uint64_t bmask = (1ull << w) - 1ull;
 #pragma unroll
     for (int e = 0; e < VPT; ++e) {
-      // balanced b-bit limb: g = sum_j 2^{jb} g_j mod 2^64, |g_j| <= 2^(b-1)
       const int64_t s0 = (int64_t)((gv[e] + half) & bmask) - (int64_t)half;
       const int64_t s1 = (int64_t)((gv[e + VPT] + half) & bmask) - (int64_t)half;
       gv[e] = (gv[e] - (uint64_t)s0) >> bits;
@@ -446,12 +539,13 @@ __global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, c
 // host side
 // ------------------------------------------------------------------------------------------
 struct Tables {
-  cplx* W = nullptr;
-  cplx* Z = nullptr;
+  cplx* Wlo = nullptr;  // e^{-2 pi i j/M}, j < TW_LO
+  cplx* Whi = nullptr;  // e^{-2 pi i j TW_LO/M}, j < max(1, M/TW_LO)
+  cplx* Z = nullptr;    // zeta^j, j < M
 };
 
-// W (e^{-2 pi i j/M}) and Z (zeta^j) for polynomial size N on the current device, built once in
-// long double (correctly rounded to f64) and kept for the life of the process.
+// Twiddle and twist tables for polynomial size N on the current device, built once in long
+// double (correctly rounded to f64) and kept for the life of the process.
 static Tables tables_for(uint32_t N) {
   static std::mutex mu;
   static std::map<std::pair<int, uint32_t>, Tables> cache;
@@ -460,19 +554,19 @@ static Tables tables_for(uint32_t N) {
   std::lock_guard<std::mutex> g(mu);
   auto it = cache.find({dev, N});
   if (it != cache.end()) return it->second;
-  const uint32_t M = N / 2;
+  const uint32_t M = N / 2, NHI = M / TW_LO > 1 ? M / TW_LO : 1;
   const long double PI = 3.14159265358979323846264338327950288L;
-  std::vector<cplx> w(M), z(M);
-  for (uint32_t j = 0; j < M; ++j) {
-    const long double aw = -2.0L * PI * (long double)j / (long double)M;
-    const long double az = PI * (long double)j / (long double)N;
-    w[j] = {(double)cosl(aw), (double)sinl(aw)};
-    z[j] = {(double)cosl(az), (double)sinl(az)};
-  }
+  auto ex = [&](long double ang) { return cplx{(double)cosl(ang), (double)sinl(ang)}; };
+  std::vector<cplx> lo(TW_LO), hi(NHI), z(M);
+  for (uint32_t j = 0; j < (uint32_t)TW_LO; ++j) lo[j] = ex(-2.0L * PI * (long double)j / (long double)M);
+  for (uint32_t j = 0; j < NHI; ++j) hi[j] = ex(-2.0L * PI * (long double)(j * TW_LO) / (long double)M);
+  for (uint32_t j = 0; j < M; ++j) z[j] = ex(PI * (long double)j / (long double)N);
   Tables t;
-  CHIP_CHECK(hipMalloc((void**)&t.W, M * sizeof(cplx)));
+  CHIP_CHECK(hipMalloc((void**)&t.Wlo, TW_LO * sizeof(cplx)));
+  CHIP_CHECK(hipMalloc((void**)&t.Whi, NHI * sizeof(cplx)));
   CHIP_CHECK(hipMalloc((void**)&t.Z, M * sizeof(cplx)));
-  CHIP_CHECK(hipMemcpy(t.W, w.data(), M * sizeof(cplx), hipMemcpyHostToDevice));
+  CHIP_CHECK(hipMemcpy(t.Wlo, lo.data(), TW_LO * sizeof(cplx), hipMemcpyHostToDevice));
+  CHIP_CHECK(hipMemcpy(t.Whi, hi.data(), NHI * sizeof(cplx), hipMemcpyHostToDevice));
   CHIP_CHECK(hipMemcpy(t.Z, z.data(), M * sizeof(cplx), hipMemcpyHostToDevice));
   cache[{dev, N}] = t;
   return t;
@@ -480,7 +574,9 @@ static Tables tables_for(uint32_t N) {
 
 template <int M, int MODE>
 static void launch_step(const StepArgs& s, uint32_t K1, hipStream_t st) {
-  hipLaunchKernelGGL((gen_step_kernel<M, MODE>), dim3(s.count * K1), dim3(Geo<M>::THREADS), 0, st, s);
+  const uint64_t polys = (uint64_t)s.count * K1;
+  const uint32_t blocks = (uint32_t)((polys + Geo<M>::PPB - 1) / Geo<M>::PPB);
+  hipLaunchKernelGGL((gen_step_kernel<M, MODE>), dim3(blocks), dim3(Geo<M>::BLOCK), 0, st, s);
 }
 
 template <int MODE>
@@ -531,14 +627,14 @@ int pbs_generic_launch(const PbsArgs& a) {
   int rc = 0;
   for (uint32_t base = 0; base < a.num_samples && rc == 0; base += chunk) {
     const uint32_t cnt = std::min(chunk, a.num_samples - base);
-    StepArgs s{acc,  X,   Y,   tb.W, tb.Z,    a.in,       a.in_idx, a.luts, a.lut_idx, a.resid,
-               base, cnt, a.n, a.k,  a.level, a.base_log, b,        L,      T,         0};
+    StepArgs s{acc,  X,    Y,   tb.Wlo, tb.Whi,  tb.Z,       a.in, a.in_idx, a.luts, a.lut_idx,
+               a.resid, base, cnt, a.n,    a.k,     a.level, a.base_log, b,    L,        T,      0};
     rc = step_dispatch<MODE_INIT | MODE_FRONT>(a.N, s, K1, a.stream);
     MacArgs m{X, Y, reinterpret_cast<const cplx*>(a.fbsk), cnt, a.k, a.level, L, T, M, 0};
     const dim3 mg((M + 255) / 256, K1 * L, (cnt + MAC_CTS - 1) / MAC_CTS);
     for (uint32_t i = 0; i < a.n && rc == 0; ++i) {
       m.i = i;
-      hipLaunchKernelGGL(gen_mac_kernel, mg, dim3(256), 0, a.stream, m);
+      if (!launch_mac2(m, cnt, a.stream)) hipLaunchKernelGGL(gen_mac_kernel, mg, dim3(256), 0, a.stream, m);
       s.step = i + 1;
       rc = i + 1 < a.n ? step_dispatch<MODE_BACK | MODE_FRONT>(a.N, s, K1, a.stream)
                        : step_dispatch<MODE_BACK>(a.N, s, K1, a.stream);
@@ -570,7 +666,7 @@ int convert_bsk_generic_launch(const ConvertArgs& a) {
   cplx* G = reinterpret_cast<cplx*>(a.dest);
 #define GEN_CONV(MM)                                                                                        \
   hipLaunchKernelGGL(gen_convert_kernel<MM>, dim3((uint32_t)blocks), dim3(Geo<MM>::THREADS), 0, a.stream, G, \
-                     a.src_dev, tb.W, tb.Z, a.k, a.level, fmt.bits, fmt.limbs)
+                     a.src_dev, tb.Wlo, tb.Whi, tb.Z, a.k, a.level, fmt.bits, fmt.limbs)
   switch (a.N) {
     case 256: GEN_CONV(128); break;
     case 512: GEN_CONV(256); break;

@@ -135,7 +135,8 @@ def generic_error_bound(k: int, N: int, l: int, logB: int, bits: int, fbsk_gpu=N
     u = 2.0 ** -53
     M = N / 2.0
     logM = np.log2(M)
-    eta = u + 4.0 * u / (1.0 - 4.0 * u) * (np.sqrt(2.0) + u)
+    mu = 5.0 * u  # two-level twiddle tables: products of two correctly rounded entries
+    eta = mu + 4.0 * u / (1.0 - 4.0 * u) * (np.sqrt(2.0) + mu)
     gamma = 2.0 * logM * eta / (1.0 - 2.0 * logM * eta)
     T = -(-logB // bits)
     dbits = min(logB, bits)

@@ -23,7 +23,7 @@
 //   gen_step_kernel  per (ciphertext, polynomial): inverse transforms of the L slots, exact
 //                    recombination into the accumulator, then the next step's rotation
 //                    X^{a_{i+1}} acc - acc, decomposition and forward transforms -> X.
-// Transforms are block-wide radix-4 Stockham FFTs in LDS (one polynomial per workgroup).
+// Transforms are radix-8 Stockham FFTs in LDS (one polynomial per wave group of a workgroup).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -47,7 +47,7 @@ namespace chip {
 // products of a digit polynomial (||d||_2 <= sqrt(N) 2^(dbits-1)) with a key limb spectrum
 // (|G| <= maxG) through a forward transform, the pointwise product and an inverse transform
 // (Higham, Accuracy and Stability, Thm 24.2, twiddle error mu = 5u for the two-level twiddle
-// tables; gamma doubled for the radix-4 schedule), plus the
+// tables; gamma doubled for the radix-8/4 schedule), plus the
 // f64 key transform (||dG||_2 <= gamma ||g||_2, ||g||_2 <= sqrt(N) 2^(b-1)) and the final
 // rounding of the largest output.  maxG <= 0 selects the random-key estimate
 // 8 sqrt(M) 2^(b-1) sqrt(2) used by the gate; tests certify each key with its measured maxG
@@ -106,7 +106,7 @@ bool generic_pbs_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
 namespace gen {
 
 // ------------------------------------------------------------------------------------------
-// block FFT (LDS, in place, radix-4 Stockham passes + one radix-2 pass when log2 M is odd)
+// block FFT (LDS, in place, radix-8 Stockham passes after one radix-2/4 pass; radix-4 for M <= 256)
 // ------------------------------------------------------------------------------------------
 template <int M>
 struct Geo {
@@ -119,6 +119,15 @@ struct Geo {
   static_assert((1 << LOG) == M, "M");
   static_assert(VPT % 4 == 0, "values per thread");
 };
+
+// Synchronisation of one polynomial's threads around its LDS passes: a polynomial of up to 64
+// threads lives in one wave, whose LDS operations execute in issue order, so only the compiler
+// has to be fenced; larger polynomials span waves and take a workgroup barrier.
+template <int M>
+__device__ __forceinline__ void poly_sync() {
+  if constexpr (Geo<M>::THREADS <= 64) wave_lds_fence();
+  else __syncthreads();
+}
 
 // Twiddle e^{-+2 pi i idx/M} from two LDS tables: W[j] = Wlo[j mod TW_LO] * Whi[j / TW_LO]
 // (W points at Wlo; Whi follows it).
@@ -151,7 +160,7 @@ __device__ __forceinline__ void stockham_pass(cplx* buf, const cplx* W, int tid,
 #pragma unroll
     for (int r = 0; r < R; ++r) v[s][r] = buf[j + r * (M / R)];
   }
-  __syncthreads();
+  poly_sync<M>();
 #pragma unroll
   for (int s = 0; s < NB; ++s) {
     const int j = tid + s * TH;
@@ -163,32 +172,50 @@ __device__ __forceinline__ void stockham_pass(cplx* buf, const cplx* W, int tid,
       const cplx x0 = v[s][0], x1 = v[s][1];
       v[s][0] = cadd(x0, x1);
       v[s][1] = csub(x0, x1);
-    } else {
+    } else if constexpr (R == 4) {
       const cplx t0 = cadd(v[s][0], v[s][2]), t1 = csub(v[s][0], v[s][2]);
       const cplx t2 = cadd(v[s][1], v[s][3]), t3 = mul_mi<INV>(csub(v[s][1], v[s][3]));
       v[s][0] = cadd(t0, t2);
       v[s][2] = csub(t0, t2);
       v[s][1] = cadd(t1, t3);
       v[s][3] = csub(t1, t3);
+    } else {
+      dft8<INV>(v[s]);
     }
     const int d = (j - kk) * R + kk;
 #pragma unroll
     for (int r = 0; r < R; ++r) buf[d + r * Ns] = v[s][r];
   }
-  __syncthreads();
+  poly_sync<M>();
 }
 
 // Unnormalised DFT of buf (M complex, natural order) in place: forward e^{-2 pi i jk/M},
 // inverse e^{+2 pi i jk/M}; W[j] = e^{-2 pi i j/M}.  Callers synchronise before the call.
 template <int M, bool INV>
 __device__ __forceinline__ void fft_block(cplx* buf, const cplx* W, int tid) {
-  int Ns = 1;
-  if constexpr (Geo<M>::LOG & 1) {
-    stockham_pass<M, 2, INV>(buf, W, tid, Ns);
-    Ns = 2;
-  }
+  constexpr int LOG = Geo<M>::LOG;
+  if constexpr (Geo<M>::VPT >= 8) {
+    // radix-8 passes (three 8-point stages in registers per LDS round trip), the leftover
+    // factor 2 or 4 first (its stride-1 pass needs no twiddles)
+    int Ns = 1;
+    if constexpr (LOG % 3 == 1) {
+      stockham_pass<M, 2, INV>(buf, W, tid, Ns);
+      Ns = 2;
+    } else if constexpr (LOG % 3 == 2) {
+      stockham_pass<M, 4, INV>(buf, W, tid, Ns);
+      Ns = 4;
+    }
 #pragma unroll 1
-  for (; Ns < M; Ns *= 4) stockham_pass<M, 4, INV>(buf, W, tid, Ns);
+    for (; Ns < M; Ns *= 8) stockham_pass<M, 8, INV>(buf, W, tid, Ns);
+  } else {
+    int Ns = 1;
+    if constexpr (LOG & 1) {
+      stockham_pass<M, 2, INV>(buf, W, tid, Ns);
+      Ns = 2;
+    }
+#pragma unroll 1
+    for (; Ns < M; Ns *= 4) stockham_pass<M, 4, INV>(buf, W, tid, Ns);
+  }
 }
 
 // tfhe SignedDecomposer::decompose_one_level on a 64-bit state (digits up to 64 bits)
@@ -274,7 +301,7 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
       const cplx* Ym = Yc + (uint64_t)m * M;
 #pragma unroll
       for (int e = 0; e < VPT; ++e) buf[tid + e * TH] = live ? Ym[tid + e * TH] : cplx{0.0, 0.0};
-      __syncthreads();
+      poly_sync<M>();
       fft_block<M, true>(buf, W, tid);
       const uint32_t sh = m * a.bits;
 #pragma unroll
@@ -288,7 +315,7 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
           A[e + VPT] += ((uint64_t)__double_as_longlong(ti) - RND_MAGIC_BITS) << sh;
         }
       }
-      __syncthreads();
+      poly_sync<M>();
     }
   }
 
@@ -304,7 +331,7 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
     uint64_t* accl = reinterpret_cast<uint64_t*>(buf);
 #pragma unroll
     for (int e = 0; e < 2 * VPT; ++e) accl[coef(e)] = A[e];
-    __syncthreads();
+    poly_sync<M>();
     const int nrep = 64 - (int)(a.level * a.base_log);
 #pragma unroll
     for (int e = 0; e < 2 * VPT; ++e) {
@@ -313,7 +340,7 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
       const uint64_t x = (src < (uint32_t)N ? rv : 0ull - rv) - A[e];
       A[e] = nrep > 0 ? decomp_init(x, nrep) : x;  // decomposer state (reuses A)
     }
-    __syncthreads();
+    poly_sync<M>();
     cplx* Xc = a.X + ((uint64_t)ct * K1 + c) * a.level * a.subs * (uint64_t)M;
     const int logB = (int)a.base_log;
     const int sb = (int)a.bits;
@@ -338,13 +365,13 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
           const int j = tid + e * TH;
           buf[j] = cmul(cplx{(double)s0, (double)s1}, a.Z[j]);
         }
-        __syncthreads();
+        poly_sync<M>();
         fft_block<M, false>(buf, W, tid);
         cplx* dst = Xc + ((uint64_t)q * a.subs + t) * M;
         if (live)
 #pragma unroll
           for (int e = 0; e < VPT; ++e) dst[tid + e * TH] = buf[tid + e * TH];
-        __syncthreads();
+        poly_sync<M>();
       }
     }
   }

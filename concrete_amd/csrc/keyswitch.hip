@@ -17,9 +17,11 @@ namespace chip {
 constexpr int KS_TILE = 8;
 constexpr int KS_THREADS = 256;
 constexpr int KS_ICHUNK = 32;
-constexpr int KS_MAX_OUT = 3 * KS_THREADS;  // n_out + 1 <= 768
+constexpr int KS_MAX_U = 4;                       // output words per thread per sample
+constexpr int KS_MAX_OUT = KS_MAX_U * KS_THREADS;  // n_out + 1 <= 1024 (the optimizer's n <= 1006 rows)
 constexpr int KS_MAX_L = 8;
 
+template <int U>
 __global__ void __launch_bounds__(KS_THREADS)
 keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx, const uint64_t* __restrict__ in,
                  const uint64_t* __restrict__ in_idx, const uint64_t* __restrict__ ksk, uint32_t n_in,
@@ -28,11 +30,11 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
   const uint32_t s0 = blockIdx.x * KS_TILE;
   const int tid = threadIdx.x;
   const uint32_t W = n_out + 1;
-  uint64_t acc[KS_TILE][3];
+  uint64_t acc[KS_TILE][U];
 #pragma unroll
   for (int s = 0; s < KS_TILE; ++s)
 #pragma unroll
-    for (int u = 0; u < 3; ++u) acc[s][u] = 0ull;
+    for (int u = 0; u < U; ++u) acc[s][u] = 0ull;
   const int nrep = 64 - (int)(level * base_log);
 
   for (uint32_t i0 = 0; i0 < n_in; i0 += KS_ICHUNK) {
@@ -51,7 +53,7 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
       for (uint32_t t = 0; t < level; ++t) {
         const uint64_t* row = ksk + ((uint64_t)(i0 + ii) * level + t) * W;
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {
+        for (int u = 0; u < U; ++u) {
           const uint32_t j = tid + u * KS_THREADS;
           const uint64_t kv = j < W ? row[j] : 0ull;
 #pragma unroll
@@ -67,7 +69,7 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
     const uint64_t* ci = in + (in_idx ? in_idx[smp] : smp) * (uint64_t)(n_in + 1);
     uint64_t* co = out + (out_idx ? out_idx[smp] : smp) * (uint64_t)W;
 #pragma unroll
-    for (int u = 0; u < 3; ++u) {
+    for (int u = 0; u < U; ++u) {
       const uint32_t j = tid + u * KS_THREADS;
       if (j < W) co[j] = acc[s][u] + (j == n_out ? ci[n_in] : 0ull);
     }
@@ -82,8 +84,17 @@ int keyswitch_launch(const KsArgs& a) {
   }
   const uint32_t blocks = (a.num_samples + KS_TILE - 1) / KS_TILE;
   if (blocks == 0) return 0;
-  hipLaunchKernelGGL(keyswitch_kernel, dim3(blocks), dim3(KS_THREADS), 0, a.stream, a.out, a.out_idx, a.in,
-                     a.in_idx, a.ksk, a.n_in, a.n_out, a.base_log, a.level, a.num_samples);
+  const uint32_t U = (a.n_out + 1 + KS_THREADS - 1) / KS_THREADS;
+#define KS_LAUNCH(UU)                                                                                          \
+  hipLaunchKernelGGL(keyswitch_kernel<UU>, dim3(blocks), dim3(KS_THREADS), 0, a.stream, a.out, a.out_idx, a.in, \
+                     a.in_idx, a.ksk, a.n_in, a.n_out, a.base_log, a.level, a.num_samples)
+  switch (U) {
+    case 1: KS_LAUNCH(1); break;
+    case 2: KS_LAUNCH(2); break;
+    case 3: KS_LAUNCH(3); break;
+    default: KS_LAUNCH(4); break;
+  }
+#undef KS_LAUNCH
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("keyswitch launch failed: %s", hipGetErrorString(e));

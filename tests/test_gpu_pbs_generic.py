@@ -131,3 +131,21 @@ def test_generic_outside_exact_range_refused(B):
     """Sets whose certified bound would exceed the gate are refused, not rounded wrongly."""
     assert not B.pbs_supported(B.PbsParams(n=8, k=1, N=32768, level=2, base_log=15))
     assert not B.pbs_supported(B.PbsParams(n=8, k=1, N=4096, level=1, base_log=40))
+
+
+@pytest.mark.parametrize("bits", [4, 6])
+def test_keyswitch_optimizer_rows(B, oracle, torch_cuda, bits):
+    """Batched keyswitch kN -> n at the optimizer rows' sizes (n up to 880 + 1 output words),
+    bit-exact vs the oracle (keyswitch.rs:185-223 semantics)."""
+    p = B.OPTIMIZER_SETS[bits]
+    glwe_sk = B.binary_key(p.big_n, 7300 + bits)
+    lwe_sk = B.binary_key(p.n, 7310 + bits)
+    ksk = B.ksk_generate(p, glwe_sk, lwe_sk, 7320 + bits)
+    rng = np.random.RandomState(bits)
+    cts = rng.randint(0, 2 ** 63, size=(9, p.big_n + 1), dtype=np.int64).astype(np.uint64) * np.uint64(2) + \
+        np.uint64(1)
+    dev = "cuda:0"
+    out = B.keyswitch(p, B.to_device(ksk, dev), B.to_device(cts, dev))
+    torch_cuda.cuda.synchronize()
+    op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, ks_l=p.ks_level, ks_logB=p.ks_base_log)
+    assert np.array_equal(B.to_host(out), oracle.keyswitch_batch(op, cts, ksk))

@@ -9,6 +9,8 @@
 // Mapping: a workgroup owns KS_TILE samples; each KSK row (one (i, t) pair, n_out+1 words)
 // is read once per tile with 2 KB coalesced loads and applied to all KS_TILE samples, so
 // the 20.7 MB (cfg2) key is streamed B / KS_TILE times instead of B times.
+#include <algorithm>
+
 #include "common.hpp"
 #include "pbs.hpp"
 
@@ -21,11 +23,23 @@ constexpr int KS_MAX_U = 4;                       // output words per thread per
 constexpr int KS_MAX_OUT = KS_MAX_U * KS_THREADS;  // n_out + 1 <= 1024 (the optimizer's n <= 1006 rows)
 constexpr int KS_MAX_L = 8;
 
-template <int U>
+// Split-K (SPLIT): blockIdx.y takes mask positions [i_begin, i_end) and adds its partial sums
+// into pre-zeroed outputs with 64-bit atomics (wrapping addition is exact and order-free, so
+// the result is bit-identical); split 0 adds the body.  Used when the batch alone gives too
+// few workgroups for the chip (large n_in, small batches).
+__global__ void keyswitch_zero_kernel(uint64_t* out, const uint64_t* out_idx, uint32_t W, uint32_t num_samples) {
+  const uint64_t total = (uint64_t)W * num_samples;
+  for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < total; g += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t smp = (uint32_t)(g / W), j = (uint32_t)(g % W);
+    out[(out_idx ? out_idx[smp] : smp) * (uint64_t)W + j] = 0ull;
+  }
+}
+
+template <int U, bool SPLIT>
 __global__ void __launch_bounds__(KS_THREADS)
 keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx, const uint64_t* __restrict__ in,
                  const uint64_t* __restrict__ in_idx, const uint64_t* __restrict__ ksk, uint32_t n_in,
-                 uint32_t n_out, uint32_t base_log, uint32_t level, uint32_t num_samples) {
+                 uint32_t n_out, uint32_t base_log, uint32_t level, uint32_t num_samples, uint32_t i_per_split) {
   __shared__ int32_t dig[KS_TILE][KS_ICHUNK][KS_MAX_L];
   const uint32_t s0 = blockIdx.x * KS_TILE;
   const int tid = threadIdx.x;
@@ -37,18 +51,20 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
     for (int u = 0; u < U; ++u) acc[s][u] = 0ull;
   const int nrep = 64 - (int)(level * base_log);
 
-  for (uint32_t i0 = 0; i0 < n_in; i0 += KS_ICHUNK) {
+  const uint32_t i_begin = SPLIT ? blockIdx.y * i_per_split : 0u;
+  const uint32_t i_end = SPLIT ? min(n_in, i_begin + i_per_split) : n_in;
+  for (uint32_t i0 = i_begin; i0 < i_end; i0 += KS_ICHUNK) {
     __syncthreads();
     for (int e = tid; e < KS_TILE * KS_ICHUNK; e += KS_THREADS) {
       const int s = e / KS_ICHUNK, ii = e % KS_ICHUNK;
       const uint32_t smp = s0 + s, i = i0 + ii;
       uint64_t a = 0ull;
-      if (smp < num_samples && i < n_in) a = in[(in_idx ? in_idx[smp] : smp) * (uint64_t)(n_in + 1) + i];
+      if (smp < num_samples && i < i_end) a = in[(in_idx ? in_idx[smp] : smp) * (uint64_t)(n_in + 1) + i];
       uint64_t st = decomp_init(a, nrep);
       for (uint32_t t = 0; t < level; ++t) dig[s][ii][t] = decomp_next(st, (int)base_log);
     }
     __syncthreads();
-    const uint32_t iend = min(KS_ICHUNK, (int)(n_in - i0));
+    const uint32_t iend = min(KS_ICHUNK, (int)(i_end - i0));
     for (uint32_t ii = 0; ii < iend; ++ii) {
       for (uint32_t t = 0; t < level; ++t) {
         const uint64_t* row = ksk + ((uint64_t)(i0 + ii) * level + t) * W;
@@ -71,7 +87,10 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t j = tid + u * KS_THREADS;
-      if (j < W) co[j] = acc[s][u] + (j == n_out ? ci[n_in] : 0ull);
+      if (j >= W) continue;
+      const uint64_t v = acc[s][u] + (j == n_out && (!SPLIT || blockIdx.y == 0) ? ci[n_in] : 0ull);
+      if constexpr (SPLIT) atomicAdd((unsigned long long*)&co[j], (unsigned long long)v);
+      else co[j] = v;
     }
   }
 }
@@ -85,9 +104,23 @@ int keyswitch_launch(const KsArgs& a) {
   const uint32_t blocks = (a.num_samples + KS_TILE - 1) / KS_TILE;
   if (blocks == 0) return 0;
   const uint32_t U = (a.n_out + 1 + KS_THREADS - 1) / KS_THREADS;
-#define KS_LAUNCH(UU)                                                                                          \
-  hipLaunchKernelGGL(keyswitch_kernel<UU>, dim3(blocks), dim3(KS_THREADS), 0, a.stream, a.out, a.out_idx, a.in, \
-                     a.in_idx, a.ksk, a.n_in, a.n_out, a.base_log, a.level, a.num_samples)
+  // enough workgroups for 256 CUs: split the mask positions when the batch alone is short
+  uint32_t splits = 1;
+  if (blocks < 512) splits = std::min<uint32_t>((512 + blocks - 1) / blocks, std::max<uint32_t>(1, a.n_in / 128));
+  const uint32_t per = ((a.n_in + splits - 1) / splits + KS_ICHUNK - 1) / KS_ICHUNK * KS_ICHUNK;
+  splits = (a.n_in + per - 1) / per;
+  if (splits > 1) {
+    const uint64_t total = (uint64_t)(a.n_out + 1) * a.num_samples;
+    hipLaunchKernelGGL(keyswitch_zero_kernel, dim3((uint32_t)std::min<uint64_t>((total + 255) / 256, 4096)), dim3(256),
+                       0, a.stream, a.out, a.out_idx, a.n_out + 1, a.num_samples);
+  }
+#define KS_LAUNCH(UU)                                                                                            \
+  if (splits > 1)                                                                                                \
+    hipLaunchKernelGGL((keyswitch_kernel<UU, true>), dim3(blocks, splits), dim3(KS_THREADS), 0, a.stream, a.out, \
+                       a.out_idx, a.in, a.in_idx, a.ksk, a.n_in, a.n_out, a.base_log, a.level, a.num_samples, per); \
+  else                                                                                                           \
+    hipLaunchKernelGGL((keyswitch_kernel<UU, false>), dim3(blocks), dim3(KS_THREADS), 0, a.stream, a.out,       \
+                       a.out_idx, a.in, a.in_idx, a.ksk, a.n_in, a.n_out, a.base_log, a.level, a.num_samples, per)
   switch (U) {
     case 1: KS_LAUNCH(1); break;
     case 2: KS_LAUNCH(2); break;

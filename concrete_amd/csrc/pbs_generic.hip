@@ -346,6 +346,10 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
     const int sb = (int)a.bits;
     const uint64_t half = 1ull << (sb - 1);
     const uint64_t bmask = (1ull << sb) - 1ull;
+    // STAGE (large M): the twisted sub-digit inputs of all l T transforms go to their X slots
+    // first, so no decomposition state is live across the transforms (no register spills at
+    // 1024 threads); each slot is then transformed in place through LDS.
+    constexpr bool STAGE = M >= 8192;
 #pragma unroll 1
     for (uint32_t q = 0; q < a.level; ++q) {
       int64_t D[2 * VPT];
@@ -353,6 +357,7 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
       for (int e = 0; e < 2 * VPT; ++e) D[e] = decomp_next64(A[e], logB);
 #pragma unroll 1
       for (uint32_t t = 0; t < a.subs; ++t) {
+        cplx* dst = Xc + ((uint64_t)q * a.subs + t) * M;
 #pragma unroll
         for (int e = 0; e < VPT; ++e) {
           int64_t s0 = D[e], s1 = D[e + VPT];
@@ -363,11 +368,31 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
             D[e + VPT] = (D[e + VPT] - s1) >> sb;
           }
           const int j = tid + e * TH;
-          buf[j] = cmul(cplx{(double)s0, (double)s1}, a.Z[j]);
+          const cplx z = cmul(cplx{(double)s0, (double)s1}, a.Z[j]);
+          if constexpr (STAGE) {
+            if (live) dst[j] = z;
+          } else {
+            buf[j] = z;
+          }
         }
+        if constexpr (!STAGE) {
+          poly_sync<M>();
+          fft_block<M, false>(buf, W, tid);
+          if (live)
+#pragma unroll
+            for (int e = 0; e < VPT; ++e) dst[tid + e * TH] = buf[tid + e * TH];
+          poly_sync<M>();
+        }
+      }
+    }
+    if constexpr (STAGE) {
+#pragma unroll 1
+      for (uint32_t x = 0; x < a.level * a.subs; ++x) {
+        cplx* dst = Xc + (uint64_t)x * M;
+#pragma unroll
+        for (int e = 0; e < VPT; ++e) buf[tid + e * TH] = live ? dst[tid + e * TH] : cplx{0.0, 0.0};
         poly_sync<M>();
         fft_block<M, false>(buf, W, tid);
-        cplx* dst = Xc + ((uint64_t)q * a.subs + t) * M;
         if (live)
 #pragma unroll
           for (int e = 0; e < VPT; ++e) dst[tid + e * TH] = buf[tid + e * TH];

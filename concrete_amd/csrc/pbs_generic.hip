@@ -146,6 +146,11 @@ __device__ __forceinline__ void load_twiddles(cplx* tw, const cplx* Wlo, const c
   for (int e = t; e < TW_LO + NHI; e += nt) tw[e] = e < TW_LO ? Wlo[e] : Whi[e - TW_LO];
 }
 
+// LDS slot of complex element i: bits 1-3 XOR bits 4-6, so the strided writes of the first
+// Stockham passes (stride 8, 16, 32 elements) and the contiguous reads hit 8 distinct 16-byte
+// bank groups per 8-lane group (gfx950 ds_write_b128/ds_read_b128 lane groups).
+__device__ __forceinline__ int sw(int i) { return i ^ (((i >> 4) & 7) << 1); }
+
 // One Stockham pass of radix R at stride Ns (natural order in, natural order out).  Every
 // thread reads all its inputs before the barrier and writes after it, so the pass is in place.
 template <int M, int R, bool INV>
@@ -158,7 +163,7 @@ __device__ __forceinline__ void stockham_pass(cplx* buf, const cplx* W, int tid,
   for (int s = 0; s < NB; ++s) {
     const int j = tid + s * TH;
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[s][r] = buf[j + r * (M / R)];
+    for (int r = 0; r < R; ++r) v[s][r] = buf[sw(j + r * (M / R))];
   }
   poly_sync<M>();
 #pragma unroll
@@ -184,7 +189,7 @@ __device__ __forceinline__ void stockham_pass(cplx* buf, const cplx* W, int tid,
     }
     const int d = (j - kk) * R + kk;
 #pragma unroll
-    for (int r = 0; r < R; ++r) buf[d + r * Ns] = v[s][r];
+    for (int r = 0; r < R; ++r) buf[sw(d + r * Ns)] = v[s][r];
   }
   poly_sync<M>();
 }
@@ -300,14 +305,14 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
     for (uint32_t m = 0; m < a.limbs; ++m) {
       const cplx* Ym = Yc + (uint64_t)m * M;
 #pragma unroll
-      for (int e = 0; e < VPT; ++e) buf[tid + e * TH] = live ? Ym[tid + e * TH] : cplx{0.0, 0.0};
+      for (int e = 0; e < VPT; ++e) buf[sw(tid + e * TH)] = live ? Ym[tid + e * TH] : cplx{0.0, 0.0};
       poly_sync<M>();
       fft_block<M, true>(buf, W, tid);
       const uint32_t sh = m * a.bits;
 #pragma unroll
       for (int e = 0; e < VPT; ++e) {
         const int j = tid + e * TH;
-        const cplx z = cmulc(buf[j], a.Z[j]);
+        const cplx z = cmulc(buf[sw(j)], a.Z[j]);
         const double tr = z.re + RND_MAGIC, ti = z.im + RND_MAGIC;
         max_resid = fmax(max_resid, fmax(fabs(z.re - (tr - RND_MAGIC)), fabs(z.im - (ti - RND_MAGIC))));
         if (sh < 64) {
@@ -372,7 +377,7 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
           if constexpr (STAGE) {
             if (live) dst[j] = z;
           } else {
-            buf[j] = z;
+            buf[sw(j)] = z;
           }
         }
         if constexpr (!STAGE) {
@@ -380,7 +385,7 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
           fft_block<M, false>(buf, W, tid);
           if (live)
 #pragma unroll
-            for (int e = 0; e < VPT; ++e) dst[tid + e * TH] = buf[tid + e * TH];
+            for (int e = 0; e < VPT; ++e) dst[tid + e * TH] = buf[sw(tid + e * TH)];
           poly_sync<M>();
         }
       }
@@ -390,12 +395,12 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
       for (uint32_t x = 0; x < a.level * a.subs; ++x) {
         cplx* dst = Xc + (uint64_t)x * M;
 #pragma unroll
-        for (int e = 0; e < VPT; ++e) buf[tid + e * TH] = live ? dst[tid + e * TH] : cplx{0.0, 0.0};
+        for (int e = 0; e < VPT; ++e) buf[sw(tid + e * TH)] = live ? dst[tid + e * TH] : cplx{0.0, 0.0};
         poly_sync<M>();
         fft_block<M, false>(buf, W, tid);
         if (live)
 #pragma unroll
-          for (int e = 0; e < VPT; ++e) dst[tid + e * TH] = buf[tid + e * TH];
+          for (int e = 0; e < VPT; ++e) dst[tid + e * TH] = buf[sw(tid + e * TH)];
         poly_sync<M>();
       }
     }
@@ -573,14 +578,14 @@ __global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, c
       gv[e] = (gv[e] - (uint64_t)s0) >> bits;
       gv[e + VPT] = (gv[e + VPT] - (uint64_t)s1) >> bits;
       const int j = tid + e * TH;
-      buf[j] = cmul(cplx{(double)s0, (double)s1}, Z[j]);
+      buf[sw(j)] = cmul(cplx{(double)s0, (double)s1}, Z[j]);
     }
     __syncthreads();
     fft_block<M, false>(buf, W, tid);
     cplx* dst = G + ((((i * K1 + c) * limbs + lim) * K1 + r) * level + q) * (uint64_t)M;
 #pragma unroll
     for (int e = 0; e < VPT; ++e) {
-      const cplx x = buf[tid + e * TH];
+      const cplx x = buf[sw(tid + e * TH)];
       dst[tid + e * TH] = {x.re * scale, x.im * scale};
     }
     __syncthreads();

@@ -352,3 +352,23 @@ def test_cfg4_shape_fft_equals_karatsuba(oracle):
     assert np.array_equal(r_fft, r_kar)
     dec = oracle.lwe_decrypt_batch(glwe, r_fft, p.big_n)
     assert [oracle.decode(int(d), width) for d in dec] == [int(table[m]) for m in msgs]
+
+
+def test_generic_error_bound_matches_the_kernel_gate(oracle):
+    """The certified bound the GPU tests evaluate (oracle/pyoracle.py) is the same formula the
+    library's exactness gate uses (concrete_amd/csrc/pbs_generic.hip:generic_error_bound)."""
+    import ctypes as C
+
+    from concrete_amd import _native
+    L = _native.lib()
+    for k, N, l, logB in [(5, 256, 1, 15), (3, 512, 1, 18), (2, 1024, 1, 23), (1, 4096, 1, 22), (1, 16384, 2, 15),
+                          (4, 512, 3, 12), (1, 2048, 2, 10)]:
+        limbs, bits = C.c_uint32(), C.c_uint32()
+        assert L.concrete_hip_bsk_format(k, N, l, C.byref(limbs), C.byref(bits)) == 3
+        for maxg in (0.0, 1e5, 3e6):
+            c_val = L.concrete_hip_generic_error_bound(k, N, l, logB, maxg)
+            if maxg == 0.0:
+                py = oracle.generic_error_bound(k, N, l, logB, bits.value)
+            else:  # a one-value "key" whose spectrum magnitude is maxg (scaled by 1/M like the device key)
+                py = oracle.generic_error_bound(k, N, l, logB, bits.value, np.array([maxg / (N / 2), 0.0]))
+            assert abs(c_val - py) <= 1e-12 * max(1.0, abs(py)), (k, N, l, logB, maxg, c_val, py)

@@ -234,7 +234,9 @@ def main():
         bitexact = None
         cpu = None
         traffic, traffic_src = pmc_traffic(args.batch, args.config)
-        if args.verify or not args.no_cpu_baseline:
+        # the CPU baseline is timed at N = 1 only (a reported baseline, not part of the scaling runs)
+        cpu_leg = not args.no_cpu_baseline and world == 1
+        if args.verify or cpu_leg:
             from oracle import pyoracle as O  # checker / CPU baseline only
             opt = args.config.startswith("opt")
             if bsk is None:
@@ -252,7 +254,7 @@ def main():
             if args.verify:
                 ref, _ = O.pbs_batch(op, cts[: args.verify], acc[None, :], nthreads=args.cpu_threads, **kw)
                 bitexact = bool(np.array_equal(ref, out[: args.verify]))
-            if not args.no_cpu_baseline:
+            if cpu_leg:
                 sample = cts[: args.cpu_sample]
                 t1 = time.perf_counter()
                 O.pbs_batch(op, sample, acc[None, :], nthreads=args.cpu_threads, **kw)

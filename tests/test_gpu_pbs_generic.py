@@ -149,3 +149,43 @@ def test_keyswitch_optimizer_rows(B, oracle, torch_cuda, bits):
     torch_cuda.cuda.synchronize()
     op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, ks_l=p.ks_level, ks_logB=p.ks_base_log)
     assert np.array_equal(B.to_host(out), oracle.keyswitch_batch(op, cts, ksk))
+
+
+@pytest.mark.parametrize("bits", list(range(1, 9)))
+def test_reference_fixtures_at_optimizer_rows(B, torch_cuda, bits):
+    """The reference generators' cleartext vectors (tests/golden/reference_lut_fixtures.json,
+    apply_lookup_table / linalg_apply_lookup_table, every signedness variant) of width p, run at
+    the optimizer's own p-bit row (full n, secure noise; v0_last_128) as one mapped-LUT batch:
+    every output decodes to the reference's expected value.  p = 5 runs on the N = 2048 kernel,
+    the others on the general path."""
+    import json
+    import math
+    import os
+    golden = os.path.join(os.path.dirname(__file__), "golden", "reference_lut_fixtures.json")
+    fx = json.load(open(golden))
+    cases = [c for c in fx["apply_lookup_table"] + fx["linalg_apply_lookup_table"]
+             if int(math.log2(len(c["lut"]))) == bits and not c["description"].endswith("_2layer")]
+    assert len(cases) >= 15
+    p = B.OPTIMIZER_SETS[bits]
+    assert B.pbs_supported(p)
+    lwe_sk = B.binary_key(p.n, 7400 + bits)
+    glwe_sk = B.binary_key(p.big_n, 7410 + bits)
+    fbsk = B.convert_bsk(p, B.bsk_generate(p, lwe_sk, glwe_sk, 7420 + bits), "cuda:0")
+    pts, lut_idx, expect, luts = [], [], [], []
+    for ci, c in enumerate(cases):
+        table = np.array(c["lut"], dtype=np.int64).view(np.uint64)
+        luts.append(B.trivial_glwe(p, B.expand_lut(table, p.N, bits, c["input_signed"])))
+        for x, e in zip(c["input"], c["expected"]):
+            pt = int(B.encode(int(x) & ((1 << 64) - 1), bits))
+            if c["input_signed"]:  # FHEToTFHEScalar.cpp:373-413: offset 2^(p-1) on the body
+                pt = (pt + int(B.encode(1 << (bits - 1), bits))) & ((1 << 64) - 1)
+            pts.append(pt)
+            lut_idx.append(ci)
+            expect.append((e, c["output_signed"]))
+    cts = B.lwe_encrypt(lwe_sk, pts, p.n, B.secure_std(1, p.n), 7430 + bits)
+    dev = "cuda:0"
+    out = B.pbs(p, fbsk, B.to_device(cts, dev), B.to_device(np.stack(luts), dev),
+                lut_idx=B.to_device(np.array(lut_idx, dtype=np.uint64), dev))
+    torch_cuda.cuda.synchronize()
+    dec = B.lwe_decrypt(glwe_sk, B.to_host(out), p.big_n)
+    assert [B.decode(d, bits, s) for d, (_, s) in zip(dec, expect)] == [e for e, _ in expect]

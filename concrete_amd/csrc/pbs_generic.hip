@@ -129,21 +129,33 @@ __device__ __forceinline__ void poly_sync() {
   else __syncthreads();
 }
 
-// Twiddle e^{-+2 pi i idx/M} from two LDS tables: W[j] = Wlo[j mod TW_LO] * Whi[j / TW_LO]
-// (W points at Wlo; Whi follows it).
+// Twiddle e^{-+2 pi i idx/M} from LDS: the full correctly rounded table for M <= FULL_TW_MAX,
+// else two tables, W[j] = Wlo[j mod TW_LO] * Whi[j / TW_LO] (error <= 5u: the bound's mu).
 constexpr int TW_LO = 128;
-template <bool INV>
+constexpr int FULL_TW_MAX = 2048;
+template <int M>
+constexpr int tw_entries() {
+  return M <= FULL_TW_MAX ? M : TW_LO + (M / TW_LO > 1 ? M / TW_LO : 1);
+}
+template <int M, bool INV>
 __device__ __forceinline__ cplx twiddle(const cplx* W, int idx) {
-  const cplx w = cmul(W[idx & (TW_LO - 1)], W[TW_LO + (idx >> 7)]);
+  cplx w;
+  if constexpr (M <= FULL_TW_MAX) w = W[idx];
+  else w = cmul(W[idx & (TW_LO - 1)], W[TW_LO + (idx >> 7)]);
   return INV ? cplx{w.re, -w.im} : w;
 }
 static_assert(TW_LO == 128, "twiddle split");
 
-// stage the two-level twiddle tables of size M into LDS (tw: TW_LO + max(1, M / TW_LO) entries)
+// stage the twiddle table(s) of size M into LDS (tw_entries<M>() entries)
 template <int M>
-__device__ __forceinline__ void load_twiddles(cplx* tw, const cplx* Wlo, const cplx* Whi, int t, int nt) {
-  constexpr int NHI = M / TW_LO > 1 ? M / TW_LO : 1;
-  for (int e = t; e < TW_LO + NHI; e += nt) tw[e] = e < TW_LO ? Wlo[e] : Whi[e - TW_LO];
+__device__ __forceinline__ void load_twiddles(cplx* tw, const cplx* Wfull, const cplx* Wlo, const cplx* Whi, int t,
+                                              int nt) {
+  if constexpr (M <= FULL_TW_MAX) {
+    for (int e = t; e < M; e += nt) tw[e] = Wfull[e];
+  } else {
+    constexpr int NHI = M / TW_LO > 1 ? M / TW_LO : 1;
+    for (int e = t; e < TW_LO + NHI; e += nt) tw[e] = e < TW_LO ? Wlo[e] : Whi[e - TW_LO];
+  }
 }
 
 // LDS slot of complex element i: bits 1-3 XOR bits 4-6, so the strided writes of the first
@@ -172,7 +184,7 @@ __device__ __forceinline__ void stockham_pass(cplx* buf, const cplx* W, int tid,
     const int kk = j & (Ns - 1);
     const int step = M / (Ns * R);
 #pragma unroll
-    for (int r = 1; r < R; ++r) v[s][r] = cmul(v[s][r], twiddle<INV>(W, kk * r * step));
+    for (int r = 1; r < R; ++r) v[s][r] = cmul(v[s][r], twiddle<M, INV>(W, kk * r * step));
     if constexpr (R == 2) {
       const cplx x0 = v[s][0], x1 = v[s][1];
       v[s][0] = cadd(x0, x1);
@@ -240,6 +252,7 @@ struct StepArgs {
   uint64_t* acc;       // [chunk][K1][N] accumulators
   cplx* X;             // [chunk][K1 r][l q][T t][M] digit spectra
   const cplx* Y;       // [chunk][K1 c][L m][M] slot spectra
+  const cplx* Wfull;   // e^{-2 pi i j/M}, j < M
   const cplx* Wlo;     // e^{-2 pi i j/M}, j < TW_LO
   const cplx* Whi;     // e^{-2 pi i j TW_LO/M}
   const cplx* Z;       // zeta^j = e^{i pi j/N}
@@ -260,9 +273,9 @@ template <int M, int MODE>
 __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
   constexpr int N = 2 * M, TH = Geo<M>::THREADS, VPT = Geo<M>::VPT, LOG2_2N = Geo<M>::LOG + 2;
   constexpr int PPB = Geo<M>::PPB;
-  __shared__ cplx lds[PPB * M + TW_LO + (M / TW_LO > 1 ? M / TW_LO : 1)];
+  __shared__ cplx lds[PPB * M + tw_entries<M>()];
   cplx* W = lds + PPB * M;
-  load_twiddles<M>(W, a.Wlo, a.Whi, threadIdx.x, Geo<M>::BLOCK);
+  load_twiddles<M>(W, a.Wfull, a.Wlo, a.Whi, threadIdx.x, Geo<M>::BLOCK);
   __syncthreads();
   // polynomial group g of this workgroup: (ciphertext, GLWE polynomial) = divmod(poly, k + 1).
   // Groups past the batch keep taking part in the workgroup barriers of the transforms.
@@ -540,13 +553,14 @@ __global__ void gen_extract_kernel(uint64_t* out, const uint64_t* out_idx, const
 
 // Fourier key: G[i][c][lim][r][q][f] = FFT(twist(limb_lim(std[i][l-1-q][r][c])))[f] / M
 template <int M>
-__global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, const uint64_t* src, const cplx* Wlo,
+__global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, const uint64_t* src, const cplx* Wfull,
+                                                                        const cplx* Wlo,
                                                                         const cplx* Whi, const cplx* Z, uint32_t k,
                                                                         uint32_t level, uint32_t bits, uint32_t limbs) {
   constexpr int N = 2 * M, TH = Geo<M>::THREADS, VPT = Geo<M>::VPT;
-  __shared__ cplx buf[M + TW_LO + (M / TW_LO > 1 ? M / TW_LO : 1)];
+  __shared__ cplx buf[M + tw_entries<M>()];
   cplx* W = buf + M;
-  load_twiddles<M>(W, Wlo, Whi, threadIdx.x, TH);
+  load_twiddles<M>(W, Wfull, Wlo, Whi, threadIdx.x, TH);
   __syncthreads();
   const int tid = threadIdx.x;
   const uint32_t K1 = k + 1;
@@ -596,6 +610,7 @@ __global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, c
 // host side
 // ------------------------------------------------------------------------------------------
 struct Tables {
+  cplx* Wfull = nullptr;  // e^{-2 pi i j/M}, j < M
   cplx* Wlo = nullptr;  // e^{-2 pi i j/M}, j < TW_LO
   cplx* Whi = nullptr;  // e^{-2 pi i j TW_LO/M}, j < max(1, M/TW_LO)
   cplx* Z = nullptr;    // zeta^j, j < M
@@ -614,11 +629,14 @@ static Tables tables_for(uint32_t N) {
   const uint32_t M = N / 2, NHI = M / TW_LO > 1 ? M / TW_LO : 1;
   const long double PI = 3.14159265358979323846264338327950288L;
   auto ex = [&](long double ang) { return cplx{(double)cosl(ang), (double)sinl(ang)}; };
-  std::vector<cplx> lo(TW_LO), hi(NHI), z(M);
+  std::vector<cplx> full(M), lo(TW_LO), hi(NHI), z(M);
+  for (uint32_t j = 0; j < M; ++j) full[j] = ex(-2.0L * PI * (long double)j / (long double)M);
   for (uint32_t j = 0; j < (uint32_t)TW_LO; ++j) lo[j] = ex(-2.0L * PI * (long double)j / (long double)M);
   for (uint32_t j = 0; j < NHI; ++j) hi[j] = ex(-2.0L * PI * (long double)(j * TW_LO) / (long double)M);
   for (uint32_t j = 0; j < M; ++j) z[j] = ex(PI * (long double)j / (long double)N);
   Tables t;
+  CHIP_CHECK(hipMalloc((void**)&t.Wfull, M * sizeof(cplx)));
+  CHIP_CHECK(hipMemcpy(t.Wfull, full.data(), M * sizeof(cplx), hipMemcpyHostToDevice));
   CHIP_CHECK(hipMalloc((void**)&t.Wlo, TW_LO * sizeof(cplx)));
   CHIP_CHECK(hipMalloc((void**)&t.Whi, NHI * sizeof(cplx)));
   CHIP_CHECK(hipMalloc((void**)&t.Z, M * sizeof(cplx)));
@@ -684,7 +702,7 @@ int pbs_generic_launch(const PbsArgs& a) {
   int rc = 0;
   for (uint32_t base = 0; base < a.num_samples && rc == 0; base += chunk) {
     const uint32_t cnt = std::min(chunk, a.num_samples - base);
-    StepArgs s{acc,  X,    Y,   tb.Wlo, tb.Whi,  tb.Z,       a.in, a.in_idx, a.luts, a.lut_idx,
+    StepArgs s{acc,  X,    Y,   tb.Wfull, tb.Wlo, tb.Whi,  tb.Z,       a.in, a.in_idx, a.luts, a.lut_idx,
                a.resid, base, cnt, a.n,    a.k,     a.level, a.base_log, b,    L,        T,      0};
     rc = step_dispatch<MODE_INIT | MODE_FRONT>(a.N, s, K1, a.stream);
     MacArgs m{X, Y, reinterpret_cast<const cplx*>(a.fbsk), cnt, a.k, a.level, L, T, M, 0};
@@ -723,7 +741,7 @@ int convert_bsk_generic_launch(const ConvertArgs& a) {
   cplx* G = reinterpret_cast<cplx*>(a.dest);
 #define GEN_CONV(MM)                                                                                        \
   hipLaunchKernelGGL(gen_convert_kernel<MM>, dim3((uint32_t)blocks), dim3(Geo<MM>::THREADS), 0, a.stream, G, \
-                     a.src_dev, tb.Wlo, tb.Whi, tb.Z, a.k, a.level, fmt.bits, fmt.limbs)
+                     a.src_dev, tb.Wfull, tb.Wlo, tb.Whi, tb.Z, a.k, a.level, fmt.bits, fmt.limbs)
   switch (a.N) {
     case 256: GEN_CONV(128); break;
     case 512: GEN_CONV(256); break;

@@ -273,14 +273,23 @@ template <int M, int MODE>
 __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
   constexpr int N = 2 * M, TH = Geo<M>::THREADS, VPT = Geo<M>::VPT, LOG2_2N = Geo<M>::LOG + 2;
   constexpr int PPB = Geo<M>::PPB;
-  __shared__ cplx lds[PPB * M + tw_entries<M>()];
-  cplx* W = lds + PPB * M;
+  // ZLDS: the twist table in LDS next to the twiddles; YDMA: the slot spectra of the inverse
+  // transforms double-buffered by LDS-DMA (slot m + 1 lands while slot m is transformed)
+  constexpr bool ZLDS = M <= 1024;
+  constexpr bool YDMA = TH >= 64 && M <= 512;
+  constexpr int NBUF = YDMA ? 2 : 1;
+  __shared__ cplx lds[NBUF * PPB * M + tw_entries<M>() + (ZLDS ? M : 0)];
+  cplx* W = lds + NBUF * PPB * M;
   load_twiddles<M>(W, a.Wfull, a.Wlo, a.Whi, threadIdx.x, Geo<M>::BLOCK);
+  cplx* Zl = W + tw_entries<M>();
+  if constexpr (ZLDS)
+    for (int e = threadIdx.x; e < M; e += Geo<M>::BLOCK) Zl[e] = a.Z[e];
+  auto zeta = [&](int j) { return ZLDS ? Zl[j] : a.Z[j]; };
   __syncthreads();
   // polynomial group g of this workgroup: (ciphertext, GLWE polynomial) = divmod(poly, k + 1).
   // Groups past the batch keep taking part in the workgroup barriers of the transforms.
   const int g = threadIdx.x / TH, tid = threadIdx.x % TH;
-  cplx* buf = lds + g * M;
+  cplx* buf = lds + g * NBUF * M;
   const uint32_t K1 = a.k + 1;
   const uint64_t poly = (uint64_t)blockIdx.x * PPB + g;
   const bool live = poly < (uint64_t)a.count * K1;
@@ -314,18 +323,38 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
     // acc_c += sum_m 2^{m b} round(iFFT(Y_m) conj(zeta^j)); the key spectra carry the 1/M.
     // bits(v + MAGIC) - MAGIC_BITS = round(v) mod 2^64 for |v| < 2^51 (either sign).
     const cplx* Yc = a.Y + ((uint64_t)ct * K1 + c) * a.limbs * (uint64_t)M;
+    // YDMA: wave-linear LDS destination, swizzle applied on the source side (slot p holds
+    // element sw(p)); a group past the batch loads ciphertext 0's rows (in bounds, unused)
+    auto issue_y = [&](uint32_t m, cplx* dst) {
+      const cplx* Ym = Yc + (uint64_t)m * M;
+      const int w0 = tid & ~63, ln = tid & 63;
+#pragma unroll
+      for (int e = 0; e < VPT; ++e) {
+        const int L0 = w0 + e * TH;
+        __builtin_amdgcn_global_load_lds(Ym + sw(L0 + ln), (lds_ptr_t)(dst + L0), 16, 0, 0);
+      }
+    };
+    if constexpr (YDMA) issue_y(0, buf);
 #pragma unroll 1
     for (uint32_t m = 0; m < a.limbs; ++m) {
-      const cplx* Ym = Yc + (uint64_t)m * M;
+      cplx* cur = buf;
+      if constexpr (YDMA) {
+        cur = buf + (m & 1) * M;
+        wait_vmcnt<0>();
+        poly_sync<M>();
+        if (m + 1 < a.limbs) issue_y(m + 1, buf + ((m + 1) & 1) * M);
+      } else {
+        const cplx* Ym = Yc + (uint64_t)m * M;
 #pragma unroll
-      for (int e = 0; e < VPT; ++e) buf[sw(tid + e * TH)] = live ? Ym[tid + e * TH] : cplx{0.0, 0.0};
-      poly_sync<M>();
-      fft_block<M, true>(buf, W, tid);
+        for (int e = 0; e < VPT; ++e) cur[sw(tid + e * TH)] = live ? Ym[tid + e * TH] : cplx{0.0, 0.0};
+        poly_sync<M>();
+      }
+      fft_block<M, true>(cur, W, tid);
       const uint32_t sh = m * a.bits;
 #pragma unroll
       for (int e = 0; e < VPT; ++e) {
         const int j = tid + e * TH;
-        const cplx z = cmulc(buf[sw(j)], a.Z[j]);
+        const cplx z = cmulc(cur[sw(j)], zeta(j));
         const double tr = z.re + RND_MAGIC, ti = z.im + RND_MAGIC;
         max_resid = fmax(max_resid, fmax(fabs(z.re - (tr - RND_MAGIC)), fabs(z.im - (ti - RND_MAGIC))));
         if (sh < 64) {
@@ -386,7 +415,7 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
             D[e + VPT] = (D[e + VPT] - s1) >> sb;
           }
           const int j = tid + e * TH;
-          const cplx z = cmul(cplx{(double)s0, (double)s1}, a.Z[j]);
+          const cplx z = cmul(cplx{(double)s0, (double)s1}, zeta(j));
           if constexpr (STAGE) {
             if (live) dst[j] = z;
           } else {

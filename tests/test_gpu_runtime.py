@@ -121,3 +121,27 @@ def test_batched_bootstrap_n2048(env):
     ks.close()
     ref, _ = O.pbs_batch(op, cts, B.trivial_glwe(p, tlu)[None, :], fbsk=O.bsk_to_fourier(op, bsk))
     assert np.array_equal(got, ref)
+
+
+def test_batched_bootstrap_general_path(env):
+    """The runtime glue drives the general path (k = 3, N = 512: the optimizer's 3-bit row,
+    small n), sharded over two device entries; bit-exact vs the oracle's Karatsuba product."""
+    B, R, O = env["B"], env["R"], env["O"]
+    p = replace(B.OPTIMIZER_SETS[3], n=12)
+    lwe_sk = B.binary_key(p.n, 91)
+    glwe_sk = B.binary_key(p.big_n, 92)
+    bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 93)
+    width = 3
+    table = np.array([3, 1, 4, 1, 5, 2, 6, 5], dtype=np.uint64)
+    tlu = B.expand_lut(table, p.N, width)
+    msgs = np.array([0, 1, 2, 3, 4, 5, 6, 7, 2])
+    cts = B.lwe_encrypt(lwe_sk, [B.encode(m, width) for m in msgs], p.n, 2.0 ** -30, 94)
+    ks = R.Keyset([0, 0])
+    ks.add_bsk(0, bsk, p)
+    got = R.batched_bootstrap(ks, p, cts, tlu)
+    ks.close()
+    op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
+    ref, _ = O.pbs_batch(op, cts, B.trivial_glwe(p, tlu)[None, :], bsk=bsk, mode=O.MODE_KARATSUBA)
+    assert np.array_equal(got, ref)
+    dec = B.lwe_decrypt(glwe_sk, got, p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]

@@ -456,6 +456,134 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
   }
 }
 
+// N = 1024 (M = 512): one wave per polynomial with the register-resident transforms of
+// fft512.hpp (three radix-8 passes, one LDS transpose per direction, the twist folded into the
+// tables). Spectra are stored in the transforms' own order p = k2 * 64 + lane (frequency
+// fft512_freq(lane, k2)); X, Y and the Fourier key (gen_convert512_kernel) agree on it, and the
+// product kernels are order-agnostic. No workgroup barrier after the table build, so a wave
+// past the batch leaves at once.
+constexpr int S512_PPB = 4;  // polynomials (waves) per workgroup
+template <int MODE>
+__global__ void __launch_bounds__(64 * S512_PPB) gen_step512_kernel(StepArgs a) {
+  constexpr int M = 512, N = 1024, LOG2_2N = 11;
+  __shared__ cplx lds[FFT512_TABLE_ENTRIES + S512_PPB * PBS1024_XCH_SLOTS];
+  cplx* T1 = lds;
+  cplx* T2 = lds + 8 * T1_STRIDE;
+  build_fft512_tables(T1, T2, threadIdx.x, 64 * S512_PPB);
+  __syncthreads();
+  const Fft512Tables T{T1, T2};
+  const int g = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  cplx* xch = lds + FFT512_TABLE_ENTRIES + g * PBS1024_XCH_SLOTS;
+  const uint32_t K1 = a.k + 1;
+  const uint64_t poly = (uint64_t)blockIdx.x * S512_PPB + g;
+  if (poly >= (uint64_t)a.count * K1) return;
+  const uint32_t ct = (uint32_t)(poly / K1), c = (uint32_t)(poly % K1);
+  const uint32_t s = a.base + ct;
+  const uint64_t row = a.in_idx ? a.in_idx[s] : s;
+  const uint64_t* lwe = a.in + row * (uint64_t)(a.n + 1);
+  uint64_t* acc = a.acc + ((uint64_t)ct * K1 + c) * N;
+  // this lane's coefficients: j = lane + 64 e (e < 16); j and j + 512 pair up as (e, e + 8)
+  uint64_t A[16];
+  double max_resid = 0.0;
+
+  if constexpr ((MODE & MODE_INIT) != 0) {
+    const uint64_t* lut = a.luts + (a.lut_idx ? a.lut_idx[s] : 0ull) * (uint64_t)(K1 * N) + (uint64_t)c * N;
+    const uint32_t bt = modswitch(lwe[a.n], LOG2_2N);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t src = (lane + 64 * e + bt) & (2 * N - 1);
+      const uint64_t v = lut[src & (N - 1)];
+      A[e] = src < (uint32_t)N ? v : 0ull - v;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) A[e] = acc[lane + 64 * e];
+  }
+
+  if constexpr ((MODE & MODE_BACK) != 0) {
+    const cplx* Yc = a.Y + ((uint64_t)ct * K1 + c) * a.limbs * (uint64_t)M + lane;
+    cplx v[8], nx[8];
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) nx[k2] = Yc[64 * k2];
+#pragma unroll 1
+    for (uint32_t m = 0; m < a.limbs; ++m) {
+#pragma unroll
+      for (int k2 = 0; k2 < 8; ++k2) v[k2] = nx[k2];
+      if (m + 1 < a.limbs) {
+        const cplx* Yn = Yc + (uint64_t)(m + 1) * M;
+#pragma unroll
+        for (int k2 = 0; k2 < 8; ++k2) nx[k2] = Yn[64 * k2];
+      }
+      fft512_inv(v, xch, T, lane);
+      const uint32_t sh = m * a.bits;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const double tr = v[e].re + RND_MAGIC, ti = v[e].im + RND_MAGIC;
+        max_resid = fmax(max_resid, fmax(fabs(v[e].re - (tr - RND_MAGIC)), fabs(v[e].im - (ti - RND_MAGIC))));
+        if (sh < 64) {
+          A[e] += ((uint64_t)__double_as_longlong(tr) - RND_MAGIC_BITS) << sh;
+          A[e + 8] += ((uint64_t)__double_as_longlong(ti) - RND_MAGIC_BITS) << sh;
+        }
+      }
+    }
+    if (a.resid) {
+      for (int off = 32; off > 0; off >>= 1) max_resid = fmax(max_resid, __shfl_xor(max_resid, off));
+      if (lane == 0) atomicMax(a.resid, (unsigned long long)__double_as_longlong(max_resid));
+    }
+  }
+
+  if constexpr ((MODE & (MODE_BACK | MODE_INIT)) != 0) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[lane + 64 * e] = A[e];
+  }
+
+  if constexpr ((MODE & MODE_FRONT) != 0) {
+    // rotation through the wave's exchange scratch (1024 u64 = 8 KB of its 9.2 KB)
+    const uint32_t at = modswitch(lwe[a.step], LOG2_2N);
+    uint64_t* rot = reinterpret_cast<uint64_t*>(xch);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) rot[lane + 64 * e] = A[e];
+    wave_lds_fence();
+    const int nrep = 64 - (int)(a.level * a.base_log);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t src = (lane + 64 * e - at) & (2 * N - 1);
+      const uint64_t rv = rot[src & (N - 1)];
+      const uint64_t x = (src < (uint32_t)N ? rv : 0ull - rv) - A[e];
+      A[e] = nrep > 0 ? decomp_init(x, nrep) : x;
+    }
+    wave_lds_fence();
+    cplx* Xc = a.X + ((uint64_t)ct * K1 + c) * a.level * a.subs * (uint64_t)M + lane;
+    const int logB = (int)a.base_log, sb = (int)a.bits;
+    const uint64_t half = 1ull << (sb - 1), bmask = (1ull << sb) - 1ull;
+#pragma unroll 1
+    for (uint32_t q = 0; q < a.level; ++q) {
+      int64_t D[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) D[e] = decomp_next64(A[e], logB);
+#pragma unroll 1
+      for (uint32_t t = 0; t < a.subs; ++t) {
+        cplx v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          int64_t s0 = D[e], s1 = D[e + 8];
+          if (a.subs > 1) {  // balanced b-bit sub-digit, exact: D - s is a multiple of 2^b
+            s0 = (int64_t)(((uint64_t)D[e] + half) & bmask) - (int64_t)half;
+            s1 = (int64_t)(((uint64_t)D[e + 8] + half) & bmask) - (int64_t)half;
+            D[e] = (D[e] - s0) >> sb;
+            D[e + 8] = (D[e + 8] - s1) >> sb;
+          }
+          v[e] = {(double)s0, (double)s1};
+        }
+        fft512_fwd(v, xch, T, lane);
+        cplx* dst = Xc + ((uint64_t)q * a.subs + t) * M;
+#pragma unroll
+        for (int k2 = 0; k2 < 8; ++k2) dst[64 * k2] = v[k2];
+      }
+    }
+  }
+}
+
 // Y[ct][c][m][f] = sum over (r, q, t) with 0 <= m - t < L of X[ct][r][q][t][f] * G_i[c][m-t][r][q][f]
 struct MacArgs {
   const cplx* X;
@@ -635,6 +763,51 @@ __global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, c
   }
 }
 
+// N = 1024: the same key in gen_step512_kernel's spectral order (one wave per standard polynomial)
+__global__ void __launch_bounds__(64) gen_convert512_kernel(cplx* G, const uint64_t* src, uint32_t k,
+                                                           uint32_t level, uint32_t bits, uint32_t limbs) {
+  constexpr int M = 512, N = 1024;
+  __shared__ cplx lds[FFT512_TABLE_ENTRIES + PBS1024_XCH_SLOTS];
+  build_fft512_tables(lds, lds + 8 * T1_STRIDE, threadIdx.x, 64);
+  __syncthreads();
+  const Fft512Tables T{lds, lds + 8 * T1_STRIDE};
+  cplx* xch = lds + FFT512_TABLE_ENTRIES;
+  const int lane = threadIdx.x;
+  const uint32_t K1 = k + 1;
+  uint64_t p = blockIdx.x;
+  const uint32_t c = p % K1;
+  p /= K1;
+  const uint32_t r = p % K1;
+  p /= K1;
+  const uint32_t v = p % level;
+  const uint64_t i = p / level;
+  const uint32_t q = level - 1 - v;
+  const uint64_t* g = src + (uint64_t)blockIdx.x * N;
+  uint64_t gv[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) gv[e] = g[lane + 64 * e];
+  const double scale = 1.0 / (double)M;
+#pragma unroll 1
+  for (uint32_t lim = 0; lim < limbs; ++lim) {
+    const uint32_t w = lim + 1 < limbs ? bits : 64 - (limbs - 1) * bits;
+    const uint64_t half = 1ull << (w - 1);
+    const uint64_t bmask = (1ull << w) - 1ull;
+    cplx x[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int64_t s0 = (int64_t)((gv[e] + half) & bmask) - (int64_t)half;
+      const int64_t s1 = (int64_t)((gv[e + 8] + half) & bmask) - (int64_t)half;
+      gv[e] = (gv[e] - (uint64_t)s0) >> bits;
+      gv[e + 8] = (gv[e + 8] - (uint64_t)s1) >> bits;
+      x[e] = {(double)s0, (double)s1};
+    }
+    fft512_fwd(x, xch, T, lane);
+    cplx* dst = G + ((((i * K1 + c) * limbs + lim) * K1 + r) * level + q) * (uint64_t)M + lane;
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) dst[64 * k2] = {x[k2].re * scale, x[k2].im * scale};
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
@@ -688,7 +861,12 @@ static int step_dispatch(uint32_t N, const StepArgs& s, uint32_t K1, hipStream_t
   switch (N) {
     case 256: launch_step<128, MODE>(s, K1, st); break;
     case 512: launch_step<256, MODE>(s, K1, st); break;
-    case 1024: launch_step<512, MODE>(s, K1, st); break;
+    case 1024: {
+      const uint64_t polys = (uint64_t)s.count * K1;
+      hipLaunchKernelGGL((gen_step512_kernel<MODE>), dim3((uint32_t)((polys + S512_PPB - 1) / S512_PPB)),
+                         dim3(64 * S512_PPB), 0, st, s);
+      break;
+    }
     case 2048: launch_step<1024, MODE>(s, K1, st); break;
     case 4096: launch_step<2048, MODE>(s, K1, st); break;
     case 8192: launch_step<4096, MODE>(s, K1, st); break;
@@ -774,7 +952,10 @@ int convert_bsk_generic_launch(const ConvertArgs& a) {
   switch (a.N) {
     case 256: GEN_CONV(128); break;
     case 512: GEN_CONV(256); break;
-    case 1024: GEN_CONV(512); break;
+    case 1024:
+      hipLaunchKernelGGL(gen_convert512_kernel, dim3((uint32_t)blocks), dim3(64), 0, a.stream, G, a.src_dev, a.k,
+                         a.level, fmt.bits, fmt.limbs);
+      break;
     case 2048: GEN_CONV(1024); break;
     case 4096: GEN_CONV(2048); break;
     case 8192: GEN_CONV(4096); break;

@@ -686,6 +686,214 @@ static bool launch_mac2(const MacArgs& m, uint32_t cnt, hipStream_t st) {
   return false;
 }
 
+// ------------------------------------------------------------------------------------------
+// N <= 512: the whole bootstrap of a tile of C ciphertexts in one workgroup (one launch per
+// call).  The accumulator lives in the registers of the polynomial's thread group, the digit
+// spectra and one slot spectrum per polynomial in LDS; the key is the only data streamed per
+// CMUX step, each key value loaded once per tile and used for its C ciphertexts.  No spectra
+// go through HBM (the two-launch path moves ~170 KB of X/Y spectra per ciphertext and step).
+// ------------------------------------------------------------------------------------------
+struct TileArgs {
+  uint64_t* out;
+  const uint64_t* out_idx;
+  const uint64_t* in;
+  const uint64_t* in_idx;
+  const uint64_t* luts;
+  const uint64_t* lut_idx;
+  const cplx* G;  // Fourier key [n][K1 c][L lim][K1 l rq][M]
+  const cplx* Wfull;
+  const cplx* Z;
+  unsigned long long* resid;
+  uint32_t count, n, base_log, bits;
+};
+
+template <int M, int K1, int KL, int T, int L, int C>
+struct TileGeo {
+  static constexpr int TH = Geo<M>::THREADS;  // threads per polynomial
+  static constexpr int NT = C * K1 * TH;      // threads per workgroup
+  static constexpr int BASE = ((C * KL * T + C * K1) * M + tw_entries<M>()) * 16;
+  static constexpr bool ZLDS = BASE + M * 16 <= 160 * 1024;  // twist table in LDS when it fits
+  static constexpr int LDS = BASE + (ZLDS ? M * 16 : 0);
+  static_assert(M <= 256 && NT <= 1024 && LDS <= 160 * 1024, "tile shape");
+};
+
+template <int M, int K1, int KL, int T, int L, int C>
+__global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_kernel(TileArgs a) {
+  using TG = TileGeo<M, K1, KL, T, L, C>;
+  constexpr int N = 2 * M, TH = TG::TH, VPT = Geo<M>::VPT, NT = TG::NT, LOG2_2N = Geo<M>::LOG + 2;
+  constexpr int LV = KL / K1;                           // decomposition levels
+  constexpr int ITEMS = K1 * M, IPT = (ITEMS + NT - 1) / NT;  // product items (c, f) per thread
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  cplx* Xs = reinterpret_cast<cplx*>(smem);  // [C][KL rq][T t][M] digit spectra (slots sw(f))
+  cplx* Ys = Xs + C * KL * T * M;            // [C][K1 c][M] slot spectra / rotation scratch
+  cplx* W = Ys + C * K1 * M;
+  cplx* Zl = W + tw_entries<M>();
+  load_twiddles<M>(W, a.Wfull, nullptr, nullptr, threadIdx.x, NT);
+  if constexpr (TG::ZLDS)
+    for (int e = threadIdx.x; e < M; e += NT) Zl[e] = a.Z[e];
+  auto zeta = [&](int j) { return TG::ZLDS ? Zl[j] : a.Z[j]; };
+  const int g = threadIdx.x / TH, tid = threadIdx.x % TH;
+  const int lct = g / K1, c = g % K1;  // this group's polynomial: (ciphertext of the tile, c)
+  const uint32_t ct = blockIdx.x * C + lct;
+  const bool live = ct < a.count;  // groups past the batch run on row 0 and write nothing
+  const uint64_t row = live ? (a.in_idx ? a.in_idx[ct] : ct) : 0ull;
+  const uint64_t* lwe = a.in + row * (uint64_t)(a.n + 1);
+  cplx* ybuf = Ys + g * M;
+  auto coef = [&](int e) { return (uint32_t)(tid + (e % VPT) * TH + (e / VPT) * M); };
+  uint64_t A[2 * VPT];
+  double max_resid = 0.0;
+  {
+    const uint64_t* lut =
+        a.luts + (live && a.lut_idx ? a.lut_idx[ct] : 0ull) * (uint64_t)(K1 * N) + (uint64_t)c * N;
+    const uint32_t bt = live ? modswitch(lwe[a.n], LOG2_2N) : 0u;
+#pragma unroll
+    for (int e = 0; e < 2 * VPT; ++e) {
+      const uint32_t src = (coef(e) + bt) & (2 * N - 1);
+      const uint64_t v = live ? lut[src & (N - 1)] : 0ull;
+      A[e] = src < (uint32_t)N ? v : 0ull - v;
+    }
+  }
+  __syncthreads();
+  const int logB = (int)a.base_log, sb = (int)a.bits;
+  const int nrep = 64 - LV * logB;
+  const uint64_t half = 1ull << (sb - 1), bmask = (1ull << sb) - 1ull;
+  // key values of product item (c, f) = (it / M, it % M), it = threadIdx.x + s NT, for slot m
+  cplx gn[IPT][KL];
+  auto load_key = [&](uint32_t step, int m) {
+#pragma unroll
+    for (int s = 0; s < IPT; ++s) {
+      const int it = threadIdx.x + s * NT;
+      if (ITEMS % NT == 0 || it < ITEMS) {
+        const cplx* Gp = a.G + (((uint64_t)step * K1 + it / M) * L + m) * (uint64_t)(KL * M) + it % M;
+#pragma unroll
+        for (int rq = 0; rq < KL; ++rq) gn[s][rq] = Gp[rq * M];
+      }
+    }
+  };
+  if (a.n > 0) load_key(0, 0);
+#pragma unroll 1
+  for (uint32_t i = 0; i < a.n; ++i) {
+    // ct1 = X^{ms(a_i)} acc - acc (rotation through this group's slot buffer), decomposition,
+    // b-bit sub-digits, forward transforms into the tile's digit spectra
+    const uint32_t at = live ? modswitch(lwe[i], LOG2_2N) : 0u;
+    uint64_t* rot = reinterpret_cast<uint64_t*>(ybuf);
+#pragma unroll
+    for (int e = 0; e < 2 * VPT; ++e) rot[coef(e)] = A[e];
+    poly_sync<M>();
+    uint64_t S[2 * VPT];
+#pragma unroll
+    for (int e = 0; e < 2 * VPT; ++e) {
+      const uint32_t src = (coef(e) - at) & (2 * N - 1);
+      const uint64_t rv = rot[src & (N - 1)];
+      const uint64_t x = (src < (uint32_t)N ? rv : 0ull - rv) - A[e];
+      S[e] = nrep > 0 ? decomp_init(x, nrep) : x;
+    }
+#pragma unroll 1
+    for (int q = 0; q < LV; ++q) {
+      int64_t D[2 * VPT];
+#pragma unroll
+      for (int e = 0; e < 2 * VPT; ++e) D[e] = decomp_next64(S[e], logB);
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        cplx* xs = Xs + ((lct * KL + c * LV + q) * T + t) * M;
+#pragma unroll
+        for (int e = 0; e < VPT; ++e) {
+          int64_t s0 = D[e], s1 = D[e + VPT];
+          if constexpr (T > 1) {
+            s0 = (int64_t)(((uint64_t)D[e] + half) & bmask) - (int64_t)half;
+            s1 = (int64_t)(((uint64_t)D[e + VPT] + half) & bmask) - (int64_t)half;
+            D[e] = (D[e] - s0) >> sb;
+            D[e + VPT] = (D[e + VPT] - s1) >> sb;
+          }
+          const int j = tid + e * TH;
+          xs[sw(j)] = cmul(cplx{(double)s0, (double)s1}, zeta(j));
+        }
+        poly_sync<M>();
+        fft_block<M, false>(xs, W, tid);
+      }
+    }
+    __syncthreads();
+    // slots m = 0 .. L-1: Y_m = sum_rq X[rq][0] G[m][rq] + X[rq][1] G[m-1][rq]; inverse; acc += 2^{mb} round
+    // limb j's key values serve slot j (sub-digit 0) and slot j + 1 (sub-digit 1); the
+    // sub-digit-1 partial of slot j + 1 waits in registers (same thread, same item)
+    cplx carry[IPT][C];
+#pragma unroll 1
+    for (int m = 0; m < L; ++m) {
+      // this limb's key values were loaded one limb ahead; issue the next limb's now
+      cplx gk[IPT][KL];
+#pragma unroll
+      for (int s = 0; s < IPT; ++s)
+#pragma unroll
+        for (int rq = 0; rq < KL; ++rq) gk[s][rq] = gn[s][rq];
+      if (m + 1 < L)
+        load_key(i, m + 1);
+      else if (i + 1 < a.n)
+        load_key(i + 1, 0);
+#pragma unroll
+      for (int s = 0; s < IPT; ++s) {
+        const int it = threadIdx.x + s * NT;
+        if (ITEMS % NT == 0 || it < ITEMS) {
+          const int cc = it / M, f = it % M;
+          const int sf = sw(f);
+#pragma unroll
+          for (int lc = 0; lc < C; ++lc) {
+            cplx y = (T > 1 && m > 0) ? carry[s][lc] : cplx{0.0, 0.0};
+#pragma unroll
+            for (int rq = 0; rq < KL; ++rq) {
+              const cplx xv = Xs[((lc * KL + rq) * T) * M + sf], gv = gk[s][rq];
+              y.re = __builtin_fma(xv.re, gv.re, __builtin_fma(-xv.im, gv.im, y.re));
+              y.im = __builtin_fma(xv.re, gv.im, __builtin_fma(xv.im, gv.re, y.im));
+            }
+            Ys[(lc * K1 + cc) * M + sf] = y;
+            if constexpr (T > 1) {
+              cplx z = {0.0, 0.0};
+#pragma unroll
+              for (int rq = 0; rq < KL; ++rq) {
+                const cplx xv = Xs[((lc * KL + rq) * T + 1) * M + sf], gv = gk[s][rq];
+                z.re = __builtin_fma(xv.re, gv.re, __builtin_fma(-xv.im, gv.im, z.re));
+                z.im = __builtin_fma(xv.re, gv.im, __builtin_fma(xv.im, gv.re, z.im));
+              }
+              carry[s][lc] = z;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      fft_block<M, true>(ybuf, W, tid);
+      const uint32_t sh = m * a.bits;
+#pragma unroll
+      for (int e = 0; e < VPT; ++e) {
+        const int j = tid + e * TH;
+        const cplx z = cmulc(ybuf[sw(j)], zeta(j));
+        const double tr = z.re + RND_MAGIC, ti = z.im + RND_MAGIC;
+        max_resid = fmax(max_resid, fmax(fabs(z.re - (tr - RND_MAGIC)), fabs(z.im - (ti - RND_MAGIC))));
+        if (sh < 64) {
+          A[e] += ((uint64_t)__double_as_longlong(tr) - RND_MAGIC_BITS) << sh;
+          A[e + VPT] += ((uint64_t)__double_as_longlong(ti) - RND_MAGIC_BITS) << sh;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // sample extract (nth = 0): out[r N + 0] = A_r[0], out[r N + j] = -A_r[N - j], out[k N] = B[0]
+  if (live) {
+    const uint64_t orow = a.out_idx ? a.out_idx[ct] : ct;
+    uint64_t* o = a.out + orow * ((uint64_t)(K1 - 1) * N + 1);
+#pragma unroll
+    for (int e = 0; e < 2 * VPT; ++e) {
+      const uint32_t j = coef(e);
+      if (c < K1 - 1)
+        o[(uint64_t)c * N + ((N - j) & (N - 1))] = j == 0 ? A[e] : 0ull - A[e];
+      else if (j == 0)
+        o[(uint64_t)(K1 - 1) * N] = A[e];
+    }
+  }
+  if (a.resid) {
+    for (int off = 32; off > 0; off >>= 1) max_resid = fmax(max_resid, __shfl_xor(max_resid, off));
+    if ((threadIdx.x & 63) == 0) atomicMax(a.resid, (unsigned long long)__double_as_longlong(max_resid));
+  }
+}
+
 // sample extract (nth = 0): out[r N + 0] = A_r[0], out[r N + j] = -A_r[N - j], out[k N] = B[0]
 __global__ void gen_extract_kernel(uint64_t* out, const uint64_t* out_idx, const uint64_t* acc, uint32_t base,
                                    uint32_t count, uint32_t k, uint32_t N) {
@@ -876,6 +1084,35 @@ static int step_dispatch(uint32_t N, const StepArgs& s, uint32_t K1, hipStream_t
   return 0;
 }
 
+// one-launch tile path for the instantiated shapes
+template <int M, int K1, int KL, int T, int L, int C>
+static void launch_tile(const TileArgs& t, hipStream_t st) {
+  using TG = TileGeo<M, K1, KL, T, L, C>;
+  auto kern = gen_tile_kernel<M, K1, KL, T, L, C>;
+  CHIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TG::LDS));
+  hipLaunchKernelGGL(kern, dim3((t.count + C - 1) / C), dim3(TG::NT), TG::LDS, st, t);
+}
+
+// Tile sizes (ciphertexts per workgroup) measured on MI355X: N = 256, k = 5: C = 4 (54.5k PBS/s;
+// C = 2 spills: 33.3k); N = 512, k = 3: C = 1 (34.9k; C = 2: 33.4k).  CONCRETE_HIP_TILE_C=2
+// selects the alternative for A/B runs.  N = 1024 stays on the two-launch path: a tile of one
+// k = 2 ciphertext needs 398 VGPRs (two spill) and was no faster.  false: no tile instance.
+static bool tile_dispatch(uint32_t N, uint32_t K1, uint32_t KL, uint32_t T, uint32_t L, const TileArgs& t,
+                          hipStream_t st) {
+  static const int tile_c = getenv("CONCRETE_HIP_TILE_C") ? atoi(getenv("CONCRETE_HIP_TILE_C")) : 0;
+  if (N == 256 && K1 == 6 && KL == 6 && T == 2 && L == 5) {
+    if (tile_c == 2) launch_tile<128, 6, 6, 2, 5, 2>(t, st);
+    else launch_tile<128, 6, 6, 2, 5, 4>(t, st);
+    return true;
+  }
+  if (N == 512 && K1 == 4 && KL == 4 && T == 2 && L == 5) {
+    if (tile_c == 2) launch_tile<256, 4, 4, 2, 5, 2>(t, st);
+    else launch_tile<256, 4, 4, 2, 5, 1>(t, st);
+    return true;
+  }
+  return false;
+}
+
 }  // namespace gen
 
 uint64_t generic_scratch_bytes_per_sample(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
@@ -897,6 +1134,18 @@ int pbs_generic_launch(const PbsArgs& a) {
   const uint32_t K1 = a.k + 1, M = a.N / 2, L = fmt.limbs, b = fmt.bits;
   const uint32_t T = (a.base_log + b - 1) / b;
   const Tables tb = tables_for(a.N);
+  {
+    const TileArgs t{a.out,   a.out_idx, a.in,    a.in_idx, a.luts,         a.lut_idx, reinterpret_cast<const cplx*>(a.fbsk),
+                     tb.Wfull, tb.Z,     a.resid, a.num_samples, a.n, a.base_log, b};
+    if (tile_dispatch(a.N, K1, K1 * a.level, T, L, t, a.stream)) {
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) {
+        set_error("generic pbs (tile) launch failed: %s", hipGetErrorString(e));
+        return -1;
+      }
+      return 0;
+    }
+  }
   const uint64_t per_ct = generic_scratch_bytes_per_sample(a.k, a.N, a.level, a.base_log);
   const uint64_t budget = 2ull << 30;
   const uint32_t chunk = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(a.num_samples, 65536),

@@ -104,9 +104,12 @@ def test_generic_8bit_long_chain_decrypts(B, oracle, torch_cuda):
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
 
 
-def test_generic_index_arrays(B, oracle, torch_cuda):
-    """Mapped LUTs and permuted input/output rows (GPUDFG.cpp:1149-1205) on the general path."""
-    label, k, N, n, l, logB, width = CASES[2]
+@pytest.mark.parametrize("ci", [0, 2, 3], ids=[CASES[i][0] for i in (0, 2, 3)])
+def test_generic_index_arrays(B, oracle, torch_cuda, ci):
+    """Mapped LUTs and permuted input/output rows (GPUDFG.cpp:1149-1205) on the general path:
+    the one-launch tile kernels (N = 256: 4 ciphertexts per workgroup, the last one partly
+    empty; N = 512) and the N = 1024 two-launch path."""
+    label, k, N, n, l, logB, width = CASES[ci]
     p, lwe_sk, glwe_sk, bsk, fbsk = setup(B, torch_cuda, k, N, n, l, logB, 7200)
     rng = np.random.RandomState(3)
     tables = [rng.randint(0, 1 << width, size=1 << width).astype(np.uint64) for _ in range(3)]

@@ -707,11 +707,89 @@ struct TileArgs {
   uint32_t count, n, base_log, bits;
 };
 
+// Tile transforms (M <= 256, radix-4 Stockham as fft_block) with each pass's twiddles laid out
+// per pass, TWP[off(Ns) + kk (R-1) + r - 1] = W[kk r M / (Ns R)] (copies of the correctly rounded
+// table, so the bound is unchanged): the lanes of a ds_read_b128 group read consecutive kk at a
+// 48-byte stride instead of the full table's 2-8-way conflicted strides, and the first pass
+// (all twiddles 1) multiplies by nothing.
+template <int M>
+constexpr int tile_tw_entries() {
+  int n = 0;
+  for (int Ns = (Geo<M>::LOG & 1) ? 2 : 4; Ns < M; Ns *= 4) n += 3 * Ns;
+  return n;
+}
+
+template <int M>
+__device__ __forceinline__ void build_tile_tw(cplx* TWP, const cplx* W, int t, int nt) {
+  int off = 0;
+  for (int Ns = (Geo<M>::LOG & 1) ? 2 : 4; Ns < M; Ns *= 4) {
+    const int step = M / (Ns * 4);
+    for (int e = t; e < 3 * Ns; e += nt) TWP[off + e] = W[(e / 3) * (e % 3 + 1) * step];
+    off += 3 * Ns;
+  }
+}
+
+template <int M, int R, bool INV, bool FIRST>
+__device__ __forceinline__ void tile_pass(cplx* buf, const cplx* TW, int tid, int Ns) {
+  constexpr int TH = Geo<M>::THREADS;
+  constexpr int NB = M / R / TH;
+  static_assert(NB >= 1 && (M / R) % TH == 0, "pass split");
+  cplx v[NB][R];
+#pragma unroll
+  for (int s = 0; s < NB; ++s) {
+    const int j = tid + s * TH;
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[s][r] = buf[sw(j + r * (M / R))];
+  }
+  poly_sync<M>();
+#pragma unroll
+  for (int s = 0; s < NB; ++s) {
+    const int j = tid + s * TH;
+    const int kk = FIRST ? 0 : (j & (Ns - 1));
+    if constexpr (!FIRST) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        const cplx w = TW[kk * (R - 1) + r - 1];
+        v[s][r] = INV ? cmulc(v[s][r], w) : cmul(v[s][r], w);
+      }
+    }
+    if constexpr (R == 2) {
+      const cplx x0 = v[s][0], x1 = v[s][1];
+      v[s][0] = cadd(x0, x1);
+      v[s][1] = csub(x0, x1);
+    } else {
+      const cplx t0 = cadd(v[s][0], v[s][2]), t1 = csub(v[s][0], v[s][2]);
+      const cplx t2 = cadd(v[s][1], v[s][3]), t3 = mul_mi<INV>(csub(v[s][1], v[s][3]));
+      v[s][0] = cadd(t0, t2);
+      v[s][2] = csub(t0, t2);
+      v[s][1] = cadd(t1, t3);
+      v[s][3] = csub(t1, t3);
+    }
+    const int d = (j - kk) * R + kk;
+#pragma unroll
+    for (int r = 0; r < R; ++r) buf[sw(d + r * Ns)] = v[s][r];
+  }
+  poly_sync<M>();
+}
+
+template <int M, bool INV>
+__device__ __forceinline__ void tile_fft(cplx* buf, const cplx* TWP, int tid) {
+  static_assert(Geo<M>::VPT == 4, "radix-4 schedule");
+  constexpr int R0 = (Geo<M>::LOG & 1) ? 2 : 4;
+  tile_pass<M, R0, INV, true>(buf, nullptr, tid, 1);
+  int off = 0;
+#pragma unroll 1
+  for (int Ns = R0; Ns < M; Ns *= 4) {
+    tile_pass<M, 4, INV, false>(buf, TWP + off, tid, Ns);
+    off += 3 * Ns;
+  }
+}
+
 template <int M, int K1, int KL, int T, int L, int C>
 struct TileGeo {
   static constexpr int TH = Geo<M>::THREADS;  // threads per polynomial
   static constexpr int NT = C * K1 * TH;      // threads per workgroup
-  static constexpr int BASE = ((C * KL * T + C * K1) * M + tw_entries<M>()) * 16;
+  static constexpr int BASE = ((C * KL * T + C * K1) * M + tile_tw_entries<M>()) * 16;
   static constexpr bool ZLDS = BASE + M * 16 <= 160 * 1024;  // twist table in LDS when it fits
   static constexpr int LDS = BASE + (ZLDS ? M * 16 : 0);
   static_assert(M <= 256 && NT <= 1024 && LDS <= 160 * 1024, "tile shape");
@@ -726,9 +804,9 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cplx* Xs = reinterpret_cast<cplx*>(smem);  // [C][KL rq][T t][M] digit spectra (slots sw(f))
   cplx* Ys = Xs + C * KL * T * M;            // [C][K1 c][M] slot spectra / rotation scratch
-  cplx* W = Ys + C * K1 * M;
-  cplx* Zl = W + tw_entries<M>();
-  load_twiddles<M>(W, a.Wfull, nullptr, nullptr, threadIdx.x, NT);
+  cplx* W = Ys + C * K1 * M;  // per-pass twiddles (tile_fft)
+  cplx* Zl = W + tile_tw_entries<M>();
+  build_tile_tw<M>(W, a.Wfull, threadIdx.x, NT);
   if constexpr (TG::ZLDS)
     for (int e = threadIdx.x; e < M; e += NT) Zl[e] = a.Z[e];
   auto zeta = [&](int j) { return TG::ZLDS ? Zl[j] : a.Z[j]; };
@@ -809,7 +887,7 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
           xs[sw(j)] = cmul(cplx{(double)s0, (double)s1}, zeta(j));
         }
         poly_sync<M>();
-        fft_block<M, false>(xs, W, tid);
+        tile_fft<M, false>(xs, W, tid);
       }
     }
     __syncthreads();
@@ -859,7 +937,7 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
         }
       }
       __syncthreads();
-      fft_block<M, true>(ybuf, W, tid);
+      tile_fft<M, true>(ybuf, W, tid);
       const uint32_t sh = m * a.bits;
 #pragma unroll
       for (int e = 0; e < VPT; ++e) {

@@ -334,7 +334,16 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
         __builtin_amdgcn_global_load_lds(Ym + sw(L0 + ln), (lds_ptr_t)(dst + L0), 16, 0, 0);
       }
     };
-    if constexpr (YDMA) issue_y(0, buf);
+    // PREF (up to M = 4096; M = 8192 has no registers to spare): slot m + 1 is loaded into
+    // registers while slot m is transformed
+    constexpr bool PREF = !YDMA && M <= 4096;
+    cplx nx[PREF ? VPT : 1];
+    if constexpr (YDMA) {
+      issue_y(0, buf);
+    } else if constexpr (PREF) {
+#pragma unroll
+      for (int e = 0; e < VPT; ++e) nx[e] = live ? Yc[tid + e * TH] : cplx{0.0, 0.0};
+    }
 #pragma unroll 1
     for (uint32_t m = 0; m < a.limbs; ++m) {
       cplx* cur = buf;
@@ -343,6 +352,15 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
         wait_vmcnt<0>();
         poly_sync<M>();
         if (m + 1 < a.limbs) issue_y(m + 1, buf + ((m + 1) & 1) * M);
+      } else if constexpr (PREF) {
+#pragma unroll
+        for (int e = 0; e < VPT; ++e) cur[sw(tid + e * TH)] = nx[e];
+        if (m + 1 < a.limbs) {
+          const cplx* Yn = Yc + (uint64_t)(m + 1) * M;
+#pragma unroll
+          for (int e = 0; e < VPT; ++e) nx[e] = live ? Yn[tid + e * TH] : cplx{0.0, 0.0};
+        }
+        poly_sync<M>();
       } else {
         const cplx* Ym = Yc + (uint64_t)m * M;
 #pragma unroll

@@ -474,134 +474,6 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
   }
 }
 
-// N = 1024 (M = 512): one wave per polynomial with the register-resident transforms of
-// fft512.hpp (three radix-8 passes, one LDS transpose per direction, the twist folded into the
-// tables). Spectra are stored in the transforms' own order p = k2 * 64 + lane (frequency
-// fft512_freq(lane, k2)); X, Y and the Fourier key (gen_convert512_kernel) agree on it, and the
-// product kernels are order-agnostic. No workgroup barrier after the table build, so a wave
-// past the batch leaves at once.
-constexpr int S512_PPB = 4;  // polynomials (waves) per workgroup
-template <int MODE>
-__global__ void __launch_bounds__(64 * S512_PPB) gen_step512_kernel(StepArgs a) {
-  constexpr int M = 512, N = 1024, LOG2_2N = 11;
-  __shared__ cplx lds[FFT512_TABLE_ENTRIES + S512_PPB * PBS1024_XCH_SLOTS];
-  cplx* T1 = lds;
-  cplx* T2 = lds + 8 * T1_STRIDE;
-  build_fft512_tables(T1, T2, threadIdx.x, 64 * S512_PPB);
-  __syncthreads();
-  const Fft512Tables T{T1, T2};
-  const int g = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  cplx* xch = lds + FFT512_TABLE_ENTRIES + g * PBS1024_XCH_SLOTS;
-  const uint32_t K1 = a.k + 1;
-  const uint64_t poly = (uint64_t)blockIdx.x * S512_PPB + g;
-  if (poly >= (uint64_t)a.count * K1) return;
-  const uint32_t ct = (uint32_t)(poly / K1), c = (uint32_t)(poly % K1);
-  const uint32_t s = a.base + ct;
-  const uint64_t row = a.in_idx ? a.in_idx[s] : s;
-  const uint64_t* lwe = a.in + row * (uint64_t)(a.n + 1);
-  uint64_t* acc = a.acc + ((uint64_t)ct * K1 + c) * N;
-  // this lane's coefficients: j = lane + 64 e (e < 16); j and j + 512 pair up as (e, e + 8)
-  uint64_t A[16];
-  double max_resid = 0.0;
-
-  if constexpr ((MODE & MODE_INIT) != 0) {
-    const uint64_t* lut = a.luts + (a.lut_idx ? a.lut_idx[s] : 0ull) * (uint64_t)(K1 * N) + (uint64_t)c * N;
-    const uint32_t bt = modswitch(lwe[a.n], LOG2_2N);
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const uint32_t src = (lane + 64 * e + bt) & (2 * N - 1);
-      const uint64_t v = lut[src & (N - 1)];
-      A[e] = src < (uint32_t)N ? v : 0ull - v;
-    }
-  } else {
-#pragma unroll
-    for (int e = 0; e < 16; ++e) A[e] = acc[lane + 64 * e];
-  }
-
-  if constexpr ((MODE & MODE_BACK) != 0) {
-    const cplx* Yc = a.Y + ((uint64_t)ct * K1 + c) * a.limbs * (uint64_t)M + lane;
-    cplx v[8], nx[8];
-#pragma unroll
-    for (int k2 = 0; k2 < 8; ++k2) nx[k2] = Yc[64 * k2];
-#pragma unroll 1
-    for (uint32_t m = 0; m < a.limbs; ++m) {
-#pragma unroll
-      for (int k2 = 0; k2 < 8; ++k2) v[k2] = nx[k2];
-      if (m + 1 < a.limbs) {
-        const cplx* Yn = Yc + (uint64_t)(m + 1) * M;
-#pragma unroll
-        for (int k2 = 0; k2 < 8; ++k2) nx[k2] = Yn[64 * k2];
-      }
-      fft512_inv(v, xch, T, lane);
-      const uint32_t sh = m * a.bits;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const double tr = v[e].re + RND_MAGIC, ti = v[e].im + RND_MAGIC;
-        max_resid = fmax(max_resid, fmax(fabs(v[e].re - (tr - RND_MAGIC)), fabs(v[e].im - (ti - RND_MAGIC))));
-        if (sh < 64) {
-          A[e] += ((uint64_t)__double_as_longlong(tr) - RND_MAGIC_BITS) << sh;
-          A[e + 8] += ((uint64_t)__double_as_longlong(ti) - RND_MAGIC_BITS) << sh;
-        }
-      }
-    }
-    if (a.resid) {
-      for (int off = 32; off > 0; off >>= 1) max_resid = fmax(max_resid, __shfl_xor(max_resid, off));
-      if (lane == 0) atomicMax(a.resid, (unsigned long long)__double_as_longlong(max_resid));
-    }
-  }
-
-  if constexpr ((MODE & (MODE_BACK | MODE_INIT)) != 0) {
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[lane + 64 * e] = A[e];
-  }
-
-  if constexpr ((MODE & MODE_FRONT) != 0) {
-    // rotation through the wave's exchange scratch (1024 u64 = 8 KB of its 9.2 KB)
-    const uint32_t at = modswitch(lwe[a.step], LOG2_2N);
-    uint64_t* rot = reinterpret_cast<uint64_t*>(xch);
-#pragma unroll
-    for (int e = 0; e < 16; ++e) rot[lane + 64 * e] = A[e];
-    wave_lds_fence();
-    const int nrep = 64 - (int)(a.level * a.base_log);
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const uint32_t src = (lane + 64 * e - at) & (2 * N - 1);
-      const uint64_t rv = rot[src & (N - 1)];
-      const uint64_t x = (src < (uint32_t)N ? rv : 0ull - rv) - A[e];
-      A[e] = nrep > 0 ? decomp_init(x, nrep) : x;
-    }
-    wave_lds_fence();
-    cplx* Xc = a.X + ((uint64_t)ct * K1 + c) * a.level * a.subs * (uint64_t)M + lane;
-    const int logB = (int)a.base_log, sb = (int)a.bits;
-    const uint64_t half = 1ull << (sb - 1), bmask = (1ull << sb) - 1ull;
-#pragma unroll 1
-    for (uint32_t q = 0; q < a.level; ++q) {
-      int64_t D[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) D[e] = decomp_next64(A[e], logB);
-#pragma unroll 1
-      for (uint32_t t = 0; t < a.subs; ++t) {
-        cplx v[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          int64_t s0 = D[e], s1 = D[e + 8];
-          if (a.subs > 1) {  // balanced b-bit sub-digit, exact: D - s is a multiple of 2^b
-            s0 = (int64_t)(((uint64_t)D[e] + half) & bmask) - (int64_t)half;
-            s1 = (int64_t)(((uint64_t)D[e + 8] + half) & bmask) - (int64_t)half;
-            D[e] = (D[e] - s0) >> sb;
-            D[e + 8] = (D[e + 8] - s1) >> sb;
-          }
-          v[e] = {(double)s0, (double)s1};
-        }
-        fft512_fwd(v, xch, T, lane);
-        cplx* dst = Xc + ((uint64_t)q * a.subs + t) * M;
-#pragma unroll
-        for (int k2 = 0; k2 < 8; ++k2) dst[64 * k2] = v[k2];
-      }
-    }
-  }
-}
-
 // Y[ct][c][m][f] = sum over (r, q, t) with 0 <= m - t < L of X[ct][r][q][t][f] * G_i[c][m-t][r][q][f]
 struct MacArgs {
   const cplx* X;
@@ -730,26 +602,49 @@ struct TileArgs {
 // table, so the bound is unchanged): the lanes of a ds_read_b128 group read consecutive kk at a
 // 48-byte stride instead of the full table's 2-8-way conflicted strides, and the first pass
 // (all twiddles 1) multiplies by nothing.
+// threads per polynomial in the tile kernels: the step kernel's for M <= 256, 128 (two waves,
+// four values each) at M = 512
+#ifndef TILE512_TH
+#define TILE512_TH 128
+#endif
+template <int M>
+constexpr int tile_threads() { return M == 512 ? TILE512_TH : Geo<M>::THREADS; }
+template <int TH>
+__device__ __forceinline__ void tile_sync() {
+  if constexpr (TH <= 64) wave_lds_fence();
+  else __syncthreads();  // every polynomial of the tile transforms in lockstep
+}
+
+// radix of the tile transforms' passes (values per thread) and of the first pass (the leftover
+// factor, or a full pass: its twiddles are all 1)
+template <int M>
+constexpr int tile_radix() { return M / tile_threads<M>(); }
+template <int M>
+constexpr int tile_first_radix() {
+  constexpr int LR = tile_radix<M>() == 8 ? 3 : 2, REM = Geo<M>::LOG % LR;
+  return REM ? (1 << REM) : tile_radix<M>();
+}
 template <int M>
 constexpr int tile_tw_entries() {
   int n = 0;
-  for (int Ns = (Geo<M>::LOG & 1) ? 2 : 4; Ns < M; Ns *= 4) n += 3 * Ns;
+  for (int Ns = tile_first_radix<M>(); Ns < M; Ns *= tile_radix<M>()) n += (tile_radix<M>() - 1) * Ns;
   return n;
 }
 
 template <int M>
 __device__ __forceinline__ void build_tile_tw(cplx* TWP, const cplx* W, int t, int nt) {
+  constexpr int R = tile_radix<M>();
   int off = 0;
-  for (int Ns = (Geo<M>::LOG & 1) ? 2 : 4; Ns < M; Ns *= 4) {
-    const int step = M / (Ns * 4);
-    for (int e = t; e < 3 * Ns; e += nt) TWP[off + e] = W[(e / 3) * (e % 3 + 1) * step];
-    off += 3 * Ns;
+  for (int Ns = tile_first_radix<M>(); Ns < M; Ns *= R) {
+    const int step = M / (Ns * R);
+    for (int e = t; e < (R - 1) * Ns; e += nt) TWP[off + e] = W[(e / (R - 1)) * (e % (R - 1) + 1) * step];
+    off += (R - 1) * Ns;
   }
 }
 
 template <int M, int R, bool INV, bool FIRST>
 __device__ __forceinline__ void tile_pass(cplx* buf, const cplx* TW, int tid, int Ns) {
-  constexpr int TH = Geo<M>::THREADS;
+  constexpr int TH = tile_threads<M>();
   constexpr int NB = M / R / TH;
   static_assert(NB >= 1 && (M / R) % TH == 0, "pass split");
   cplx v[NB][R];
@@ -759,7 +654,7 @@ __device__ __forceinline__ void tile_pass(cplx* buf, const cplx* TW, int tid, in
 #pragma unroll
     for (int r = 0; r < R; ++r) v[s][r] = buf[sw(j + r * (M / R))];
   }
-  poly_sync<M>();
+  tile_sync<TH>();
 #pragma unroll
   for (int s = 0; s < NB; ++s) {
     const int j = tid + s * TH;
@@ -775,48 +670,50 @@ __device__ __forceinline__ void tile_pass(cplx* buf, const cplx* TW, int tid, in
       const cplx x0 = v[s][0], x1 = v[s][1];
       v[s][0] = cadd(x0, x1);
       v[s][1] = csub(x0, x1);
-    } else {
+    } else if constexpr (R == 4) {
       const cplx t0 = cadd(v[s][0], v[s][2]), t1 = csub(v[s][0], v[s][2]);
       const cplx t2 = cadd(v[s][1], v[s][3]), t3 = mul_mi<INV>(csub(v[s][1], v[s][3]));
       v[s][0] = cadd(t0, t2);
       v[s][2] = csub(t0, t2);
       v[s][1] = cadd(t1, t3);
       v[s][3] = csub(t1, t3);
+    } else {
+      dft8<INV>(v[s]);
     }
     const int d = (j - kk) * R + kk;
 #pragma unroll
     for (int r = 0; r < R; ++r) buf[sw(d + r * Ns)] = v[s][r];
   }
-  poly_sync<M>();
+  tile_sync<TH>();
 }
 
 template <int M, bool INV>
 __device__ __forceinline__ void tile_fft(cplx* buf, const cplx* TWP, int tid) {
-  static_assert(Geo<M>::VPT == 4, "radix-4 schedule");
-  constexpr int R0 = (Geo<M>::LOG & 1) ? 2 : 4;
+  constexpr int R = tile_radix<M>(), R0 = tile_first_radix<M>();
+  static_assert(R == 4 || R == 8, "tile radix");
   tile_pass<M, R0, INV, true>(buf, nullptr, tid, 1);
   int off = 0;
 #pragma unroll 1
-  for (int Ns = R0; Ns < M; Ns *= 4) {
-    tile_pass<M, 4, INV, false>(buf, TWP + off, tid, Ns);
-    off += 3 * Ns;
+  for (int Ns = R0; Ns < M; Ns *= R) {
+    tile_pass<M, R, INV, false>(buf, TWP + off, tid, Ns);
+    off += (R - 1) * Ns;
   }
 }
 
 template <int M, int K1, int KL, int T, int L, int C>
 struct TileGeo {
-  static constexpr int TH = Geo<M>::THREADS;  // threads per polynomial
+  static constexpr int TH = tile_threads<M>();  // threads per polynomial
   static constexpr int NT = C * K1 * TH;      // threads per workgroup
   static constexpr int BASE = ((C * KL * T + C * K1) * M + tile_tw_entries<M>()) * 16;
   static constexpr bool ZLDS = BASE + M * 16 <= 160 * 1024;  // twist table in LDS when it fits
   static constexpr int LDS = BASE + (ZLDS ? M * 16 : 0);
-  static_assert(M <= 256 && NT <= 1024 && LDS <= 160 * 1024, "tile shape");
+  static_assert(M <= 512 && NT <= 1024 && LDS <= 160 * 1024, "tile shape");
 };
 
 template <int M, int K1, int KL, int T, int L, int C>
 __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_kernel(TileArgs a) {
   using TG = TileGeo<M, K1, KL, T, L, C>;
-  constexpr int N = 2 * M, TH = TG::TH, VPT = Geo<M>::VPT, NT = TG::NT, LOG2_2N = Geo<M>::LOG + 2;
+  constexpr int N = 2 * M, TH = TG::TH, VPT = M / TH, NT = TG::NT, LOG2_2N = Geo<M>::LOG + 2;
   constexpr int LV = KL / K1;                           // decomposition levels
   constexpr int ITEMS = K1 * M, IPT = (ITEMS + NT - 1) / NT;  // product items (c, f) per thread
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -875,7 +772,7 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
     uint64_t* rot = reinterpret_cast<uint64_t*>(ybuf);
 #pragma unroll
     for (int e = 0; e < 2 * VPT; ++e) rot[coef(e)] = A[e];
-    poly_sync<M>();
+    tile_sync<TH>();
     uint64_t S[2 * VPT];
 #pragma unroll
     for (int e = 0; e < 2 * VPT; ++e) {
@@ -904,7 +801,7 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
           const int j = tid + e * TH;
           xs[sw(j)] = cmul(cplx{(double)s0, (double)s1}, zeta(j));
         }
-        poly_sync<M>();
+        tile_sync<TH>();
         tile_fft<M, false>(xs, W, tid);
       }
     }
@@ -1067,51 +964,6 @@ __global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, c
   }
 }
 
-// N = 1024: the same key in gen_step512_kernel's spectral order (one wave per standard polynomial)
-__global__ void __launch_bounds__(64) gen_convert512_kernel(cplx* G, const uint64_t* src, uint32_t k,
-                                                           uint32_t level, uint32_t bits, uint32_t limbs) {
-  constexpr int M = 512, N = 1024;
-  __shared__ cplx lds[FFT512_TABLE_ENTRIES + PBS1024_XCH_SLOTS];
-  build_fft512_tables(lds, lds + 8 * T1_STRIDE, threadIdx.x, 64);
-  __syncthreads();
-  const Fft512Tables T{lds, lds + 8 * T1_STRIDE};
-  cplx* xch = lds + FFT512_TABLE_ENTRIES;
-  const int lane = threadIdx.x;
-  const uint32_t K1 = k + 1;
-  uint64_t p = blockIdx.x;
-  const uint32_t c = p % K1;
-  p /= K1;
-  const uint32_t r = p % K1;
-  p /= K1;
-  const uint32_t v = p % level;
-  const uint64_t i = p / level;
-  const uint32_t q = level - 1 - v;
-  const uint64_t* g = src + (uint64_t)blockIdx.x * N;
-  uint64_t gv[16];
-#pragma unroll
-  for (int e = 0; e < 16; ++e) gv[e] = g[lane + 64 * e];
-  const double scale = 1.0 / (double)M;
-#pragma unroll 1
-  for (uint32_t lim = 0; lim < limbs; ++lim) {
-    const uint32_t w = lim + 1 < limbs ? bits : 64 - (limbs - 1) * bits;
-    const uint64_t half = 1ull << (w - 1);
-    const uint64_t bmask = (1ull << w) - 1ull;
-    cplx x[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int64_t s0 = (int64_t)((gv[e] + half) & bmask) - (int64_t)half;
-      const int64_t s1 = (int64_t)((gv[e + 8] + half) & bmask) - (int64_t)half;
-      gv[e] = (gv[e] - (uint64_t)s0) >> bits;
-      gv[e + 8] = (gv[e + 8] - (uint64_t)s1) >> bits;
-      x[e] = {(double)s0, (double)s1};
-    }
-    fft512_fwd(x, xch, T, lane);
-    cplx* dst = G + ((((i * K1 + c) * limbs + lim) * K1 + r) * level + q) * (uint64_t)M + lane;
-#pragma unroll
-    for (int k2 = 0; k2 < 8; ++k2) dst[64 * k2] = {x[k2].re * scale, x[k2].im * scale};
-  }
-}
-
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
@@ -1165,12 +1017,7 @@ static int step_dispatch(uint32_t N, const StepArgs& s, uint32_t K1, hipStream_t
   switch (N) {
     case 256: launch_step<128, MODE>(s, K1, st); break;
     case 512: launch_step<256, MODE>(s, K1, st); break;
-    case 1024: {
-      const uint64_t polys = (uint64_t)s.count * K1;
-      hipLaunchKernelGGL((gen_step512_kernel<MODE>), dim3((uint32_t)((polys + S512_PPB - 1) / S512_PPB)),
-                         dim3(64 * S512_PPB), 0, st, s);
-      break;
-    }
+    case 1024: launch_step<512, MODE>(s, K1, st); break;
     case 2048: launch_step<1024, MODE>(s, K1, st); break;
     case 4096: launch_step<2048, MODE>(s, K1, st); break;
     case 8192: launch_step<4096, MODE>(s, K1, st); break;
@@ -1204,6 +1051,11 @@ static bool tile_dispatch(uint32_t N, uint32_t K1, uint32_t KL, uint32_t T, uint
   if (N == 512 && K1 == 4 && KL == 4 && T == 2 && L == 5) {
     if (tile_c == 2) launch_tile<256, 4, 4, 2, 5, 2>(t, st);
     else launch_tile<256, 4, 4, 2, 5, 1>(t, st);
+    return true;
+  }
+  if (N == 1024 && K1 == 3 && KL == 3 && T == 2 && L == 5) {
+    if (tile_c == 1) launch_tile<512, 3, 3, 2, 5, 1>(t, st);
+    else launch_tile<512, 3, 3, 2, 5, 2>(t, st);
     return true;
   }
   return false;
@@ -1297,10 +1149,7 @@ int convert_bsk_generic_launch(const ConvertArgs& a) {
   switch (a.N) {
     case 256: GEN_CONV(128); break;
     case 512: GEN_CONV(256); break;
-    case 1024:
-      hipLaunchKernelGGL(gen_convert512_kernel, dim3((uint32_t)blocks), dim3(64), 0, a.stream, G, a.src_dev, a.k,
-                         a.level, fmt.bits, fmt.limbs);
-      break;
+    case 1024: GEN_CONV(512); break;
     case 2048: GEN_CONV(1024); break;
     case 4096: GEN_CONV(2048); break;
     case 8192: GEN_CONV(4096); break;

@@ -40,6 +40,9 @@ CASES = [
     ("6bit_k1_N4096", 1, 4096, 6, 1, 22, 6),
     ("7bit_k1_N8192", 1, 8192, 4, 1, 22, 7),
     ("8bit_k1_N16384", 1, 16384, 3, 2, 15, 8),
+    # shapes off the tile kernels' instances (T = 1): the two-launch path at N = 512 and 1024
+    ("k3_N512_T1_two_launch", 3, 512, 12, 1, 12, 3),
+    ("k2_N1024_l2_two_launch", 2, 1024, 10, 2, 10, 3),
 ]
 
 

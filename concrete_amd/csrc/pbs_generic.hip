@@ -235,6 +235,108 @@ __device__ __forceinline__ void fft_block(cplx* buf, const cplx* W, int tid) {
   }
 }
 
+// Tile transforms (M <= 256, radix-4 Stockham as fft_block) with each pass's twiddles laid out
+// per pass, TWP[off(Ns) + kk (R-1) + r - 1] = W[kk r M / (Ns R)] (copies of the correctly rounded
+// table, so the bound is unchanged): the lanes of a ds_read_b128 group read consecutive kk at a
+// 48-byte stride instead of the full table's 2-8-way conflicted strides, and the first pass
+// (all twiddles 1) multiplies by nothing.
+// threads per polynomial in the tile kernels: the step kernel's for M <= 256, 128 (two waves,
+// four values each) at M = 512
+#ifndef TILE512_TH
+#define TILE512_TH 128
+#endif
+template <int M>
+constexpr int tile_threads() { return M == 512 ? TILE512_TH : Geo<M>::THREADS; }
+template <int TH>
+__device__ __forceinline__ void tile_sync() {
+  if constexpr (TH <= 64) wave_lds_fence();
+  else __syncthreads();  // every polynomial of the tile transforms in lockstep
+}
+
+// radix of the tile transforms' passes (values per thread) and of the first pass (the leftover
+// factor, or a full pass: its twiddles are all 1)
+template <int M, int TH>
+constexpr int tile_radix() { return M / TH; }
+template <int M, int TH>
+constexpr int tile_first_radix() {
+  constexpr int LR = tile_radix<M, TH>() == 8 ? 3 : 2, REM = Geo<M>::LOG % LR;
+  return REM ? (1 << REM) : tile_radix<M, TH>();
+}
+template <int M, int TH>
+constexpr int tile_tw_entries() {
+  int n = 0;
+  for (int Ns = tile_first_radix<M, TH>(); Ns < M; Ns *= tile_radix<M, TH>()) n += (tile_radix<M, TH>() - 1) * Ns;
+  return n;
+}
+
+template <int M, int TH>
+__device__ __forceinline__ void build_tile_tw(cplx* TWP, const cplx* W, int t, int nt) {
+  constexpr int R = tile_radix<M, TH>();
+  int off = 0;
+  for (int Ns = tile_first_radix<M, TH>(); Ns < M; Ns *= R) {
+    const int step = M / (Ns * R);
+    for (int e = t; e < (R - 1) * Ns; e += nt) TWP[off + e] = W[(e / (R - 1)) * (e % (R - 1) + 1) * step];
+    off += (R - 1) * Ns;
+  }
+}
+
+template <int M, int TH, int R, bool INV, bool FIRST>
+__device__ __forceinline__ void tile_pass(cplx* buf, const cplx* TW, int tid, int Ns) {
+  constexpr int NB = M / R / TH;
+  static_assert(NB >= 1 && (M / R) % TH == 0, "pass split");
+  cplx v[NB][R];
+#pragma unroll
+  for (int s = 0; s < NB; ++s) {
+    const int j = tid + s * TH;
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[s][r] = buf[sw(j + r * (M / R))];
+  }
+  tile_sync<TH>();
+#pragma unroll
+  for (int s = 0; s < NB; ++s) {
+    const int j = tid + s * TH;
+    const int kk = FIRST ? 0 : (j & (Ns - 1));
+    if constexpr (!FIRST) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        const cplx w = TW[kk * (R - 1) + r - 1];
+        v[s][r] = INV ? cmulc(v[s][r], w) : cmul(v[s][r], w);
+      }
+    }
+    if constexpr (R == 2) {
+      const cplx x0 = v[s][0], x1 = v[s][1];
+      v[s][0] = cadd(x0, x1);
+      v[s][1] = csub(x0, x1);
+    } else if constexpr (R == 4) {
+      const cplx t0 = cadd(v[s][0], v[s][2]), t1 = csub(v[s][0], v[s][2]);
+      const cplx t2 = cadd(v[s][1], v[s][3]), t3 = mul_mi<INV>(csub(v[s][1], v[s][3]));
+      v[s][0] = cadd(t0, t2);
+      v[s][2] = csub(t0, t2);
+      v[s][1] = cadd(t1, t3);
+      v[s][3] = csub(t1, t3);
+    } else {
+      dft8<INV>(v[s]);
+    }
+    const int d = (j - kk) * R + kk;
+#pragma unroll
+    for (int r = 0; r < R; ++r) buf[sw(d + r * Ns)] = v[s][r];
+  }
+  tile_sync<TH>();
+}
+
+template <int M, int TH, bool INV>
+__device__ __forceinline__ void tile_fft(cplx* buf, const cplx* TWP, int tid) {
+  constexpr int R = tile_radix<M, TH>(), R0 = tile_first_radix<M, TH>();
+  static_assert(R == 4 || R == 8, "tile radix");
+  tile_pass<M, TH, R0, INV, true>(buf, nullptr, tid, 1);
+  int off = 0;
+#pragma unroll 1
+  for (int Ns = R0; Ns < M; Ns *= R) {
+    tile_pass<M, TH, R, INV, false>(buf, TWP + off, tid, Ns);
+    off += (R - 1) * Ns;
+  }
+}
+
 // tfhe SignedDecomposer::decompose_one_level on a 64-bit state (digits up to 64 bits)
 __device__ __forceinline__ int64_t decomp_next64(uint64_t& state, int logB) {
   const uint64_t mask = logB >= 64 ? ~0ull : (1ull << logB) - 1ull;
@@ -278,10 +380,17 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
   constexpr bool ZLDS = M <= 1024;
   constexpr bool YDMA = TH >= 64 && M <= 512;
   constexpr int NBUF = YDMA ? 2 : 1;
-  __shared__ cplx lds[NBUF * PPB * M + tw_entries<M>() + (ZLDS ? M : 0)];
+  // PP: per-pass twiddle tables (tile_fft; they do not fit next to an M = 8192 polynomial,
+  // which keeps the two-level table of fft_block)
+  constexpr bool PP = M <= 4096;
+  constexpr int TWN = PP ? tile_tw_entries<M, TH>() : tw_entries<M>();
+  __shared__ cplx lds[NBUF * PPB * M + TWN + (ZLDS ? M : 0)];
   cplx* W = lds + NBUF * PPB * M;
-  load_twiddles<M>(W, a.Wfull, a.Wlo, a.Whi, threadIdx.x, Geo<M>::BLOCK);
-  cplx* Zl = W + tw_entries<M>();
+  if constexpr (PP)
+    build_tile_tw<M, TH>(W, a.Wfull, threadIdx.x, Geo<M>::BLOCK);
+  else
+    load_twiddles<M>(W, a.Wfull, a.Wlo, a.Whi, threadIdx.x, Geo<M>::BLOCK);
+  cplx* Zl = W + TWN;
   if constexpr (ZLDS)
     for (int e = threadIdx.x; e < M; e += Geo<M>::BLOCK) Zl[e] = a.Z[e];
   auto zeta = [&](int j) { return ZLDS ? Zl[j] : a.Z[j]; };
@@ -289,6 +398,10 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
   // polynomial group g of this workgroup: (ciphertext, GLWE polynomial) = divmod(poly, k + 1).
   // Groups past the batch keep taking part in the workgroup barriers of the transforms.
   const int g = threadIdx.x / TH, tid = threadIdx.x % TH;
+  auto fwd = [&](cplx* b) {
+    if constexpr (PP) tile_fft<M, TH, false>(b, W, tid);
+    else fft_block<M, false>(b, W, tid);
+  };
   cplx* buf = lds + g * NBUF * M;
   const uint32_t K1 = a.k + 1;
   const uint64_t poly = (uint64_t)blockIdx.x * PPB + g;
@@ -367,7 +480,10 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
         for (int e = 0; e < VPT; ++e) cur[sw(tid + e * TH)] = live ? Ym[tid + e * TH] : cplx{0.0, 0.0};
         poly_sync<M>();
       }
-      fft_block<M, true>(cur, W, tid);
+      if constexpr (PP)
+        tile_fft<M, TH, true>(cur, W, tid);
+      else
+        fft_block<M, true>(cur, W, tid);
       const uint32_t sh = m * a.bits;
 #pragma unroll
       for (int e = 0; e < VPT; ++e) {
@@ -442,7 +558,7 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
         }
         if constexpr (!STAGE) {
           poly_sync<M>();
-          fft_block<M, false>(buf, W, tid);
+          fwd(buf);
           if (live)
 #pragma unroll
             for (int e = 0; e < VPT; ++e) dst[tid + e * TH] = buf[sw(tid + e * TH)];
@@ -457,7 +573,7 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
 #pragma unroll
         for (int e = 0; e < VPT; ++e) buf[sw(tid + e * TH)] = live ? dst[tid + e * TH] : cplx{0.0, 0.0};
         poly_sync<M>();
-        fft_block<M, false>(buf, W, tid);
+        fwd(buf);
         if (live)
 #pragma unroll
           for (int e = 0; e < VPT; ++e) dst[tid + e * TH] = buf[sw(tid + e * TH)];
@@ -597,114 +713,11 @@ struct TileArgs {
   uint32_t count, n, base_log, bits;
 };
 
-// Tile transforms (M <= 256, radix-4 Stockham as fft_block) with each pass's twiddles laid out
-// per pass, TWP[off(Ns) + kk (R-1) + r - 1] = W[kk r M / (Ns R)] (copies of the correctly rounded
-// table, so the bound is unchanged): the lanes of a ds_read_b128 group read consecutive kk at a
-// 48-byte stride instead of the full table's 2-8-way conflicted strides, and the first pass
-// (all twiddles 1) multiplies by nothing.
-// threads per polynomial in the tile kernels: the step kernel's for M <= 256, 128 (two waves,
-// four values each) at M = 512
-#ifndef TILE512_TH
-#define TILE512_TH 128
-#endif
-template <int M>
-constexpr int tile_threads() { return M == 512 ? TILE512_TH : Geo<M>::THREADS; }
-template <int TH>
-__device__ __forceinline__ void tile_sync() {
-  if constexpr (TH <= 64) wave_lds_fence();
-  else __syncthreads();  // every polynomial of the tile transforms in lockstep
-}
-
-// radix of the tile transforms' passes (values per thread) and of the first pass (the leftover
-// factor, or a full pass: its twiddles are all 1)
-template <int M>
-constexpr int tile_radix() { return M / tile_threads<M>(); }
-template <int M>
-constexpr int tile_first_radix() {
-  constexpr int LR = tile_radix<M>() == 8 ? 3 : 2, REM = Geo<M>::LOG % LR;
-  return REM ? (1 << REM) : tile_radix<M>();
-}
-template <int M>
-constexpr int tile_tw_entries() {
-  int n = 0;
-  for (int Ns = tile_first_radix<M>(); Ns < M; Ns *= tile_radix<M>()) n += (tile_radix<M>() - 1) * Ns;
-  return n;
-}
-
-template <int M>
-__device__ __forceinline__ void build_tile_tw(cplx* TWP, const cplx* W, int t, int nt) {
-  constexpr int R = tile_radix<M>();
-  int off = 0;
-  for (int Ns = tile_first_radix<M>(); Ns < M; Ns *= R) {
-    const int step = M / (Ns * R);
-    for (int e = t; e < (R - 1) * Ns; e += nt) TWP[off + e] = W[(e / (R - 1)) * (e % (R - 1) + 1) * step];
-    off += (R - 1) * Ns;
-  }
-}
-
-template <int M, int R, bool INV, bool FIRST>
-__device__ __forceinline__ void tile_pass(cplx* buf, const cplx* TW, int tid, int Ns) {
-  constexpr int TH = tile_threads<M>();
-  constexpr int NB = M / R / TH;
-  static_assert(NB >= 1 && (M / R) % TH == 0, "pass split");
-  cplx v[NB][R];
-#pragma unroll
-  for (int s = 0; s < NB; ++s) {
-    const int j = tid + s * TH;
-#pragma unroll
-    for (int r = 0; r < R; ++r) v[s][r] = buf[sw(j + r * (M / R))];
-  }
-  tile_sync<TH>();
-#pragma unroll
-  for (int s = 0; s < NB; ++s) {
-    const int j = tid + s * TH;
-    const int kk = FIRST ? 0 : (j & (Ns - 1));
-    if constexpr (!FIRST) {
-#pragma unroll
-      for (int r = 1; r < R; ++r) {
-        const cplx w = TW[kk * (R - 1) + r - 1];
-        v[s][r] = INV ? cmulc(v[s][r], w) : cmul(v[s][r], w);
-      }
-    }
-    if constexpr (R == 2) {
-      const cplx x0 = v[s][0], x1 = v[s][1];
-      v[s][0] = cadd(x0, x1);
-      v[s][1] = csub(x0, x1);
-    } else if constexpr (R == 4) {
-      const cplx t0 = cadd(v[s][0], v[s][2]), t1 = csub(v[s][0], v[s][2]);
-      const cplx t2 = cadd(v[s][1], v[s][3]), t3 = mul_mi<INV>(csub(v[s][1], v[s][3]));
-      v[s][0] = cadd(t0, t2);
-      v[s][2] = csub(t0, t2);
-      v[s][1] = cadd(t1, t3);
-      v[s][3] = csub(t1, t3);
-    } else {
-      dft8<INV>(v[s]);
-    }
-    const int d = (j - kk) * R + kk;
-#pragma unroll
-    for (int r = 0; r < R; ++r) buf[sw(d + r * Ns)] = v[s][r];
-  }
-  tile_sync<TH>();
-}
-
-template <int M, bool INV>
-__device__ __forceinline__ void tile_fft(cplx* buf, const cplx* TWP, int tid) {
-  constexpr int R = tile_radix<M>(), R0 = tile_first_radix<M>();
-  static_assert(R == 4 || R == 8, "tile radix");
-  tile_pass<M, R0, INV, true>(buf, nullptr, tid, 1);
-  int off = 0;
-#pragma unroll 1
-  for (int Ns = R0; Ns < M; Ns *= R) {
-    tile_pass<M, R, INV, false>(buf, TWP + off, tid, Ns);
-    off += (R - 1) * Ns;
-  }
-}
-
 template <int M, int K1, int KL, int T, int L, int C>
 struct TileGeo {
   static constexpr int TH = tile_threads<M>();  // threads per polynomial
   static constexpr int NT = C * K1 * TH;      // threads per workgroup
-  static constexpr int BASE = ((C * KL * T + C * K1) * M + tile_tw_entries<M>()) * 16;
+  static constexpr int BASE = ((C * KL * T + C * K1) * M + tile_tw_entries<M, TH>()) * 16;
   static constexpr bool ZLDS = BASE + M * 16 <= 160 * 1024;  // twist table in LDS when it fits
   static constexpr int LDS = BASE + (ZLDS ? M * 16 : 0);
   static_assert(M <= 512 && NT <= 1024 && LDS <= 160 * 1024, "tile shape");
@@ -720,8 +733,8 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
   cplx* Xs = reinterpret_cast<cplx*>(smem);  // [C][KL rq][T t][M] digit spectra (slots sw(f))
   cplx* Ys = Xs + C * KL * T * M;            // [C][K1 c][M] slot spectra / rotation scratch
   cplx* W = Ys + C * K1 * M;  // per-pass twiddles (tile_fft)
-  cplx* Zl = W + tile_tw_entries<M>();
-  build_tile_tw<M>(W, a.Wfull, threadIdx.x, NT);
+  cplx* Zl = W + tile_tw_entries<M, TH>();
+  build_tile_tw<M, TH>(W, a.Wfull, threadIdx.x, NT);
   if constexpr (TG::ZLDS)
     for (int e = threadIdx.x; e < M; e += NT) Zl[e] = a.Z[e];
   auto zeta = [&](int j) { return TG::ZLDS ? Zl[j] : a.Z[j]; };
@@ -802,7 +815,7 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
           xs[sw(j)] = cmul(cplx{(double)s0, (double)s1}, zeta(j));
         }
         tile_sync<TH>();
-        tile_fft<M, false>(xs, W, tid);
+        tile_fft<M, TH, false>(xs, W, tid);
       }
     }
     __syncthreads();
@@ -852,7 +865,7 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
         }
       }
       __syncthreads();
-      tile_fft<M, true>(ybuf, W, tid);
+      tile_fft<M, TH, true>(ybuf, W, tid);
       const uint32_t sh = m * a.bits;
 #pragma unroll
       for (int e = 0; e < VPT; ++e) {
@@ -916,9 +929,13 @@ __global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, c
                                                                         const cplx* Whi, const cplx* Z, uint32_t k,
                                                                         uint32_t level, uint32_t bits, uint32_t limbs) {
   constexpr int N = 2 * M, TH = Geo<M>::THREADS, VPT = Geo<M>::VPT;
-  __shared__ cplx buf[M + tw_entries<M>()];
+  constexpr bool PP = M <= 4096;  // as gen_step_kernel
+  __shared__ cplx buf[M + (PP ? tile_tw_entries<M, TH>() : tw_entries<M>())];
   cplx* W = buf + M;
-  load_twiddles<M>(W, Wfull, Wlo, Whi, threadIdx.x, TH);
+  if constexpr (PP)
+    build_tile_tw<M, TH>(W, Wfull, threadIdx.x, TH);
+  else
+    load_twiddles<M>(W, Wfull, Wlo, Whi, threadIdx.x, TH);
   __syncthreads();
   const int tid = threadIdx.x;
   const uint32_t K1 = k + 1;
@@ -953,7 +970,10 @@ __global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, c
       buf[sw(j)] = cmul(cplx{(double)s0, (double)s1}, Z[j]);
     }
     __syncthreads();
-    fft_block<M, false>(buf, W, tid);
+    if constexpr (PP)
+      tile_fft<M, TH, false>(buf, W, tid);
+    else
+      fft_block<M, false>(buf, W, tid);
     cplx* dst = G + ((((i * K1 + c) * limbs + lim) * K1 + r) * level + q) * (uint64_t)M;
 #pragma unroll
     for (int e = 0; e < VPT; ++e) {

@@ -673,9 +673,66 @@ __global__ void __launch_bounds__(256) gen_mac2_kernel(MacArgs a) {
   }
 }
 
+// k = 1 (two output polynomials): one thread per frequency computing both outputs, so each
+// digit spectrum value is read once per tile instead of once per output polynomial (the
+// product is HBM-bound on the X/Y spectra at N >= 2048).
+template <int KL, int L, int T>
+__global__ void __launch_bounds__(256) gen_mac2k1_kernel(MacArgs a) {
+  const uint32_t f = blockIdx.x * 256 + threadIdx.x;
+  const uint64_t M = a.M;
+  if (f >= M) return;
+  cplx kv[2][L][KL];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int lim = 0; lim < L; ++lim)
+#pragma unroll
+      for (int rq = 0; rq < KL; ++rq)
+        kv[c][lim][rq] = a.G[((((uint64_t)a.i * 2 + c) * L + lim) * KL + rq) * M + f];
+  const uint32_t ct0 = blockIdx.z * MAC_CTS;
+  for (uint32_t ct = ct0; ct < ct0 + MAC_CTS && ct < a.count; ++ct) {
+    const cplx* Xct = a.X + (uint64_t)ct * KL * T * M + f;
+    cplx xv[KL][T];
+#pragma unroll
+    for (int rq = 0; rq < KL; ++rq)
+#pragma unroll
+      for (int t = 0; t < T; ++t) xv[rq][t] = Xct[(uint64_t)(rq * T + t) * M];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      cplx* Yct = a.Y + ((uint64_t)ct * 2 + c) * L * M + f;
+#pragma unroll
+      for (int m = 0; m < L; ++m) {
+        cplx y = {0.0, 0.0};
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          if (m - t < 0 || m - t >= L) continue;
+#pragma unroll
+          for (int rq = 0; rq < KL; ++rq) {
+            const cplx xg = xv[rq][t], g = kv[c][m - t][rq];
+            y.re = __builtin_fma(xg.re, g.re, __builtin_fma(-xg.im, g.im, y.re));
+            y.im = __builtin_fma(xg.re, g.im, __builtin_fma(xg.im, g.re, y.im));
+          }
+        }
+        Yct[(uint64_t)m * M] = y;
+      }
+    }
+  }
+}
+
 // launch the register-tiled product for (K1 l, L, T) when instantiated, else the generic one
 static bool launch_mac2(const MacArgs& m, uint32_t cnt, hipStream_t st) {
   const uint32_t KL = (m.k + 1) * m.level;
+  if (m.k == 1 && m.M >= 1024) {
+    const dim3 g1((m.M + 255) / 256, 1, (cnt + MAC_CTS - 1) / MAC_CTS);
+#define GEN_MAC2K1(KLv, Lv, Tv)                                                              \
+    if (KL == KLv && m.limbs == Lv && m.subs == Tv) {                                        \
+      hipLaunchKernelGGL((gen_mac2k1_kernel<KLv, Lv, Tv>), g1, dim3(256), 0, st, m);         \
+      return true;                                                                           \
+    }
+    GEN_MAC2K1(2, 5, 2) GEN_MAC2K1(2, 6, 2) GEN_MAC2K1(4, 6, 2) GEN_MAC2K1(4, 5, 2) GEN_MAC2K1(4, 5, 1)
+    GEN_MAC2K1(4, 6, 1)
+#undef GEN_MAC2K1
+  }
   const dim3 grid((m.M + 255) / 256, m.k + 1, (cnt + MAC_CTS - 1) / MAC_CTS);
 #define GEN_MAC2(KLv, Lv, Tv)                                                               \
   if (KL == KLv && m.limbs == Lv && m.subs == Tv) {                                           \

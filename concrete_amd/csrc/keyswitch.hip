@@ -35,7 +35,11 @@ __global__ void keyswitch_zero_kernel(uint64_t* out, const uint64_t* out_idx, ui
   }
 }
 
-template <int U, bool SPLIT>
+// CH16: the 64-bit products d * k split into four 16-bit key chunks, d * k_c summed in int32
+// with full-rate 24-bit multiplies (|d| <= 2^(logB-1), so a KS_ICHUNK block of level rows sums
+// below 2^31 when level 2^logB <= 2^11, see keyswitch_launch) and folded into the u64
+// accumulators once per block: exact, and it replaces the quarter-rate 32-bit multiplies.
+template <int U, bool SPLIT, bool CH16>
 __global__ void __launch_bounds__(KS_THREADS)
 keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx, const uint64_t* __restrict__ in,
                  const uint64_t* __restrict__ in_idx, const uint64_t* __restrict__ ksk, uint32_t n_in,
@@ -65,15 +69,49 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
     }
     __syncthreads();
     const uint32_t iend = min(KS_ICHUNK, (int)(i_end - i0));
-    for (uint32_t ii = 0; ii < iend; ++ii) {
-      for (uint32_t t = 0; t < level; ++t) {
-        const uint64_t* row = ksk + ((uint64_t)(i0 + ii) * level + t) * W;
+    if constexpr (CH16) {
+      int32_t ca[KS_TILE][U][4];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const uint32_t j = tid + u * KS_THREADS;
-          const uint64_t kv = j < W ? row[j] : 0ull;
+      for (int s = 0; s < KS_TILE; ++s)
 #pragma unroll
-          for (int s = 0; s < KS_TILE; ++s) acc[s][u] -= (uint64_t)(int64_t)dig[s][ii][t] * kv;
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) ca[s][u][c] = 0;
+      for (uint32_t ii = 0; ii < iend; ++ii) {
+        for (uint32_t t = 0; t < level; ++t) {
+          const uint64_t* row = ksk + ((uint64_t)(i0 + ii) * level + t) * W;
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const uint32_t j = tid + u * KS_THREADS;
+            const uint64_t kv = j < W ? row[j] : 0ull;
+            const int32_t kc[4] = {(int32_t)(kv & 0xffffu), (int32_t)((kv >> 16) & 0xffffu),
+                                   (int32_t)((kv >> 32) & 0xffffu), (int32_t)(kv >> 48)};
+#pragma unroll
+            for (int s = 0; s < KS_TILE; ++s) {
+              const int32_t d = dig[s][ii][t];
+#pragma unroll
+              for (int c = 0; c < 4; ++c) ca[s][u][c] += __mul24(d, kc[c]);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < KS_TILE; ++s)
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          acc[s][u] -= (uint64_t)(int64_t)ca[s][u][0] + ((uint64_t)(int64_t)ca[s][u][1] << 16) +
+                       ((uint64_t)(int64_t)ca[s][u][2] << 32) + ((uint64_t)(int64_t)ca[s][u][3] << 48);
+    } else {
+      for (uint32_t ii = 0; ii < iend; ++ii) {
+        for (uint32_t t = 0; t < level; ++t) {
+          const uint64_t* row = ksk + ((uint64_t)(i0 + ii) * level + t) * W;
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const uint32_t j = tid + u * KS_THREADS;
+            const uint64_t kv = j < W ? row[j] : 0ull;
+#pragma unroll
+            for (int s = 0; s < KS_TILE; ++s) acc[s][u] -= (uint64_t)(int64_t)dig[s][ii][t] * kv;
+          }
         }
       }
     }
@@ -114,13 +152,22 @@ int keyswitch_launch(const KsArgs& a) {
     hipLaunchKernelGGL(keyswitch_zero_kernel, dim3((uint32_t)std::min<uint64_t>((total + 255) / 256, 4096)), dim3(256),
                        0, a.stream, a.out, a.out_idx, a.n_out + 1, a.num_samples);
   }
-#define KS_LAUNCH(UU)                                                                                            \
-  if (splits > 1)                                                                                                \
-    hipLaunchKernelGGL((keyswitch_kernel<UU, true>), dim3(blocks, splits), dim3(KS_THREADS), 0, a.stream, a.out, \
-                       a.out_idx, a.in, a.in_idx, a.ksk, a.n_in, a.n_out, a.base_log, a.level, a.num_samples, per); \
-  else                                                                                                           \
-    hipLaunchKernelGGL((keyswitch_kernel<UU, false>), dim3(blocks), dim3(KS_THREADS), 0, a.stream, a.out,       \
+  // int32 chunk sums of one block: KS_ICHUNK level 2^(logB-1) (2^16 - 1) < 2^31
+  const bool ch16 = (uint64_t)KS_ICHUNK * a.level * (1ull << (a.base_log - 1)) * 65535ull < (1ull << 31);
+#define KS_LAUNCH2(UU, CH)                                                                                         \
+  if (splits > 1)                                                                                                  \
+    hipLaunchKernelGGL((keyswitch_kernel<UU, true, CH>), dim3(blocks, splits), dim3(KS_THREADS), 0, a.stream,     \
+                       a.out, a.out_idx, a.in, a.in_idx, a.ksk, a.n_in, a.n_out, a.base_log, a.level,              \
+                       a.num_samples, per);                                                                        \
+  else                                                                                                             \
+    hipLaunchKernelGGL((keyswitch_kernel<UU, false, CH>), dim3(blocks), dim3(KS_THREADS), 0, a.stream, a.out,     \
                        a.out_idx, a.in, a.in_idx, a.ksk, a.n_in, a.n_out, a.base_log, a.level, a.num_samples, per)
+#define KS_LAUNCH(UU)          \
+  if (ch16) {                  \
+    KS_LAUNCH2(UU, true);      \
+  } else {                     \
+    KS_LAUNCH2(UU, false);     \
+  }
   switch (U) {
     case 1: KS_LAUNCH(1); break;
     case 2: KS_LAUNCH(2); break;
@@ -128,6 +175,7 @@ int keyswitch_launch(const KsArgs& a) {
     default: KS_LAUNCH(4); break;
   }
 #undef KS_LAUNCH
+#undef KS_LAUNCH2
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("keyswitch launch failed: %s", hipGetErrorString(e));

@@ -44,7 +44,8 @@ __global__ void __launch_bounds__(KS_THREADS)
 keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx, const uint64_t* __restrict__ in,
                  const uint64_t* __restrict__ in_idx, const uint64_t* __restrict__ ksk, uint32_t n_in,
                  uint32_t n_out, uint32_t base_log, uint32_t level, uint32_t num_samples, uint32_t i_per_split) {
-  __shared__ int32_t dig[KS_TILE][KS_ICHUNK][KS_MAX_L];
+  // digits sample-minor: the KS_TILE digits of one (position, level) are two 16-byte reads
+  __shared__ __attribute__((aligned(16))) int32_t dig[KS_ICHUNK][KS_MAX_L][KS_TILE];
   const uint32_t s0 = blockIdx.x * KS_TILE;
   const int tid = threadIdx.x;
   const uint32_t W = n_out + 1;
@@ -65,7 +66,7 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
       uint64_t a = 0ull;
       if (smp < num_samples && i < i_end) a = in[(in_idx ? in_idx[smp] : smp) * (uint64_t)(n_in + 1) + i];
       uint64_t st = decomp_init(a, nrep);
-      for (uint32_t t = 0; t < level; ++t) dig[s][ii][t] = decomp_next(st, (int)base_log);
+      for (uint32_t t = 0; t < level; ++t) dig[ii][t][s] = decomp_next(st, (int)base_log);
     }
     __syncthreads();
     const uint32_t iend = min(KS_ICHUNK, (int)(i_end - i0));
@@ -88,7 +89,7 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
                                    (int32_t)((kv >> 32) & 0xffffu), (int32_t)(kv >> 48)};
 #pragma unroll
             for (int s = 0; s < KS_TILE; ++s) {
-              const int32_t d = dig[s][ii][t];
+              const int32_t d = dig[ii][t][s];
 #pragma unroll
               for (int c = 0; c < 4; ++c) ca[s][u][c] += __mul24(d, kc[c]);
             }
@@ -110,7 +111,7 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
             const uint32_t j = tid + u * KS_THREADS;
             const uint64_t kv = j < W ? row[j] : 0ull;
 #pragma unroll
-            for (int s = 0; s < KS_TILE; ++s) acc[s][u] -= (uint64_t)(int64_t)dig[s][ii][t] * kv;
+            for (int s = 0; s < KS_TILE; ++s) acc[s][u] -= (uint64_t)(int64_t)dig[ii][t][s] * kv;
           }
         }
       }

@@ -892,6 +892,42 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
         load_key(i, m + 1);
       else if (i + 1 < a.n)
         load_key(i + 1, 0);
+      if constexpr (NT % M == 0 && IPT > 1) {
+        // a thread's items share one frequency (it % M = threadIdx.x % M): each digit spectrum
+        // value is read from LDS once per limb for all its output polynomials
+        const int sf = sw(threadIdx.x % M);
+#pragma unroll
+        for (int lc = 0; lc < C; ++lc) {
+          cplx x0[KL], x1[KL];
+#pragma unroll
+          for (int rq = 0; rq < KL; ++rq) {
+            x0[rq] = Xs[((lc * KL + rq) * T) * M + sf];
+            if constexpr (T > 1) x1[rq] = Xs[((lc * KL + rq) * T + 1) * M + sf];
+          }
+#pragma unroll
+          for (int s = 0; s < IPT; ++s) {
+            const int cc = (threadIdx.x + s * NT) / M;
+            cplx y = (T > 1 && m > 0) ? carry[s][lc] : cplx{0.0, 0.0};
+#pragma unroll
+            for (int rq = 0; rq < KL; ++rq) {
+              const cplx xv = x0[rq], gv = gk[s][rq];
+              y.re = __builtin_fma(xv.re, gv.re, __builtin_fma(-xv.im, gv.im, y.re));
+              y.im = __builtin_fma(xv.re, gv.im, __builtin_fma(xv.im, gv.re, y.im));
+            }
+            Ys[(lc * K1 + cc) * M + sf] = y;
+            if constexpr (T > 1) {
+              cplx z = {0.0, 0.0};
+#pragma unroll
+              for (int rq = 0; rq < KL; ++rq) {
+                const cplx xv = x1[rq], gv = gk[s][rq];
+                z.re = __builtin_fma(xv.re, gv.re, __builtin_fma(-xv.im, gv.im, z.re));
+                z.im = __builtin_fma(xv.re, gv.im, __builtin_fma(xv.im, gv.re, z.im));
+              }
+              carry[s][lc] = z;
+            }
+          }
+        }
+      } else {
 #pragma unroll
       for (int s = 0; s < IPT; ++s) {
         const int it = threadIdx.x + s * NT;
@@ -920,6 +956,7 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
             }
           }
         }
+      }
       }
       __syncthreads();
       tile_fft<M, TH, true>(ybuf, W, tid);
@@ -1113,10 +1150,10 @@ static void launch_tile(const TileArgs& t, hipStream_t st) {
   hipLaunchKernelGGL(kern, dim3((t.count + C - 1) / C), dim3(TG::NT), TG::LDS, st, t);
 }
 
-// Tile sizes (ciphertexts per workgroup) measured on MI355X: N = 256, k = 5: C = 4 (54.5k PBS/s;
-// C = 2 spills: 33.3k); N = 512, k = 3: C = 1 (34.9k; C = 2: 33.4k).  CONCRETE_HIP_TILE_C=2
-// selects the alternative for A/B runs.  N = 1024 stays on the two-launch path: a tile of one
-// k = 2 ciphertext needs 398 VGPRs (two spill) and was no faster.  false: no tile instance.
+// Tile sizes (ciphertexts per workgroup) measured on MI355X: N = 256, k = 5: C = 4 (55.4k PBS/s;
+// C = 2: 44.3k); N = 512, k = 3: C = 2 (35.7k; C = 1: 22.3k at 269 VGPRs); N = 1024, k = 2:
+// C = 2 (18.5k; C = 1: 12.1k).  CONCRETE_HIP_TILE_C selects the alternative for A/B runs.
+// false: no tile instance for this shape (two-launch path).
 static bool tile_dispatch(uint32_t N, uint32_t K1, uint32_t KL, uint32_t T, uint32_t L, const TileArgs& t,
                           hipStream_t st) {
   static const int tile_c = getenv("CONCRETE_HIP_TILE_C") ? atoi(getenv("CONCRETE_HIP_TILE_C")) : 0;
@@ -1126,8 +1163,8 @@ static bool tile_dispatch(uint32_t N, uint32_t K1, uint32_t KL, uint32_t T, uint
     return true;
   }
   if (N == 512 && K1 == 4 && KL == 4 && T == 2 && L == 5) {
-    if (tile_c == 2) launch_tile<256, 4, 4, 2, 5, 2>(t, st);
-    else launch_tile<256, 4, 4, 2, 5, 1>(t, st);
+    if (tile_c == 1) launch_tile<256, 4, 4, 2, 5, 1>(t, st);
+    else launch_tile<256, 4, 4, 2, 5, 2>(t, st);
     return true;
   }
   if (N == 1024 && K1 == 3 && KL == 3 && T == 2 && L == 5) {

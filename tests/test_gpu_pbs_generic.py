@@ -91,6 +91,19 @@ def test_generic_pbs_bit_exact(B, oracle, torch_cuda, case):
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
 
 
+@pytest.mark.parametrize("ci", [0, 2, 3], ids=[CASES[i][0] for i in (0, 2, 3)])
+def test_generic_tile_many_workgroups(B, oracle, torch_cuda, ci):
+    """The one-launch tile kernels over many workgroups (67 ciphertexts: not a multiple of any
+    tile size, so the last workgroup runs empty groups), bit-exact vs the exact oracle."""
+    case = CASES[ci][:3] + (4,) + CASES[ci][4:]
+    p, glwe_sk, bsk, fbsk, cts, acc, table, msgs, got, resid = run_case(B, oracle, torch_cuda, case, 7500, batch=67)
+    op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
+    ref, _ = oracle.pbs_batch(op, cts, acc[None, :], bsk=bsk, mode=oracle.MODE_KARATSUBA)
+    assert np.array_equal(got, ref)
+    dec = B.lwe_decrypt(glwe_sk, got, p.big_n)
+    assert [B.decode(d, case[6]) for d in dec] == [int(table[m]) for m in msgs]
+
+
 def test_generic_8bit_long_chain_decrypts(B, oracle, torch_cuda):
     """v0_last_128 8-bit row (k = 1, N = 16384, l = 2, logB = 15) over a 128-step blind rotation:
     every output decrypts to LUT[m] (decrypt-level: 128 Karatsuba steps at N = 16384 are slow)."""

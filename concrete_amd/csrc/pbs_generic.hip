@@ -242,8 +242,8 @@ __device__ __forceinline__ void fft_block(cplx* buf, const cplx* W, int tid) {
 // (all twiddles 1) multiplies by nothing.
 // threads per polynomial in the tile kernels: the step kernel's for M <= 256, 128 (two waves,
 // four values each) at M = 512
-#ifndef TILE_PAIR
-#define TILE_PAIR 1
+#ifndef TILE_GROUPS
+#define TILE_GROUPS 1
 #endif
 #ifndef TILE512_TH
 #define TILE512_TH 128
@@ -824,9 +824,16 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
   const int nrep = 64 - LV * logB;
   const uint64_t half = 1ull << (sb - 1), bmask = (1ull << sb) - 1ull;
   // key values of product item (c, f) = (it / M, it % M), it = threadIdx.x + s NT, for slot m
-  // PAIR (N = 256 tiles): product items of two output polynomials each (each digit-spectrum
-  // value read from LDS serves both; the product phase is LDS-bound: 55.4k -> 61.3k PBS/s)
-  constexpr bool PAIR = TILE_PAIR && NT == K1 * M && C % 2 == 0 && K1 % 2 == 0;
+  // Output-group items (PAIR): an item = (frequency, CP output polynomials, C / LCS ciphertexts
+  // of the tile), so each digit-spectrum value read from LDS serves CP outputs (the product
+  // phase is LDS-bound): N = 256: CP = 2, LCS = 2 (55.4k -> 61.3k PBS/s at opt1).  Measured
+  // slower where the per-item key prefetch it gives up mattered more: N = 512 with CP = 4
+  // (34.1k vs 35.7k), N = 1024 with CP = 3 (18.3k vs 18.5k).
+  constexpr int CP = !TILE_GROUPS ? 0 : (M == 128 && K1 == 6 && C == 4) ? 2 : 0;
+  constexpr int LCS = CP == 2 ? 2 : CP == 4 ? 2 : 1;
+  constexpr bool PAIR = CP > 0;
+  constexpr int NGRP = PAIR ? K1 / CP : 1, LPG = PAIR ? C / LCS : 1, GITEMS = NGRP * M * LCS;
+  static_assert(!PAIR || (K1 % CP == 0 && C % LCS == 0 && GITEMS <= NT), "output groups");
   cplx gn[IPT][KL];
   auto load_key = [&](uint32_t step, int m) {
 #pragma unroll
@@ -886,7 +893,7 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
     // limb j's key values serve slot j (sub-digit 0) and slot j + 1 (sub-digit 1); the
     // sub-digit-1 partial of slot j + 1 waits in registers (same thread, same item)
     cplx carry[IPT][C];
-    cplx carry2[2][C / 2 > 0 ? C / 2 : 1];
+    cplx carry2[PAIR ? CP : 1][LPG];
 #pragma unroll 1
     for (int m = 0; m < L; ++m) {
       // this limb's key values were loaded one limb ahead; issue the next limb's now
@@ -902,53 +909,56 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
           load_key(i + 1, 0);
       }
       if constexpr (PAIR) {
-        // item = (frequency, pair of output polynomials, half of the tile's ciphertexts):
-        // each digit-spectrum value read serves two outputs
-        const int f = threadIdx.x % M, r1 = threadIdx.x / M, cg = r1 % (K1 / 2), lg = r1 / (K1 / 2);
-        const int sf = sw(f);
-        // key values loaded at the start of the limb: a prefetch (24 more VGPRs) spills at
-        // 768 threads and measured slower (55.2k vs 61.3k PBS/s at opt1)
-        cplx g2[2][KL];
+        const int it = threadIdx.x;
+        if (GITEMS == NT || it < GITEMS) {
+          const int f = it % M, r1 = it / M, cg = r1 % NGRP, lg = r1 / NGRP;
+          const int sf = sw(f);
+          // key values loaded at the start of the limb: a prefetch (24 more VGPRs at N = 256)
+          // spills at 768 threads and measured slower (55.2k vs 61.3k PBS/s at opt1)
+          cplx g2[CP][KL];
 #pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const cplx* Gp = a.G + (((uint64_t)i * K1 + cg * 2 + p) * L + m) * (uint64_t)(KL * M) + f;
+          for (int p = 0; p < CP; ++p) {
+            const cplx* Gp = a.G + (((uint64_t)i * K1 + cg * CP + p) * L + m) * (uint64_t)(KL * M) + f;
 #pragma unroll
-          for (int rq = 0; rq < KL; ++rq) g2[p][rq] = Gp[rq * M];
-        }
-#pragma unroll
-        for (int lcl = 0; lcl < C / 2; ++lcl) {
-          const int lc = lg * (C / 2) + lcl;
-          // sub-digit 0 (completes slot m), then sub-digit 1 (starts slot m + 1): one spectrum
-          // row in registers at a time
-          cplx y[2];
-#pragma unroll
-          for (int p = 0; p < 2; ++p) y[p] = (T > 1 && m > 0) ? carry2[p][lcl] : cplx{0.0, 0.0};
-#pragma unroll
-          for (int rq = 0; rq < KL; ++rq) {
-            const cplx xv = Xs[((lc * KL + rq) * T) * M + sf];
-#pragma unroll
-            for (int p = 0; p < 2; ++p) {
-              const cplx gv = g2[p][rq];
-              y[p].re = __builtin_fma(xv.re, gv.re, __builtin_fma(-xv.im, gv.im, y[p].re));
-              y[p].im = __builtin_fma(xv.re, gv.im, __builtin_fma(xv.im, gv.re, y[p].im));
-            }
+            for (int rq = 0; rq < KL; ++rq) g2[p][rq] = Gp[rq * M];
           }
 #pragma unroll
-          for (int p = 0; p < 2; ++p) Ys[(lc * K1 + cg * 2 + p) * M + sf] = y[p];
-          if constexpr (T > 1) {
-            cplx z[2] = {{0.0, 0.0}, {0.0, 0.0}};
+          for (int lcl = 0; lcl < LPG; ++lcl) {
+            const int lc = lg * LPG + lcl;
+            // sub-digit 0 (completes slot m), then sub-digit 1 (starts slot m + 1): one
+            // spectrum row in registers at a time
+            cplx y[CP];
+#pragma unroll
+            for (int p = 0; p < CP; ++p) y[p] = (T > 1 && m > 0) ? carry2[p][lcl] : cplx{0.0, 0.0};
 #pragma unroll
             for (int rq = 0; rq < KL; ++rq) {
-              const cplx xv = Xs[((lc * KL + rq) * T + 1) * M + sf];
+              const cplx xv = Xs[((lc * KL + rq) * T) * M + sf];
 #pragma unroll
-              for (int p = 0; p < 2; ++p) {
+              for (int p = 0; p < CP; ++p) {
                 const cplx gv = g2[p][rq];
-                z[p].re = __builtin_fma(xv.re, gv.re, __builtin_fma(-xv.im, gv.im, z[p].re));
-                z[p].im = __builtin_fma(xv.re, gv.im, __builtin_fma(xv.im, gv.re, z[p].im));
+                y[p].re = __builtin_fma(xv.re, gv.re, __builtin_fma(-xv.im, gv.im, y[p].re));
+                y[p].im = __builtin_fma(xv.re, gv.im, __builtin_fma(xv.im, gv.re, y[p].im));
               }
             }
 #pragma unroll
-            for (int p = 0; p < 2; ++p) carry2[p][lcl] = z[p];
+            for (int p = 0; p < CP; ++p) Ys[(lc * K1 + cg * CP + p) * M + sf] = y[p];
+            if constexpr (T > 1) {
+              cplx z[CP];
+#pragma unroll
+              for (int p = 0; p < CP; ++p) z[p] = {0.0, 0.0};
+#pragma unroll
+              for (int rq = 0; rq < KL; ++rq) {
+                const cplx xv = Xs[((lc * KL + rq) * T + 1) * M + sf];
+#pragma unroll
+                for (int p = 0; p < CP; ++p) {
+                  const cplx gv = g2[p][rq];
+                  z[p].re = __builtin_fma(xv.re, gv.re, __builtin_fma(-xv.im, gv.im, z[p].re));
+                  z[p].im = __builtin_fma(xv.re, gv.im, __builtin_fma(xv.im, gv.re, z[p].im));
+                }
+              }
+#pragma unroll
+              for (int p = 0; p < CP; ++p) carry2[p][lcl] = z[p];
+            }
           }
         }
       } else if constexpr (NT % M == 0 && IPT > 1) {

@@ -826,10 +826,12 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
   // key values of product item (c, f) = (it / M, it % M), it = threadIdx.x + s NT, for slot m
   // Output-group items (PAIR): an item = (frequency, CP output polynomials, C / LCS ciphertexts
   // of the tile), so each digit-spectrum value read from LDS serves CP outputs (the product
-  // phase is LDS-bound): N = 256: CP = 2, LCS = 2 (55.4k -> 61.3k PBS/s at opt1).  Measured
-  // slower where the per-item key prefetch it gives up mattered more: N = 512 with CP = 4
-  // (34.1k vs 35.7k), N = 1024 with CP = 3 (18.3k vs 18.5k).
-  constexpr int CP = !TILE_GROUPS ? 0 : (M == 128 && K1 == 6 && C == 4) ? 2 : 0;
+  // phase is LDS-bound): N = 256: CP = 2, LCS = 2 (55.4k -> 61.3k PBS/s at opt1); N = 1024:
+  // CP = 3, LCS = 1 with the key prefetch (512 items, a third of the threads idle in the
+  // product).  N = 512 keeps per-(output, frequency) items with shared-frequency reads: CP = 4
+  // measured 34.1k (33.5k with prefetch) vs 35.9k.
+  constexpr int CP = !TILE_GROUPS ? 0 : (M == 128 && K1 == 6 && C == 4) ? 2 : (M == 512 && K1 == 3 && C == 2) ? 3 : 0;
+  constexpr bool GPF = CP == 3;  // N = 1024: the group's next-limb key values prefetched (18.5k -> 18.8k)
   constexpr int LCS = CP == 2 ? 2 : CP == 4 ? 2 : 1;
   constexpr bool PAIR = CP > 0;
   constexpr int NGRP = PAIR ? K1 / CP : 1, LPG = PAIR ? C / LCS : 1, GITEMS = NGRP * M * LCS;
@@ -847,6 +849,15 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
     }
   };
   if (!PAIR && a.n > 0) load_key(0, 0);
+  cplx gp2[GPF ? CP : 1][KL];  // GPF: the group's key values of the next limb
+  if constexpr (GPF) {
+    const int f = threadIdx.x % M, cg = (threadIdx.x / M) % NGRP;
+    if (a.n > 0 && (GITEMS == NT || (int)threadIdx.x < GITEMS))
+#pragma unroll
+      for (int p = 0; p < CP; ++p)
+#pragma unroll
+        for (int rq = 0; rq < KL; ++rq) gp2[p][rq] = a.G[((uint64_t)(cg * CP + p) * L * KL + rq) * M + f];
+  }
 #pragma unroll 1
   for (uint32_t i = 0; i < a.n; ++i) {
     // ct1 = X^{ms(a_i)} acc - acc (rotation through this group's slot buffer), decomposition,
@@ -916,11 +927,28 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
           // key values loaded at the start of the limb: a prefetch (24 more VGPRs at N = 256)
           // spills at 768 threads and measured slower (55.2k vs 61.3k PBS/s at opt1)
           cplx g2[CP][KL];
+          if constexpr (GPF) {
 #pragma unroll
-          for (int p = 0; p < CP; ++p) {
-            const cplx* Gp = a.G + (((uint64_t)i * K1 + cg * CP + p) * L + m) * (uint64_t)(KL * M) + f;
+            for (int p = 0; p < CP; ++p)
 #pragma unroll
-            for (int rq = 0; rq < KL; ++rq) g2[p][rq] = Gp[rq * M];
+              for (int rq = 0; rq < KL; ++rq) g2[p][rq] = gp2[p][rq];
+            const uint32_t ni = m + 1 < L ? i : i + 1;
+            const int nm = m + 1 < L ? m + 1 : 0;
+            if (ni < a.n) {
+#pragma unroll
+              for (int p = 0; p < CP; ++p) {
+                const cplx* Gp = a.G + (((uint64_t)ni * K1 + cg * CP + p) * L + nm) * (uint64_t)(KL * M) + f;
+#pragma unroll
+                for (int rq = 0; rq < KL; ++rq) gp2[p][rq] = Gp[rq * M];
+              }
+            }
+          } else {
+#pragma unroll
+            for (int p = 0; p < CP; ++p) {
+              const cplx* Gp = a.G + (((uint64_t)i * K1 + cg * CP + p) * L + m) * (uint64_t)(KL * M) + f;
+#pragma unroll
+              for (int rq = 0; rq < KL; ++rq) g2[p][rq] = Gp[rq * M];
+            }
           }
 #pragma unroll
           for (int lcl = 0; lcl < LPG; ++lcl) {

@@ -242,6 +242,9 @@ __device__ __forceinline__ void fft_block(cplx* buf, const cplx* W, int tid) {
 // (all twiddles 1) multiplies by nothing.
 // threads per polynomial in the tile kernels: the step kernel's for M <= 256, 128 (two waves,
 // four values each) at M = 512
+#ifndef TILE128_CP
+#define TILE128_CP 2
+#endif
 #ifndef TILE_GROUPS
 #define TILE_GROUPS 1
 #endif
@@ -829,10 +832,10 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
   // phase is LDS-bound): N = 256: CP = 2, LCS = 2 (55.4k -> 61.3k PBS/s at opt1); N = 1024:
   // CP = 3, LCS = 1 with the key prefetch (512 items, a third of the threads idle in the
   // product).  N = 512 keeps per-(output, frequency) items with shared-frequency reads: CP = 4
-  // measured 34.1k (33.5k with prefetch) vs 35.9k.
-  constexpr int CP = !TILE_GROUPS ? 0 : (M == 128 && K1 == 6 && C == 4) ? 2 : (M == 512 && K1 == 3 && C == 2) ? 3 : 0;
-  constexpr bool GPF = CP == 3;  // N = 1024: the group's next-limb key values prefetched (18.5k -> 18.8k)
-  constexpr int LCS = CP == 2 ? 2 : CP == 4 ? 2 : 1;
+  // measured 34.1k (33.5k with prefetch) vs 35.9k.  N = 256 with CP = 3 (512 items): 55.4k.
+  constexpr int CP = !TILE_GROUPS ? 0 : (M == 128 && K1 == 6 && C == 4) ? TILE128_CP : (M == 512 && K1 == 3 && C == 2) ? 3 : 0;
+  constexpr bool GPF = M == 512 && CP == 3;  // N = 1024: next-limb key values prefetched (18.5k -> 18.8k)
+  constexpr int LCS = M == 128 ? 2 : 1;
   constexpr bool PAIR = CP > 0;
   constexpr int NGRP = PAIR ? K1 / CP : 1, LPG = PAIR ? C / LCS : 1, GITEMS = NGRP * M * LCS;
   static_assert(!PAIR || (K1 % CP == 0 && C % LCS == 0 && GITEMS <= NT), "output groups");

@@ -326,6 +326,25 @@ def test_keyswitch_bit_exact_and_chain(B, oracle, cfg2, torch_cuda):
         assert [B.decode(d, width) for d in dec] == c["expected"], c["description"]
 
 
+@pytest.mark.parametrize("ks_l,ks_logB", [(4, 3), (6, 6), (2, 10), (2, 11), (1, 20)])
+def test_keyswitch_decompositions(B, oracle, torch_cuda, ks_l, ks_logB):
+    """The keyswitch's two product paths (keyswitch.hip): 16-bit key chunks with int32 block sums
+    when 32 l 2^(logB-1) (2^16 - 1) < 2^31 ((4,3), (6,6), and (2,10) at the edge), the 64-bit
+    products otherwise ((2,11), (1,20)); random inputs, 37 samples (a partial tile), bit-exact vs
+    the oracle."""
+    p = replace(B.CFG2, ks_level=ks_l, ks_base_log=ks_logB)
+    glwe_sk = B.binary_key(p.big_n, 8100 + ks_logB)
+    lwe_sk = B.binary_key(p.n, 8200 + ks_logB)
+    ksk = B.ksk_generate(p, glwe_sk, lwe_sk, 8300 + ks_logB)
+    rng = np.random.RandomState(ks_logB)
+    cts = rng.randint(0, 2 ** 63, size=(37, p.big_n + 1), dtype=np.int64).astype(np.uint64) * np.uint64(2) + \
+        np.uint64(1)
+    out = B.keyswitch(p, B.to_device(ksk, "cuda:0"), B.to_device(cts, "cuda:0"))
+    torch_cuda.cuda.synchronize()
+    op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, ks_l=ks_l, ks_logB=ks_logB)
+    assert np.array_equal(B.to_host(out), oracle.keyswitch_batch(op, cts, ksk))
+
+
 def test_configs2_total_batch_65536(B, oracle, cfg2, torch_cuda):
     """BASELINE configs[2]'s whole batch (65,536 PBS) in one launch on one GPU: every sample
     decrypts to LUT[m], 8 random rows bit-exact, outputs of identical inputs identical."""

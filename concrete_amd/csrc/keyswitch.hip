@@ -35,11 +35,12 @@ __global__ void keyswitch_zero_kernel(uint64_t* out, const uint64_t* out_idx, ui
   }
 }
 
-// CH16: the 64-bit products d * k split into four 16-bit key chunks, d * k_c summed in int32
-// with full-rate 24-bit multiplies (|d| <= 2^(logB-1), so a KS_ICHUNK block of level rows sums
-// below 2^31 when level 2^logB <= 2^11, see keyswitch_launch) and folded into the u64
-// accumulators once per block: exact, and it replaces the quarter-rate 32-bit multiplies.
-template <int U, bool SPLIT, bool CH16>
+// NCH > 0: the 64-bit products d * k split into NCH key chunks (3: 22/21/21 bits, 4: 16 bits
+// each), d * k_c summed in int32 with full-rate 24-bit multiply-adds (|d| <= 2^(logB-1), so a
+// block of FP positions x level rows stays below 2^31 — the host picks NCH by that bound, see
+// keyswitch_launch) and folded into the u64 accumulators once per block: exact, and it
+// replaces the quarter-rate 32-bit multiplies.  NCH = 0: the 64-bit products.
+template <int U, bool SPLIT, int NCH>
 __global__ void __launch_bounds__(KS_THREADS)
 keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx, const uint64_t* __restrict__ in,
                  const uint64_t* __restrict__ in_idx, const uint64_t* __restrict__ ksk, uint32_t n_in,
@@ -70,38 +71,53 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
     }
     __syncthreads();
     const uint32_t iend = min(KS_ICHUNK, (int)(i_end - i0));
-    if constexpr (CH16) {
-      int32_t ca[KS_TILE][U][4];
+    if constexpr (NCH > 0) {
+      constexpr int FP = NCH == 3 ? 16 : KS_ICHUNK;  // positions per int32 block
+      for (uint32_t b0 = 0; b0 < iend; b0 += FP) {
+        int32_t ca[KS_TILE][U][NCH];
 #pragma unroll
-      for (int s = 0; s < KS_TILE; ++s)
+        for (int s = 0; s < KS_TILE; ++s)
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+          for (int u = 0; u < U; ++u)
 #pragma unroll
-          for (int c = 0; c < 4; ++c) ca[s][u][c] = 0;
-      for (uint32_t ii = 0; ii < iend; ++ii) {
-        for (uint32_t t = 0; t < level; ++t) {
-          const uint64_t* row = ksk + ((uint64_t)(i0 + ii) * level + t) * W;
+            for (int c = 0; c < NCH; ++c) ca[s][u][c] = 0;
+        const uint32_t b1 = min(b0 + FP, iend);
+        for (uint32_t ii = b0; ii < b1; ++ii) {
+          for (uint32_t t = 0; t < level; ++t) {
+            const uint64_t* row = ksk + ((uint64_t)(i0 + ii) * level + t) * W;
 #pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const uint32_t j = tid + u * KS_THREADS;
-            const uint64_t kv = j < W ? row[j] : 0ull;
-            const int32_t kc[4] = {(int32_t)(kv & 0xffffu), (int32_t)((kv >> 16) & 0xffffu),
-                                   (int32_t)((kv >> 32) & 0xffffu), (int32_t)(kv >> 48)};
+            for (int u = 0; u < U; ++u) {
+              const uint32_t j = tid + u * KS_THREADS;
+              const uint64_t kv = j < W ? row[j] : 0ull;
+              int32_t kc[NCH];
+              if constexpr (NCH == 3) {
+                kc[0] = (int32_t)(kv & 0x3fffffu);
+                kc[1] = (int32_t)((kv >> 22) & 0x1fffffu);
+                kc[2] = (int32_t)(kv >> 43);
+              } else {
 #pragma unroll
-            for (int s = 0; s < KS_TILE; ++s) {
-              const int32_t d = dig[ii][t][s];
+                for (int c = 0; c < NCH; ++c) kc[c] = (int32_t)((kv >> (16 * c)) & 0xffffu);
+              }
 #pragma unroll
-              for (int c = 0; c < 4; ++c) ca[s][u][c] += __mul24(d, kc[c]);
+              for (int s = 0; s < KS_TILE; ++s) {
+                const int32_t d = dig[ii][t][s];
+#pragma unroll
+                for (int c = 0; c < NCH; ++c) ca[s][u][c] += __mul24(d, kc[c]);
+              }
             }
           }
         }
+#pragma unroll
+        for (int s = 0; s < KS_TILE; ++s)
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            uint64_t sum = 0ull;
+#pragma unroll
+            for (int c = 0; c < NCH; ++c)
+              sum += (uint64_t)(int64_t)ca[s][u][c] << (NCH == 3 ? (c == 0 ? 0 : c == 1 ? 22 : 43) : 16 * c);
+            acc[s][u] -= sum;
+          }
       }
-#pragma unroll
-      for (int s = 0; s < KS_TILE; ++s)
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          acc[s][u] -= (uint64_t)(int64_t)ca[s][u][0] + ((uint64_t)(int64_t)ca[s][u][1] << 16) +
-                       ((uint64_t)(int64_t)ca[s][u][2] << 32) + ((uint64_t)(int64_t)ca[s][u][3] << 48);
     } else {
       for (uint32_t ii = 0; ii < iend; ++ii) {
         for (uint32_t t = 0; t < level; ++t) {
@@ -153,8 +169,10 @@ int keyswitch_launch(const KsArgs& a) {
     hipLaunchKernelGGL(keyswitch_zero_kernel, dim3((uint32_t)std::min<uint64_t>((total + 255) / 256, 4096)), dim3(256),
                        0, a.stream, a.out, a.out_idx, a.n_out + 1, a.num_samples);
   }
-  // int32 chunk sums of one block: KS_ICHUNK level 2^(logB-1) (2^16 - 1) < 2^31
-  const bool ch16 = (uint64_t)KS_ICHUNK * a.level * (1ull << (a.base_log - 1)) * 65535ull < (1ull << 31);
+  // int32 chunk sums of one block: FP level 2^(logB-1) (max chunk) < 2^31
+  const uint64_t dmax = (1ull << (a.base_log - 1)) * a.level;
+  const int nch = 16ull * dmax * ((1ull << 22) - 1) < (1ull << 31) ? 3
+                  : (uint64_t)KS_ICHUNK * dmax * 65535ull < (1ull << 31) ? 4 : 0;
 #define KS_LAUNCH2(UU, CH)                                                                                         \
   if (splits > 1)                                                                                                  \
     hipLaunchKernelGGL((keyswitch_kernel<UU, true, CH>), dim3(blocks, splits), dim3(KS_THREADS), 0, a.stream,     \
@@ -164,10 +182,12 @@ int keyswitch_launch(const KsArgs& a) {
     hipLaunchKernelGGL((keyswitch_kernel<UU, false, CH>), dim3(blocks), dim3(KS_THREADS), 0, a.stream, a.out,     \
                        a.out_idx, a.in, a.in_idx, a.ksk, a.n_in, a.n_out, a.base_log, a.level, a.num_samples, per)
 #define KS_LAUNCH(UU)          \
-  if (ch16) {                  \
-    KS_LAUNCH2(UU, true);      \
+  if (nch == 3) {              \
+    KS_LAUNCH2(UU, 3);         \
+  } else if (nch == 4) {       \
+    KS_LAUNCH2(UU, 4);         \
   } else {                     \
-    KS_LAUNCH2(UU, false);     \
+    KS_LAUNCH2(UU, 0);         \
   }
   switch (U) {
     case 1: KS_LAUNCH(1); break;

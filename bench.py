@@ -187,10 +187,11 @@ def main():
         ks_gbs = ks_launch_bytes / (ks_ms * 1e-3) / 1e9
         ks_res = {"metric": f"KS/sec per GPU at kN={p.big_n} -> n={p.n}, l={p.ks_level} logB={p.ks_base_log}",
                   "value": round(ks_rate, 1), "unit": "KS/s", "kernel_ms": round(ks_ms, 4),
-                  "roofline": {"bound": "hbm", "achieved": round(ks_gbs, 1), "peak": HBM_PEAK_GBS,
-                               "unit": "GB/s", "frac": round(ks_gbs / HBM_PEAK_GBS, 4),
-                               "bytes_per_launch": ks_launch_bytes, "bytes_per_ks_8d": ks_bytes,
-                               "note": "unique bytes per launch; VALU-bound (integer products)"}}
+                  # not HBM-bound: the unique bytes per launch are a small fraction of the peak, so
+                  # no HBM fraction is claimed
+                  "hbm": {"achieved": round(ks_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "bytes_per_launch": ks_launch_bytes, "bytes_per_ks_8d": ks_bytes,
+                          "note": "unique bytes per launch (the KSK once + every row in and out)"}}
         if rank == 0 and args.verify:
             from oracle import pyoracle as O
             op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, ks_l=p.ks_level, ks_logB=p.ks_base_log)

@@ -230,6 +230,17 @@ def pbs(p: PbsParams, fbsk, lwe_in, luts, lut_idx=None, in_idx=None, out_idx=Non
     return out
 
 
+def device_status(device="cuda:0") -> int:
+    """Synchronise the device and return (and clear) its sticky status: 0, or -4 when a PBS
+    kernel's wave synchronisation gave up since the last check (concrete_hip_device_status)."""
+    return int(_native.lib().concrete_hip_device_status(_gpu_index(device)))
+
+
+def set_spin_limit(polls: int) -> None:
+    """Spin bound of the PBS kernels' wave synchronisation (0 = default); a test hook."""
+    _native.lib().concrete_hip_set_spin_limit(int(polls))
+
+
 def keyswitch(p: PbsParams, ksk_dev, lwe_in, out=None, in_idx=None, out_idx=None, num_samples=None):
     """Batched LWE keyswitch kN -> n on device tensors."""
     torch = _torch()

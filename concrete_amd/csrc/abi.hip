@@ -5,6 +5,7 @@
 // The concrete_hip_* extensions return status codes for testability.
 #include <stdarg.h>
 
+#include <atomic>
 #include <mutex>
 #include <unordered_map>
 
@@ -38,6 +39,55 @@ static std::mutex g_keys_mu;
 static std::unordered_map<const void*, KeyEntry> g_keys;
 
 static void set_device(uint32_t gpu) { CHIP_CHECK(hipSetDevice((int)gpu)); }
+
+// Per-device status words (common.hpp SyncGuard): allocated on first use, zeroed, never freed.
+constexpr int STATUS_MAX_DEV = 64;
+static std::mutex g_status_mu;
+static uint32_t* g_status[STATUS_MAX_DEV] = {};
+static std::atomic<uint32_t> g_spin_limit{DEFAULT_SPIN_LIMIT};
+
+static uint32_t* status_word(int gpu) {
+  if (gpu < 0 || gpu >= STATUS_MAX_DEV) {
+    fprintf(stderr, "concrete-hip: device index %d out of range\n", gpu);
+    abort();
+  }
+  std::lock_guard<std::mutex> g(g_status_mu);
+  if (!g_status[gpu]) {
+    int prev = 0;
+    CHIP_CHECK(hipGetDevice(&prev));
+    CHIP_CHECK(hipSetDevice(gpu));
+    void* p = nullptr;
+    CHIP_CHECK(hipMalloc(&p, sizeof(uint32_t)));
+    CHIP_CHECK(hipMemset(p, 0, sizeof(uint32_t)));
+    CHIP_CHECK(hipSetDevice(prev));
+    g_status[gpu] = (uint32_t*)p;
+  }
+  return g_status[gpu];
+}
+
+SyncGuard sync_guard(int gpu) { return SyncGuard{status_word(gpu), g_spin_limit.load(std::memory_order_relaxed)}; }
+
+int take_device_status(int gpu) {
+  uint32_t* w;
+  {
+    std::lock_guard<std::mutex> g(g_status_mu);
+    w = (gpu >= 0 && gpu < STATUS_MAX_DEV) ? g_status[gpu] : nullptr;
+  }
+  if (!w) return 0;  // no PBS kernel has run on this device
+  CHIP_CHECK(hipSetDevice(gpu));
+  CHIP_CHECK(hipDeviceSynchronize());
+  uint32_t v = 0;
+  CHIP_CHECK(hipMemcpy(&v, w, sizeof v, hipMemcpyDeviceToHost));
+  if (v == 0) return 0;
+  CHIP_CHECK(hipMemset(w, 0, sizeof(uint32_t)));
+  if (v & DEV_STATUS_SYNC_TIMEOUT) {
+    set_error("device %d: a PBS wave synchronisation exceeded its spin bound; that launch's outputs are wrong",
+              gpu);
+    return -4;
+  }
+  set_error("device %d: status word 0x%x", gpu, v);
+  return -4;
+}
 
 
 }  // namespace chip
@@ -111,6 +161,9 @@ void cuda_drop_async(void* ptr, void* stream, uint32_t gpu_index) {
 void cuda_synchronize_device(uint32_t gpu_index) {
   set_device(gpu_index);
   CHIP_CHECK(hipDeviceSynchronize());
+  // the PBS kernels report synchronisation failures through the device status word: abort here,
+  // the reference's failure behaviour for the cuda_* entry points
+  if (take_device_status((int)gpu_index) != 0) die("cuda_synchronize_device");
 }
 
 // ----------------------------------------------------------------------------------------
@@ -118,6 +171,12 @@ void cuda_synchronize_device(uint32_t gpu_index) {
 // ----------------------------------------------------------------------------------------
 uint32_t concrete_hip_abi_version(void) { return 1u; }
 const char* concrete_hip_last_error(void) { return last_error(); }
+int concrete_hip_device_status(uint32_t gpu_index) { return take_device_status((int)gpu_index); }
+
+void concrete_hip_set_spin_limit(uint32_t polls) {
+  g_spin_limit.store(polls ? polls : DEFAULT_SPIN_LIMIT, std::memory_order_relaxed);
+}
+
 int concrete_hip_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -218,7 +277,8 @@ int concrete_hip_pbs(void* stream, uint32_t gpu_index, uint64_t* lwe_array_out, 
             level_count,
             default_limbs(glwe_dimension, polynomial_size, level_count),
             num_samples,
-            (unsigned long long*)resid_bits};
+            (unsigned long long*)resid_bits,
+            sync_guard((int)gpu_index)};
   return pbs_launch(a);
 }
 
@@ -314,12 +374,27 @@ void cuda_programmable_bootstrap_lwe_ciphertext_vector_64(
     set_error("num_many_lut=%u lut_stride=%u (only 1, 1 is used by the runtime)", num_many_lut, lut_stride);
     die("cuda_programmable_bootstrap_lwe_ciphertext_vector_64");
   }
-  const void* f = concrete_hip_lookup_bsk(bootstrapping_key);
-  if (!f) {
+  KeyEntry e{};
+  {
+    std::lock_guard<std::mutex> g(g_keys_mu);
+    auto it = g_keys.find(bootstrapping_key);
+    if (it != g_keys.end()) e = it->second;
+  }
+  if (!e.fourier) {
     set_error("bootstrapping key %p was not converted by cuda_convert_lwe_programmable_bootstrap_key_64",
               bootstrapping_key);
     die("cuda_programmable_bootstrap_lwe_ciphertext_vector_64");
   }
+  // the device format follows the conversion's (n, k, l, N): a call with other parameters would
+  // read past the key or reinterpret its layout
+  if (e.n != lwe_dimension || e.k != glwe_dimension || e.level != level_count || e.N != polynomial_size ||
+      e.gpu != gpu_index) {
+    set_error("bootstrapping key converted for n=%u k=%u level=%u N=%u on gpu %u, called with n=%u k=%u level=%u "
+              "N=%u on gpu %u",
+              e.n, e.k, e.level, e.N, e.gpu, lwe_dimension, glwe_dimension, level_count, polynomial_size, gpu_index);
+    die("cuda_programmable_bootstrap_lwe_ciphertext_vector_64");
+  }
+  const void* f = e.fourier;
   if (concrete_hip_pbs(stream, gpu_index, (uint64_t*)lwe_array_out, (const uint64_t*)lwe_output_indexes,
                        (const uint64_t*)lut_vector, (const uint64_t*)lut_vector_indexes,
                        (const uint64_t*)lwe_array_in, (const uint64_t*)lwe_input_indexes, f, lwe_dimension,

@@ -23,6 +23,17 @@ namespace chip {
 void set_error(const char* fmt, ...);
 const char* last_error();
 
+// Sticky per-device status word written by the PBS kernels, read back at synchronisation points
+// (cuda_synchronize_device, concrete_hip_device_status, the runtime's batch completion).
+constexpr uint32_t DEV_STATUS_SYNC_TIMEOUT = 1u;  // a wave-pair/quad sync spin hit its bound
+constexpr uint32_t DEFAULT_SPIN_LIMIT = 1u << 22;  // LDS-counter polls (~s_sleep 1 each) before giving up
+struct SyncGuard {
+  uint32_t* status;     // device word, OR-ed with DEV_STATUS_* bits
+  uint32_t spin_limit;  // polls before a sync spin gives up and flags DEV_STATUS_SYNC_TIMEOUT
+};
+SyncGuard sync_guard(int gpu);       // abi.hip: lazily allocated per device
+int take_device_status(int gpu);     // abi.hip: synchronises the device, returns and clears the word
+
 // Torus helpers -------------------------------------------------------------------------
 __host__ __device__ __forceinline__ uint32_t modswitch(uint64_t x, int log2_2n) {
   // pbs_modulus_switch (tfhe 0.10) == simulation.cpp:64-75: round(x * 2N / 2^64) mod 2N
@@ -41,6 +52,17 @@ __device__ __forceinline__ int32_t decomp_next(uint64_t& state, int logB) {
   uint64_t carry = (((res - 1ull) | state) & res) >> (logB - 1);
   state += carry;
   return (int32_t)(int64_t)(res - (carry << logB));
+}
+
+// full-width digit (any base_log < 64; a balanced digit may be +2^(logB-1), so int32 is not enough
+// past logB = 31)
+__device__ __forceinline__ int64_t decomp_next64(uint64_t& state, int logB) {
+  const uint64_t mask = (1ull << logB) - 1ull;
+  uint64_t res = state & mask;
+  state >>= logB;
+  uint64_t carry = (((res - 1ull) | state) & res) >> (logB - 1);
+  state += carry;
+  return (int64_t)(res - (carry << logB));
 }
 
 // same recurrence on a 32-bit state (valid when level * base_log <= 31)

@@ -5,6 +5,8 @@
 
 #include <type_traits>
 
+#include "common.hpp"
+
 namespace chip {
 
 // compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
@@ -24,12 +26,19 @@ constexpr uint64_t RND_MAGIC_BITS = 0x4338000000000000ull;
 // no vmcnt drain (key loads may stay in flight).
 __device__ __forceinline__ void pair_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// Bounded spin on an LDS counter: returns once *ctr >= target.  The bound (~2^22 polls, far
-// beyond any legitimate wait) turns a synchronisation bug into wrong results instead of a hung
-// GPU.
-__device__ __forceinline__ void spin_until_ge(const uint32_t* ctr, uint32_t target) {
-  for (uint32_t it = 0; it < (1u << 22); ++it) {
+// Bounded spin on an LDS counter: returns once *ctr >= target.  A wave that polls more than
+// guard.spin_limit times (default ~2^22 polls, far beyond any legitimate wait) stops waiting so a
+// synchronisation bug cannot hang the GPU, and flags DEV_STATUS_SYNC_TIMEOUT in the device status
+// word (a vector atomic): the results of that launch are then wrong, and the host reports it at
+// the next synchronisation point (cuda_synchronize_device aborts, concrete_hip_device_status
+// returns an error).
+__device__ __forceinline__ void spin_until_ge(const uint32_t* ctr, uint32_t target, const SyncGuard& guard) {
+  for (uint32_t it = 0;; ++it) {
     if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+    if (it >= guard.spin_limit) {
+      __hip_atomic_fetch_or(guard.status, DEV_STATUS_SYNC_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
     __builtin_amdgcn_s_sleep(1);
   }
   asm volatile("" ::: "memory");

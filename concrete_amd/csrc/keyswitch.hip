@@ -10,6 +10,7 @@
 // is read once per tile with 2 KB coalesced loads and applied to all KS_TILE samples, so
 // the 20.7 MB (cfg2) key is streamed B / KS_TILE times instead of B times.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.hpp"
 #include "pbs.hpp"
@@ -45,8 +46,11 @@ __global__ void __launch_bounds__(KS_THREADS)
 keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx, const uint64_t* __restrict__ in,
                  const uint64_t* __restrict__ in_idx, const uint64_t* __restrict__ ksk, uint32_t n_in,
                  uint32_t n_out, uint32_t base_log, uint32_t level, uint32_t num_samples, uint32_t i_per_split) {
-  // digits sample-minor: the KS_TILE digits of one (position, level) are two 16-byte reads
-  __shared__ __attribute__((aligned(16))) int32_t dig[KS_ICHUNK][KS_MAX_L][KS_TILE];
+  // digits sample-minor: the KS_TILE digits of one (position, level) are two 16-byte reads.
+  // The chunked paths need |d| <= 2^(logB-1) small anyway (int32); the 64-bit path keeps int64
+  // digits, so any base_log with level * base_log < 64 is exact (a balanced digit can be +2^31).
+  using dig_t = typename std::conditional<NCH == 0, int64_t, int32_t>::type;
+  __shared__ __attribute__((aligned(16))) dig_t dig[KS_ICHUNK][KS_MAX_L][KS_TILE];
   const uint32_t s0 = blockIdx.x * KS_TILE;
   const int tid = threadIdx.x;
   const uint32_t W = n_out + 1;
@@ -67,7 +71,7 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
       uint64_t a = 0ull;
       if (smp < num_samples && i < i_end) a = in[(in_idx ? in_idx[smp] : smp) * (uint64_t)(n_in + 1) + i];
       uint64_t st = decomp_init(a, nrep);
-      for (uint32_t t = 0; t < level; ++t) dig[ii][t][s] = decomp_next(st, (int)base_log);
+      for (uint32_t t = 0; t < level; ++t) dig[ii][t][s] = (dig_t)decomp_next64(st, (int)base_log);
     }
     __syncthreads();
     const uint32_t iend = min(KS_ICHUNK, (int)(i_end - i0));
@@ -127,7 +131,7 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
             const uint32_t j = tid + u * KS_THREADS;
             const uint64_t kv = j < W ? row[j] : 0ull;
 #pragma unroll
-            for (int s = 0; s < KS_TILE; ++s) acc[s][u] -= (uint64_t)(int64_t)dig[ii][t][s] * kv;
+            for (int s = 0; s < KS_TILE; ++s) acc[s][u] -= (uint64_t)dig[ii][t][s] * kv;
           }
         }
       }
@@ -169,10 +173,13 @@ int keyswitch_launch(const KsArgs& a) {
     hipLaunchKernelGGL(keyswitch_zero_kernel, dim3((uint32_t)std::min<uint64_t>((total + 255) / 256, 4096)), dim3(256),
                        0, a.stream, a.out, a.out_idx, a.n_out + 1, a.num_samples);
   }
-  // int32 chunk sums of one block: FP level 2^(logB-1) (max chunk) < 2^31
-  const uint64_t dmax = (1ull << (a.base_log - 1)) * a.level;
-  const int nch = 16ull * dmax * ((1ull << 22) - 1) < (1ull << 31) ? 3
-                  : (uint64_t)KS_ICHUNK * dmax * 65535ull < (1ull << 31) ? 4 : 0;
+  // int32 chunk sums of one block: FP * dmax * (max chunk) <= 2^31 - 1 with dmax = l 2^(logB-1)
+  // (the largest digit row sum): 3 chunks (<= 22 bits, FP = 16) when dmax <= 32, 4 chunks
+  // (16 bits, FP = 32) when dmax <= 1024, else the 64-bit products.  Compared by division so
+  // nothing overflows for any accepted base_log.
+  const uint64_t dmax = a.base_log - 1 >= 40 ? ~0ull : (1ull << (a.base_log - 1)) * a.level;
+  const int nch = dmax <= 0x7fffffffull / (16ull * ((1ull << 22) - 1)) ? 3
+                  : dmax <= 0x7fffffffull / ((uint64_t)KS_ICHUNK * 65535ull) ? 4 : 0;
 #define KS_LAUNCH2(UU, CH)                                                                                         \
   if (splits > 1)                                                                                                  \
     hipLaunchKernelGGL((keyswitch_kernel<UU, true, CH>), dim3(blocks, splits), dim3(KS_THREADS), 0, a.stream,     \

@@ -57,17 +57,17 @@ constexpr int limb_shift(int li) { return li * 21 + (li > 0 ? 1 : 0); }
 // Only LDS traffic is drained (lgkmcnt), never the key DMA (no release fence: that would add
 // vmcnt(0)).  LDS operations are coherent across the waves of a CU.
 // (DIAG_NOXBAR: timing-only builds without any exchange synchronisation.)
-__device__ __forceinline__ void xchg_barrier(uint32_t* flags, int w, uint32_t& cnt) {
+__device__ __forceinline__ void xchg_barrier(uint32_t* flags, int w, uint32_t& cnt, const SyncGuard& guard) {
 #if defined(DIAG_NOXBAR)
-  (void)flags, (void)w, (void)cnt;
+  (void)flags, (void)w, (void)cnt, (void)guard;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #elif PAIR_FLAGS
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   ++cnt;
   __hip_atomic_store(&flags[w], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  spin_until_ge(&flags[w ^ 1], cnt);
+  spin_until_ge(&flags[w ^ 1], cnt, guard);
 #else
-  (void)flags, (void)w, (void)cnt;
+  (void)flags, (void)w, (void)cnt, (void)guard;
   pair_barrier();
 #endif
 }
@@ -78,7 +78,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
                     const uint64_t* __restrict__ luts, const uint64_t* __restrict__ lut_idx,
                     const uint64_t* __restrict__ in, const uint64_t* __restrict__ in_idx,
                     const cplx* __restrict__ fbsk, uint32_t n, uint32_t base_log, uint32_t num_samples,
-                    unsigned long long* __restrict__ resid_out) {
+                    unsigned long long* __restrict__ resid_out, SyncGuard guard) {
   constexpr int K = 1, K1 = 2, N = 1024, LOG2_2N = 11, LIMBS = 3, RQ = K1 * L;
   constexpr int PER_I = K1 * LIMBS * RQ * 512;  // complex values per Fourier GGSW
   static_assert(XCH_SLOTS <= (int)PBS1024_XCH_SLOTS, "transpose scratch");
@@ -228,7 +228,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
             for (int j = 0; j < 4; ++j) mybox[(t * 4 + j) * 64 + lane] = out[t][j];
       }
-      xchg_barrier(pflags, w, pcnt);
+      xchg_barrier(pflags, w, pcnt, guard);
       if (work) {
 #pragma unroll
         for (int t = 0; t < XB; ++t)
@@ -238,7 +238,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
       }
       // partner has read my mailbox before my next transform writes the scratch; after the last
       // batch the scratch is next written behind the key windows' workgroup barriers
-      if (q0 + XB < L) xchg_barrier(pflags, w, pcnt);
+      if (q0 + XB < L) xchg_barrier(pflags, w, pcnt, guard);
     }
     if constexpr (STAMPS) {
       uint64_t t = stamp();
@@ -380,7 +380,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         acc_t[2] += t - tp;
         tp = t;
       }
-      xchg_barrier(pflags, w, pcnt);
+      xchg_barrier(pflags, w, pcnt, guard);
       // my output polynomial's spectrum, slots in order k2 ^ 4h (undone by the inverse pass 1)
       cplx vp[8];
       if (work) {
@@ -463,7 +463,8 @@ static int launch_pair_t(const PbsArgs& a) {
   CHIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const uint32_t blocks = (a.num_samples + PBS_PAIRS - 1) / PBS_PAIRS;
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(PBS_PAIRS * 128), lds, a.stream, a.out, a.out_idx, a.luts, a.lut_idx,
-                     a.in, a.in_idx, reinterpret_cast<const cplx*>(a.fbsk), a.n, a.base_log, a.num_samples, a.resid);
+                     a.in, a.in_idx, reinterpret_cast<const cplx*>(a.fbsk), a.n, a.base_log, a.num_samples, a.resid,
+                     a.guard);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("pbs launch failed: %s", hipGetErrorString(e));

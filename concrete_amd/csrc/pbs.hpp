@@ -98,6 +98,7 @@ struct PbsArgs {
   const void* fbsk;
   uint32_t n, k, N, base_log, level, limbs, num_samples;
   unsigned long long* resid;  // optional: max |x - round(x)| over all outputs (f64 bits)
+  SyncGuard guard;            // device status word + spin bound of the wave-pair/quad syncs
 };
 
 int pbs_launch(const PbsArgs& a);

@@ -34,12 +34,12 @@ constexpr uint64_t P2_MAGIC_ALL =
 // ciphertext of the workgroup): each wave publishes how many sync points it has passed and
 // waits until its three partners have reached the same count.  LDS traffic is drained, the
 // key DMA is not.
-__device__ __forceinline__ void quad_sync(uint32_t* flags, int ctl, int v, uint32_t& cnt) {
+__device__ __forceinline__ void quad_sync(uint32_t* flags, int ctl, int v, uint32_t& cnt, const SyncGuard& guard) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   ++cnt;
   __hip_atomic_store(&flags[ctl * 4 + v], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
-  for (int o = 1; o < 4; ++o) spin_until_ge(&flags[ctl * 4 + ((v + o) & 3)], cnt);
+  for (int o = 1; o < 4; ++o) spin_until_ge(&flags[ctl * 4 + ((v + o) & 3)], cnt, guard);
 }
 
 template <bool RESID>
@@ -48,7 +48,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
                     const uint64_t* __restrict__ luts, const uint64_t* __restrict__ lut_idx,
                     const uint64_t* __restrict__ in, const uint64_t* __restrict__ in_idx,
                     const cplx* __restrict__ fbsk, uint32_t n, uint32_t base_log, uint32_t num_samples,
-                    unsigned long long* __restrict__ resid_out) {
+                    unsigned long long* __restrict__ resid_out, SyncGuard guard) {
   constexpr int N = 2048, LOG2_2N = 12, K1 = 2;
   constexpr int NW = 4 * PBS2_CTS;                          // waves per workgroup
   constexpr int GROUP = 2 * 512;                            // (limb, col, row, sub): parity e and o spectra
@@ -144,7 +144,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
       for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = A[m];
     }
-    quad_sync(qflags, ctl, v, qcnt);
+    quad_sync(qflags, ctl, v, qcnt, guard);
     if (work) {
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
@@ -155,7 +155,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         st[m] = (uint32_t)decomp_init((sp < N ? rv : 0ull - rv) - A[m], nrep);
       }
     }
-    quad_sync(qflags, ctl, v, qcnt);  // every wave has read its sources: scratches are free again
+    quad_sync(qflags, ctl, v, qcnt, guard);  // every wave has read its sources: scratches are free again
 
     // ---- one decomposition level, two sub-digit polynomials, forward transforms ----------
     // X[vv][sub][jj]: spectrum of sub-digit polynomial (virtual poly vv = 2 row + parity) at
@@ -182,7 +182,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
         for (int k2 = 0; k2 < 8; ++k2) xch[k2 * 64 + lane] = vv8[k2];
       }
-      quad_sync(qflags, ctl, v, qcnt);
+      quad_sync(qflags, ctl, v, qcnt, guard);
       if (work) {
 #pragma unroll
         for (int vv = 0; vv < 4; ++vv)
@@ -191,7 +191,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
       }
       // everyone has read my spectrum before my next transform writes the scratch; after the
       // last sub-digit the scratches are next written behind the key windows' barriers
-      if (sub + 1 < PBS2_SUBS) quad_sync(qflags, ctl, v, qcnt);
+      if (sub + 1 < PBS2_SUBS) quad_sync(qflags, ctl, v, qcnt, guard);
     }
 
     // ---- per limb: MAC for the four outputs on my quarter, trade quarters, inverse ---------
@@ -250,7 +250,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) ctxw[vo * XS + (v * 2 + jj) * 64 + lane] = Y[vo >> 1][vo & 1][jj];
       }
-      quad_sync(qflags, ctl, v, qcnt);
+      quad_sync(qflags, ctl, v, qcnt, guard);
       if (work) {
 #pragma unroll
         for (int vv = 0; vv < 4; ++vv)
@@ -311,7 +311,8 @@ static int launch2048_t(const PbsArgs& a) {
   CHIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const uint32_t blocks = (a.num_samples + PBS2_CTS - 1) / PBS2_CTS;
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(PBS2_CTS * 256), lds, a.stream, a.out, a.out_idx, a.luts, a.lut_idx,
-                     a.in, a.in_idx, reinterpret_cast<const cplx*>(a.fbsk), a.n, a.base_log, a.num_samples, a.resid);
+                     a.in, a.in_idx, reinterpret_cast<const cplx*>(a.fbsk), a.n, a.base_log, a.num_samples, a.resid,
+                     a.guard);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("pbs launch failed: %s", hipGetErrorString(e));

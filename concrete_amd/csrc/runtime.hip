@@ -143,6 +143,10 @@ void finish(std::vector<Slice>& slices) {
     CHIP_CHECK(hipStreamSynchronize(sl.s));
     CHIP_CHECK(hipStreamDestroy(sl.s));
   }
+  // a PBS whose wave synchronisation gave up produced wrong outputs: abort, as the reference's
+  // wrappers do on any backend failure
+  for (auto& sl : slices)
+    if (take_device_status((int)sl.gpu) != 0) die(concrete_hip_last_error());
 }
 
 std::vector<Slice> make_slices(concrete_hip_keyset* ks, uint64_t num_samples) {
@@ -167,6 +171,13 @@ void run_batched_pbs(uint64_t* out, const uint64_t* ct0, uint64_t num_samples, c
                      uint64_t num_luts, uint32_t n, uint32_t N, uint32_t level, uint32_t base_log, uint32_t k,
                      uint32_t bsk_index, concrete_hip_keyset* ks) {
   if (num_samples == 0) return;
+  {
+    // the registered key must have the call's parameters: its device format (and size) follows
+    // them, so a mismatch would read past the key or reinterpret its layout
+    BskEntry* e = entry(ks->bsk, bsk_index, ks->m, false);
+    if (!e) die("bootstrap key index not registered");
+    RT_ASSERT(e->n == n && e->k == k && e->N == N && e->level == level && e->base_log == base_log);
+  }
   const uint64_t in_w = n + 1, out_w = (uint64_t)k * N + 1, glwe = (uint64_t)(k + 1) * N;
   auto slices = make_slices(ks, num_samples);
   for (auto& sl : slices) {

@@ -147,9 +147,20 @@ int concrete_hip_keyswitch(void *stream, uint32_t gpu_index, uint64_t *lwe_array
 const void *concrete_hip_lookup_bsk(const void *bootstrapping_key);
 /* number of visible devices */
 int concrete_hip_device_count(void);
+/* Synchronise the device and return (and clear) its sticky status: 0 ok, -4 when a PBS kernel's
+ * wave synchronisation gave up after its spin bound since the last check (that launch's outputs
+ * are wrong).  cuda_synchronize_device performs the same check and aborts. */
+int concrete_hip_device_status(uint32_t gpu_index);
+/* Spin bound (LDS-counter polls) of the PBS kernels' wave synchronisation for later launches;
+ * 0 restores the default (2^22).  Test hook: a tiny bound forces the timeout path. */
+void concrete_hip_set_spin_limit(uint32_t polls);
 
 /* ------------------------------------------------------------------------------------------
- * Part 3: client-side helpers (host code; synthetic workloads and LUT encoding).  Mirrors the
+ * Part 3: client-side helpers (host code; synthetic workloads and LUT encoding).
+ * INSECURE — FOR TESTS AND BENCHMARKS ONLY: keys, masks and noise come from xoshiro256** seeded
+ * with the caller's 64-bit seed (Box-Muller Gaussians), not from a CSPRNG; reusing a seed reuses
+ * the encryption masks.  Real key material comes from the reference's client (concrete-csprng).
+ * Mirrors the
  * concrete-cpu client ABI (backends/concrete-cpu/implementation/include/concrete-cpu.h:
  * concrete_cpu_init_secret_key_u64, concrete_cpu_encrypt_lwe_ciphertext_u64,
  * concrete_cpu_init_lwe_bootstrap_key_u64, concrete_cpu_init_lwe_keyswitch_key_u64) and the

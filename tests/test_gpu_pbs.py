@@ -326,12 +326,15 @@ def test_keyswitch_bit_exact_and_chain(B, oracle, cfg2, torch_cuda):
         assert [B.decode(d, width) for d in dec] == c["expected"], c["description"]
 
 
-@pytest.mark.parametrize("ks_l,ks_logB", [(4, 3), (6, 6), (2, 10), (2, 11), (1, 20)])
+@pytest.mark.parametrize("ks_l,ks_logB", [(4, 3), (7, 3), (3, 4), (4, 4), (6, 6), (2, 10), (2, 11), (1, 20),
+                                          (2, 31), (1, 40)])
 def test_keyswitch_decompositions(B, oracle, torch_cuda, ks_l, ks_logB):
-    """The keyswitch's two product paths (keyswitch.hip): 16-bit key chunks with int32 block sums
-    when 32 l 2^(logB-1) (2^16 - 1) < 2^31 ((4,3), (6,6), and (2,10) at the edge), the 64-bit
-    products otherwise ((2,11), (1,20)); random inputs, 37 samples (a partial tile), bit-exact vs
-    the oracle."""
+    """The keyswitch's three product paths (keyswitch.hip), selected by dmax = l 2^(logB-1):
+    three 22/21/21-bit key chunks with int32 sums over 16-position blocks when dmax <= 32 ((4,3),
+    (7,3), (3,4), and (4,4) at the edge), four 16-bit chunks over 32-position blocks when
+    dmax <= 1024 ((6,6), and (2,10) at the edge), the 64-bit products with int64 digits otherwise
+    ((2,11), (1,20), and (2,31), (1,40) where a balanced digit can reach +2^31 or beyond); random
+    inputs, 37 samples (a partial tile), bit-exact vs the oracle."""
     p = replace(B.CFG2, ks_level=ks_l, ks_base_log=ks_logB)
     glwe_sk = B.binary_key(p.big_n, 8100 + ks_logB)
     lwe_sk = B.binary_key(p.n, 8200 + ks_logB)
@@ -365,3 +368,28 @@ def test_configs2_total_batch_65536(B, oracle, cfg2, torch_cuda):
     pick = rng.choice(nb, size=8, replace=False)
     ref = run_oracle(oracle, cfg2, cts[pick], acc)
     assert np.array_equal(got[pick], ref)
+
+
+def test_sync_timeout_is_reported(B, oracle, cfg2, torch_cuda):
+    """A wave-pair synchronisation that exceeds its spin bound is reported, not silent
+    (kernel_util.hpp spin_until_ge): with the bound forced to one poll some sync of a
+    512-sample batch gives up, concrete_hip_device_status returns -4 (and clears); with the
+    default bound the same batch runs clean and bit-exact."""
+    width = 3
+    rng = np.random.RandomState(31)
+    table = rng.randint(0, 8, size=8)
+    msgs = rng.randint(0, 8, size=512)
+    cts = encrypt(B, cfg2, msgs, width, 3131)
+    acc = lut_acc(B, cfg2, table, width)
+    assert B.device_status("cuda:0") == 0
+    try:
+        B.set_spin_limit(1)
+        run_gpu(B, cfg2, cts, acc, torch_cuda)
+        assert B.device_status("cuda:0") == -4
+        assert "spin bound" in B._native.lib().concrete_hip_last_error().decode()
+    finally:
+        B.set_spin_limit(0)
+    assert B.device_status("cuda:0") == 0  # cleared
+    got = run_gpu(B, cfg2, cts[:16], acc, torch_cuda)
+    assert B.device_status("cuda:0") == 0
+    assert np.array_equal(got, run_oracle(oracle, cfg2, cts[:16], acc))

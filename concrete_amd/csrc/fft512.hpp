@@ -1,18 +1,35 @@
 // fft512.hpp — one-wavefront 512-point complex FFT for the N = 1024 negacyclic product.
 //
 // One wave64 owns one polynomial: lane t holds 8 complex points (16 f64 registers).
-// 512 = 8 x 8 x 8: three in-register radix-8 passes, two intra-wave LDS transposes.
-// Forward (DIF, natural in -> digit-permuted out):
+// 512 = 8 x 8 x 8: three in-register radix-8 passes, two intra-wave transposes (lane bits 3..5
+// in registers, lane bits 0..2 through LDS).
+// Forward (natural in -> digit-permuted out):
 //   in : lane t holds x[t + 64 m], m = 0..7 (untwisted: the negacyclic twist is folded in)
 //   out: lane (k0 = t>>3, k1 = t&7) holds Z[k0 + 8 k1 + 64 k2], k2 = 0..7, where
 //        Z = DFT_512(x_j * zeta^j), zeta = exp(i pi / 1024), DFT sign exp(-2 pi i jk / 512)
-// Inverse (the transposed DIT, conjugate twiddles, unnormalised) maps that layout back and
-// applies conj(zeta^j), so inverse(forward(x)) = 512 x.
+// Inverse (conjugate twiddles, unnormalised) maps that layout back and applies conj(zeta^j),
+// so inverse(forward(x)) = 512 x.
 // The pointwise product never needs natural frequency order, so no reordering pass exists.
 //
-// Twist folding: zeta^{t + 64 m} = zeta^t * psi^m with psi = zeta^64 = exp(i pi / 16).  psi^m
-// (8 constants) multiplies the pass-1 inputs; zeta^t is merged into the pass-1 output twiddle,
-// giving one per-lane table T1[k0][t] = zeta^t * w512^{t k0} used by both directions.
+// Forward passes as geometric DFTs.  With j = t0 + 8 t1 + 64 m and f = k0 + 8 k1 + 64 k2,
+//   Z_f = sum_t0 rho3^t0 w8^{t0 k2} sum_t1 rho2^t1 w8^{t1 k1} sum_m psi^m w8^{m k0} x_j
+//   psi = zeta^64,  rho2 = zeta^8 w64^{k0},  rho3 = zeta w512^{k0 + 8 k1}
+// i.e. every pass is an 8-point DFT of x_e rho^e ("geometric" input twiddles, rho depending on
+// the pass and the lane) and there is no separate twiddle multiplication at all.  A geometric
+// DFT8 runs as three radix-2 DIT stages of fused butterflies a +- W b with
+// W = c (1 + i t), t = tan(arg W) (Goedecker, "Fast radix 2, 3, 4 and 5 kernels for FFT on
+// computers with overlapping multiply-add instructions", 1997): 6 FMAs per butterfly, 72 per
+// pass, against 56 + 28 for an 8-point DFT plus its seven twiddle products.  The stage
+// twiddles are rho^4, rho^2, rho and rho w8 (the (-i) multiples are free relabelings), read as
+// (c, t) pairs from LDS (pass 1: compile-time constants).
+// Inverse: pass 1 is a plain 8-point DFT over k2, pass 2 the geometric DFT over k1 with
+// rho = conj(w64^{t0}), and pass 3 keeps the classic form (twiddles conj(zeta^t w512^{t k0}),
+// 8-point DFT over k0, output twist conj(psi^m)), because its conj(zeta^j) twist sits on the
+// OUTPUT side, where a twiddle cannot be fused into a butterfly.
+//
+// Rounding: |computed Wb - Wb| <= (|c| + |s|) u |b| + the table error, i.e. a butterfly's error
+// stays within Higham's radix-2 model (Accuracy and Stability, Thm 24.2) that the certified
+// bound of DESIGN.md §3 / oracle ora_fft_error_bound uses (mu ~ 2u against gamma doubled).
 //
 // LDS transpose slot (complex index within the wave's 575-slot / 9.2 KB scratch):
 //   S(a, b, c) = 72 a + 9 b + c
@@ -46,59 +63,100 @@ __device__ __forceinline__ cplx mul_mi(cplx a) {
   if constexpr (INV) return {-a.im, a.re};
   else return {a.im, -a.re};
 }
-// a * w8^1 with w8 = exp(-+ i pi/4)
-template <bool INV>
-__device__ __forceinline__ cplx mul_w8(cplx a) {
-  constexpr double r = 0.70710678118654752440084436210485;
-  if constexpr (INV) return {(a.re - a.im) * r, (a.re + a.im) * r};
-  else return {(a.re + a.im) * r, (a.im - a.re) * r};
-}
-// a * w8^3
-template <bool INV>
-__device__ __forceinline__ cplx mul_w83(cplx a) {
-  constexpr double r = 0.70710678118654752440084436210485;
-  if constexpr (INV) return {(-a.re - a.im) * r, (a.re - a.im) * r};
-  else return {(a.im - a.re) * r, (-a.re - a.im) * r};
-}
 
 // Negate a complex value when `sign` is 1ull << 63 (sign-bit XOR on both parts, no branch).
 __device__ __forceinline__ cplx cneg_if(cplx a, uint64_t sign) {
   return {__longlong_as_double((long long)((uint64_t)__double_as_longlong(a.re) ^ sign)),
           __longlong_as_double((long long)((uint64_t)__double_as_longlong(a.im) ^ sign))};
 }
+__device__ __forceinline__ double dneg_if(double a, uint64_t sign) {
+  return __longlong_as_double((long long)((uint64_t)__double_as_longlong(a) ^ sign));
+}
 
-// In-register 8-point DFT, natural order in and out: X[k] = sum_m x[m] w8^{+-mk}.
-// Uniform relabelings used by the wave of a pair that owns the upper frequency half
-// (sign = 1ull << 63, else 0):
-//   OUT_XOR4: outputs permuted k -> k ^ 4 (negate b1, b3, b5, b7 before the last stage);
-//   IN_XOR4:  inputs given in order m ^ 4 (the DFT of the permuted input is (-1)^k X[k]:
-//             negate b4..b7, the terms of the odd outputs).
-template <bool INV, int RELABEL = 0>
+// In-register 8-point DFT, natural order in and out: X[k] = sum_m x[m] w8^{+-mk}.  The two
+// w8^{1,3} products are fused into the last stage's additions (FMAs with 1/sqrt2): 52 f64
+// operations.  IN_XOR4 (sign = 1ull << 63, else 0): inputs given in order m ^ 4 — the DFT of
+// the permuted input is (-1)^k X[k], i.e. the terms of the odd outputs are negated (used by the
+// wave of a pair that owns the upper frequency half).
+template <bool INV, bool IN_XOR4 = false>
 __device__ __forceinline__ void dft8(cplx (&v)[8], uint64_t sign = 0) {
+  const double r = dneg_if(0.70710678118654752440084436210485, IN_XOR4 ? sign : 0ull);
   cplx a0 = cadd(v[0], v[4]), a4 = csub(v[0], v[4]);
   cplx a1 = cadd(v[1], v[5]), a5 = csub(v[1], v[5]);
   cplx a2 = cadd(v[2], v[6]), a6 = csub(v[2], v[6]);
   cplx a3 = cadd(v[3], v[7]), a7 = csub(v[3], v[7]);
-  a5 = mul_w8<INV>(a5);
   a6 = mul_mi<INV>(a6);
-  a7 = mul_w83<INV>(a7);
+  // w8 a5 = r p5, w8^3 a7 = r p7
+  cplx p5, p7;
+  if constexpr (INV) {
+    p5 = {a5.re - a5.im, a5.re + a5.im};
+    p7 = {-a7.re - a7.im, a7.re - a7.im};
+  } else {
+    p5 = {a5.re + a5.im, a5.im - a5.re};
+    p7 = {a7.im - a7.re, -a7.re - a7.im};
+  }
+  const cplx q = cadd(p5, p7), qq = mul_mi<INV>(csub(p5, p7));  // b5 = r q, b7 = r qq
   cplx b0 = cadd(a0, a2), b2 = csub(a0, a2);
   cplx b1 = cadd(a1, a3), b3 = mul_mi<INV>(csub(a1, a3));
   cplx b4 = cadd(a4, a6), b6 = csub(a4, a6);
-  cplx b5 = cadd(a5, a7), b7 = mul_mi<INV>(csub(a5, a7));
-  if constexpr (RELABEL == 1) {  // OUT_XOR4
-    b1 = cneg_if(b1, sign), b3 = cneg_if(b3, sign), b5 = cneg_if(b5, sign), b7 = cneg_if(b7, sign);
-  } else if constexpr (RELABEL == 2) {  // IN_XOR4
-    b4 = cneg_if(b4, sign), b5 = cneg_if(b5, sign), b6 = cneg_if(b6, sign), b7 = cneg_if(b7, sign);
-  }
+  if constexpr (IN_XOR4) b4 = cneg_if(b4, sign), b6 = cneg_if(b6, sign);
   v[0] = cadd(b0, b1);
   v[4] = csub(b0, b1);
   v[2] = cadd(b2, b3);
   v[6] = csub(b2, b3);
-  v[1] = cadd(b4, b5);
-  v[5] = csub(b4, b5);
-  v[3] = cadd(b6, b7);
-  v[7] = csub(b6, b7);
+  v[1] = {__builtin_fma(r, q.re, b4.re), __builtin_fma(r, q.im, b4.im)};
+  v[5] = {__builtin_fma(-r, q.re, b4.re), __builtin_fma(-r, q.im, b4.im)};
+  v[3] = {__builtin_fma(r, qq.re, b6.re), __builtin_fma(r, qq.im, b6.im)};
+  v[7] = {__builtin_fma(-r, qq.re, b6.re), __builtin_fma(-r, qq.im, b6.im)};
+}
+
+// Fused radix-2 butterfly (a, b) <- (a + W' b, a - W' b), W = c (1 + i t), W' = W (ROT 0),
+// -i W (ROT 1) or +i W (ROT 2): W b = c (u + i v), u = b.re - t b.im, v = b.im + t b.re.
+template <int ROT>
+__device__ __forceinline__ void gbf(cplx& a, cplx& b, double c, double t) {
+  const double u = __builtin_fma(-t, b.im, b.re);
+  const double v = __builtin_fma(t, b.re, b.im);
+  double pr, pi;
+  if constexpr (ROT == 0) pr = u, pi = v;
+  else if constexpr (ROT == 1) pr = v, pi = -u;
+  else pr = -v, pi = u;
+  const cplx y0 = {__builtin_fma(c, pr, a.re), __builtin_fma(c, pi, a.im)};
+  const cplx y1 = {__builtin_fma(-c, pr, a.re), __builtin_fma(-c, pi, a.im)};
+  a = y0;
+  b = y1;
+}
+
+// Geometric 8-point DFT: y[k] = sum_e x[e] rho^e w^{ek}, w = exp(-+ i pi / 4) (forward /
+// inverse), natural order in and out.  tw[0..3] = (c, t) of rho^4, rho^2, rho, rho w (stored as
+// cplx {c, t}).  Stages: e ^ 4 pairs with rho^4; e ^ 2 pairs with rho^2 (k even) or w^2 rho^2
+// (k odd); e ^ 1 pairs with rho w^{k mod 4}.  out_sign = 1ull << 63 emits y[k ^ 4] in slot k (the
+// sign of the last stage's twiddles; OUT_XOR4 relabeling of the upper-half wave).
+// CS4: tw[0] holds (cos, sin) of rho^4 instead of (c, t) and the first stage multiplies in full
+// (the inverse pass 2, whose rho^4 = exp(i pi t0 / 8) is exactly i at t0 = 4: no tangent).
+template <bool INV, bool CS4 = false>
+__device__ __forceinline__ void geo8(cplx (&v)[8], const cplx (&tw)[4], uint64_t out_sign = 0) {
+  constexpr int R = INV ? 2 : 1;  // w^2 = -i (forward) or +i (inverse)
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if constexpr (CS4) {
+      const cplx wb = cmul(v[e + 4], tw[0]);
+      v[e + 4] = csub(v[e], wb);
+      v[e] = cadd(v[e], wb);
+    } else {
+      gbf<0>(v[e], v[e + 4], tw[0].re, tw[0].im);
+    }
+  }
+  gbf<0>(v[0], v[2], tw[1].re, tw[1].im);
+  gbf<0>(v[1], v[3], tw[1].re, tw[1].im);
+  gbf<R>(v[4], v[6], tw[1].re, tw[1].im);
+  gbf<R>(v[5], v[7], tw[1].re, tw[1].im);
+  const double c2 = dneg_if(tw[2].re, out_sign), c3 = dneg_if(tw[3].re, out_sign);
+  gbf<0>(v[0], v[1], c2, tw[2].im);  // y0, y4
+  gbf<0>(v[4], v[5], c3, tw[3].im);  // y1, y5
+  gbf<R>(v[2], v[3], c2, tw[2].im);  // y2, y6
+  gbf<R>(v[6], v[7], c3, tw[3].im);  // y3, y7
+  const cplx y1 = v[4], y2 = v[2], y3 = v[6], y4 = v[1], y5 = v[5], y6 = v[3];
+  v[1] = y1, v[2] = y2, v[3] = y3, v[4] = y4, v[5] = y5, v[6] = y6;
 }
 
 __device__ __forceinline__ int xslot(int a, int b, int c) { return 72 * a + 9 * b + c; }
@@ -176,21 +234,47 @@ __device__ __forceinline__ cplx psi_pow(int m) {
   return {C[m], C[(8 - m) & 7] * (m == 0 ? 0.0 : 1.0)};
 }
 
-// LDS tables shared by the workgroup:
-//   T1[k0 * T1_STRIDE + t] = zeta^t * w512^{t k0}   (8 rows of 64, padded to 72 entries)
-//   T2[k1 * 8 + t0] = w64^{t0 k1}                   (64 entries, symmetric in (k1, t0))
-// The row padding makes the inverse pass-2 read T1[hi * 72 + 8 t1 + lo] conflict-free on the
-// ds_read_b128 lane groups (2-way with a 64 stride); the forward read T1[k0 * 72 + lane] stays
-// contiguous.  The inverse pass-1 read uses T2's symmetry, T2[t0 * 8 + lo], for the same reason
-// (T2[lo * 8 + t0] is 4-way conflicted).
+// LDS tables shared by the workgroup (cplx entries):
+//   T1[k0 * T1_STRIDE + t] = zeta^t * w512^{t k0}   (8 rows of 64, padded to 72 entries;
+//                                                   inverse pass-2 output twiddles, conjugated)
+//   GF2[j * 8 + k0]   (c, t) of the forward pass-2 stage twiddles, rho2 = zeta^8 w64^{k0}
+//   GF3[j * 64 + lane] (c, t) of the forward pass-3 stage twiddles, rho3 = zeta w512^{k0 + 8 k1}
+//   GI2[j * 8 + t0]   (c, t) of the inverse pass-2 stage twiddles, rho = conj(w64^{t0})
+//                     (j = 0: (cos, sin) of rho^4, which is i at t0 = 4)
+// with j = 0..3 for rho^4, rho^2, rho, rho w.  The [j][index] order keeps every read
+// conflict-free (consecutive lanes, or broadcasts of 8 distinct 16-byte entries).  The T1 row
+// padding makes the inverse pass-2 read T1[hi * 72 + 8 t1 + lo] conflict-free on the
+// ds_read_b128 lane groups (2-way with a 64 stride).
 constexpr int T1_STRIDE = 72;
-constexpr int FFT512_TABLE_ENTRIES = 8 * T1_STRIDE + 64;
+constexpr int FFT512_T1_ENTRIES = 8 * T1_STRIDE;
+constexpr int FFT512_TABLE_ENTRIES = FFT512_T1_ENTRIES + 4 * 8 + 4 * 64 + 4 * 8;
 struct Fft512Tables {
   const cplx* T1;
-  const cplx* T2;
+  const cplx* GF2;
+  const cplx* GF3;
+  const cplx* GI2;
 };
+__device__ __forceinline__ Fft512Tables fft512_tables_at(const cplx* base) {
+  return {base, base + FFT512_T1_ENTRIES, base + FFT512_T1_ENTRIES + 32, base + FFT512_T1_ENTRIES + 32 + 256};
+}
 
-__device__ __forceinline__ void build_fft512_tables(cplx* T1, cplx* T2, int tid, int nthreads) {
+// (c, t) of exp(i pi a), a in units of pi; c = cos, t = tan (never near pi/2 for the angles it is
+// used on: |cos| >= 0.012)
+__device__ __forceinline__ cplx geo_ct(double a) {
+  double s, c;
+  sincospi(a, &s, &c);
+  return {c, s / c};
+}
+// angle (units of pi) of stage twiddle j for base angle a and w8 = exp(wsign i pi / 4)
+__device__ __forceinline__ double geo_angle(int j, double a, double wsign) {
+  return j == 0 ? 4.0 * a : j == 1 ? 2.0 * a : j == 2 ? a : a + 0.25 * wsign;
+}
+
+__device__ __forceinline__ void build_fft512_tables(cplx* base, int tid, int nthreads) {
+  cplx* T1 = base;
+  cplx* GF2 = base + FFT512_T1_ENTRIES;
+  cplx* GF3 = GF2 + 32;
+  cplx* GI2 = GF3 + 256;
   for (int e = tid; e < 512; e += nthreads) {
     const int k0 = e >> 6, t = e & 63;
     double s, c;
@@ -199,36 +283,41 @@ __device__ __forceinline__ void build_fft512_tables(cplx* T1, cplx* T2, int tid,
     sincospi((double)num / 1024.0, &s, &c);
     T1[k0 * T1_STRIDE + t] = {c, s};
   }
-  for (int e = tid; e < 64; e += nthreads) {
-    const int k1 = e >> 3, t0 = e & 7;
-    double s, c;
-    sincospi(-2.0 * (double)((t0 * k1) & 63) / 64.0, &s, &c);
-    T2[e] = {c, s};
+  for (int e = tid; e < 4 * 64; e += nthreads) {
+    const int j = e >> 6, lane = e & 63, k0 = lane >> 3, k1 = lane & 7;
+    GF3[e] = geo_ct(geo_angle(j, 1.0 / 1024.0 - (double)(k0 + 8 * k1) / 256.0, -1.0));
+  }
+  for (int e = tid; e < 4 * 8; e += nthreads) {
+    const int j = e >> 3, x = e & 7;
+    GF2[e] = geo_ct(geo_angle(j, 1.0 / 128.0 - (double)x / 32.0, -1.0));
+    if (j == 0) {  // (cos, sin) of rho^4 (geo8<true, true>)
+      double s, c;
+      sincospi((double)x / 8.0, &s, &c);
+      GI2[e] = {c, s};
+    } else {
+      GI2[e] = geo_ct(geo_angle(j, (double)x / 32.0, 1.0));
+    }
   }
 }
 
 // Forward: v[m] = x[t + 64 m] (real-and-imaginary folded digits, untwisted).
-// Stages: P1 (twist, pass 1, twiddles) | W1 R1 (transpose 1) | P2 (pass 2, twiddles) | W2 R2 | P3.
-__device__ __forceinline__ void fwd_p1(cplx (&v)[8], const Fft512Tables& T, int lane) {
-#pragma unroll
-  for (int m = 1; m < 8; ++m) v[m] = cmul(v[m], psi_pow(m));
-  dft8<false>(v);
-#pragma unroll
-  for (int k0 = 0; k0 < 8; ++k0) v[k0] = cmul(v[k0], T.T1[k0 * T1_STRIDE + lane]);
+// Stages: P1 (geometric, rho = psi) | hi transpose (registers) | P2 (geometric, rho2) |
+//         W2 R2 (LDS transpose) | P3 (geometric, rho3).
+__device__ __forceinline__ void fwd_p1(cplx (&v)[8]) {
+  // (c, t) of psi^4, psi^2, psi, psi w8 with psi = exp(i pi / 16), w8 = exp(-i pi / 4)
+  const cplx tw[4] = {{0x1.6a09e667f3bcdp-1, 1.0},
+                      {0x1.d906bcf328d46p-1, 0x1.a827999fcef32p-2},
+                      {0x1.f6297cff75cb0p-1, 0x1.975f5e0553158p-3},
+                      {0x1.a9b66290ea1a3p-1, -0x1.561b82ab7f990p-1}};
+  geo8<false>(v, tw);
 }
-// transpose 1: writer lane (t1 = hi, t0 = lo) element k0 ; reader lane (k0 = hi, t0 = lo) element t1
-__device__ __forceinline__ void fwd_w1(const cplx (&v)[8], cplx* xch, int hi, int lo) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) xch[xslot(e, hi, lo)] = v[e];
+__device__ __forceinline__ void fwd_p2(cplx (&v)[8], const Fft512Tables& T, int hi) {
+  const cplx tw[4] = {T.GF2[hi], T.GF2[8 + hi], T.GF2[16 + hi], T.GF2[24 + hi]};
+  geo8<false>(v, tw);
 }
-__device__ __forceinline__ void fwd_r1(cplx (&v)[8], const cplx* xch, int hi, int lo) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = xch[xslot(hi, e, lo)];
-}
-__device__ __forceinline__ void fwd_p2(cplx (&v)[8], const Fft512Tables& T, int lo) {
-  dft8<false>(v);
-#pragma unroll
-  for (int k1 = 1; k1 < 8; ++k1) v[k1] = cmul(v[k1], T.T2[k1 * 8 + lo]);
+__device__ __forceinline__ void fwd_p3(cplx (&v)[8], const Fft512Tables& T, int lane, uint64_t out_xor4) {
+  const cplx tw[4] = {T.GF3[lane], T.GF3[64 + lane], T.GF3[128 + lane], T.GF3[192 + lane]};
+  geo8<false>(v, tw, out_xor4);
 }
 // transpose 2: writer lane (k0 = hi, t0 = lo) element k1 ; reader lane (k0 = hi, k1 = lo) element t0
 __device__ __forceinline__ void fwd_w2(const cplx (&v)[8], cplx* xch, int hi, int lo) {
@@ -240,70 +329,24 @@ __device__ __forceinline__ void fwd_r2(cplx (&v)[8], const cplx* xch, int hi, in
   for (int e = 0; e < 8; ++e) v[e] = xch[xslot(hi, lo, e)];
 }
 
-#ifndef XPOSE_HI_REGS
-#define XPOSE_HI_REGS 1  // lane-bits-3..5 transposes with cross-lane moves instead of LDS
-#endif
-
 __device__ __forceinline__ void fft512_fwd(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane,
                                            uint64_t out_xor4 = 0) {
   const int hi = lane >> 3, lo = lane & 7;
-  fwd_p1(v, T, lane);
-#if XPOSE_HI_REGS
-  xpose_hi(v);
-#else
-  fwd_w1(v, xch, hi, lo);
-  wave_lds_fence();
-  fwd_r1(v, xch, hi, lo);
-  wave_lds_fence();
-#endif
-  fwd_p2(v, T, lo);
+  fwd_p1(v);
+  xpose_hi(v);  // lane (k0 = hi, t0 = lo), element t1
+  fwd_p2(v, T, hi);
   fwd_w2(v, xch, hi, lo);
   wave_lds_fence();
   fwd_r2(v, xch, hi, lo);
   wave_lds_fence();
-  dft8<false, 1>(v, out_xor4);  // out_xor4 = 1 << 63: slots come out in order k2 ^ 4
-}
-
-// Two independent forward transforms through ONE scratch, software-pipelined: each
-// transpose's LDS round trip is covered by the other transform's butterflies.  LDS operations
-// of a wave execute in issue order, so b's writes cannot overtake a's earlier reads.
-__device__ __forceinline__ void fft512_fwd2(cplx (&a)[8], cplx (&b)[8], cplx* xch, const Fft512Tables& T,
-                                            int lane) {
-  const int hi = lane >> 3, lo = lane & 7;
-  fwd_p1(a, T, lane);
-  fwd_w1(a, xch, hi, lo);
-  wave_lds_fence();
-  fwd_r1(a, xch, hi, lo);
-  wave_lds_fence();
-  fwd_p1(b, T, lane);
-  wave_lds_fence();
-  fwd_w1(b, xch, hi, lo);
-  wave_lds_fence();
-  fwd_r1(b, xch, hi, lo);
-  wave_lds_fence();
-  fwd_p2(a, T, lo);
-  wave_lds_fence();
-  fwd_w2(a, xch, hi, lo);
-  wave_lds_fence();
-  fwd_r2(a, xch, hi, lo);
-  wave_lds_fence();
-  fwd_p2(b, T, lo);
-  wave_lds_fence();
-  fwd_w2(b, xch, hi, lo);
-  wave_lds_fence();
-  fwd_r2(b, xch, hi, lo);
-  wave_lds_fence();
-  dft8<false>(a);
-  dft8<false>(b);
+  fwd_p3(v, T, lane, out_xor4);  // out_xor4 = 1 << 63: slots come out in order k2 ^ 4
 }
 
 // Inverse: v[k2] = Y[k0 + 8 k1 + 64 k2] in lane (k0, k1) -> v[m] = sum_k Y_k w^{-jk} * conj(zeta^j),
-// j = t + 64 m in lane t.  Stages: P1 | W1 R1 | P2 | W2 R2 | P3 (the kernel interleaves them
-// with other work, so each is callable on its own).
-__device__ __forceinline__ void inv_p1(cplx (&v)[8], const Fft512Tables& T, int lo, uint64_t in_xor4 = 0) {
-  dft8<true, 2>(v, in_xor4);  // over k2 -> t0 ; lane (k0 = hi, k1 = lo); in_xor4: inputs in k2 ^ 4 order
-#pragma unroll
-  for (int t0 = 1; t0 < 8; ++t0) v[t0] = cmulc(v[t0], T.T2[t0 * 8 + lo]);
+// j = t + 64 m in lane t.  Stages: P1 | W1 R1 | P2 | hi transpose | P3 (the kernel interleaves
+// them with other work, so each is callable on its own).
+__device__ __forceinline__ void inv_p1(cplx (&v)[8], uint64_t in_xor4 = 0) {
+  dft8<true, true>(v, in_xor4);  // over k2 -> t0 ; lane (k0 = hi, k1 = lo); in_xor4: inputs in k2 ^ 4 order
 }
 // transpose 2': writer lane (k0, k1) element t0 ; reader lane (k0 = hi, t0 = lo) element k1
 __device__ __forceinline__ void inv_w1(const cplx (&v)[8], cplx* xch, int hi, int lo) {
@@ -315,18 +358,11 @@ __device__ __forceinline__ void inv_r1(cplx (&v)[8], const cplx* xch, int hi, in
   for (int e = 0; e < 8; ++e) v[e] = xch[xslot(hi, e, lo)];
 }
 __device__ __forceinline__ void inv_p2(cplx (&v)[8], const Fft512Tables& T, int hi, int lo) {
-  dft8<true>(v);  // over k1 -> t1 ; lane (k0 = hi, t0 = lo)
+  // geometric over k1 -> t1 with rho = conj(w64^{t0}); lane (k0 = hi, t0 = lo)
+  const cplx tw[4] = {T.GI2[lo], T.GI2[8 + lo], T.GI2[16 + lo], T.GI2[24 + lo]};
+  geo8<true, true>(v, tw);
 #pragma unroll
   for (int t1 = 0; t1 < 8; ++t1) v[t1] = cmulc(v[t1], T.T1[hi * T1_STRIDE + 8 * t1 + lo]);
-}
-// transpose 1': writer lane (k0 = hi, t0 = lo) element t1 ; reader lane (t1 = hi, t0 = lo) element k0
-__device__ __forceinline__ void inv_w2(const cplx (&v)[8], cplx* xch, int hi, int lo) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) xch[xslot(hi, e, lo)] = v[e];
-}
-__device__ __forceinline__ void inv_r2(cplx (&v)[8], const cplx* xch, int hi, int lo) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = xch[xslot(e, hi, lo)];
 }
 __device__ __forceinline__ void inv_p3(cplx (&v)[8]) {
   dft8<true>(v);  // over k0 -> m ; lane t holds x[t + 64 m] * zeta^t ... times psi^m still to remove
@@ -337,20 +373,13 @@ __device__ __forceinline__ void inv_p3(cplx (&v)[8]) {
 __device__ __forceinline__ void fft512_inv(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane,
                                            uint64_t in_xor4 = 0) {
   const int hi = lane >> 3, lo = lane & 7;
-  inv_p1(v, T, lo, in_xor4);
+  inv_p1(v, in_xor4);
   inv_w1(v, xch, hi, lo);
   wave_lds_fence();
   inv_r1(v, xch, hi, lo);
   wave_lds_fence();
   inv_p2(v, T, hi, lo);
-#if XPOSE_HI_REGS
   xpose_hi(v);
-#else
-  inv_w2(v, xch, hi, lo);
-  wave_lds_fence();
-  inv_r2(v, xch, hi, lo);
-  wave_lds_fence();
-#endif
   inv_p3(v);
 }
 

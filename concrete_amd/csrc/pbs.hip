@@ -72,7 +72,7 @@ __device__ __forceinline__ void xchg_barrier(uint32_t* flags, int w, uint32_t& c
 #endif
 }
 
-template <int L, bool RESID, bool STAMPS, bool STATE32>
+template <int L, bool RESID, bool STAMPS>
 __global__ void __launch_bounds__(PBS_PAIRS * 128, 2)
 pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx,
                     const uint64_t* __restrict__ luts, const uint64_t* __restrict__ lut_idx,
@@ -82,6 +82,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   constexpr int K = 1, K1 = 2, N = 1024, LOG2_2N = 11, LIMBS = 3, RQ = K1 * L;
   constexpr int PER_I = K1 * LIMBS * RQ * 512;  // complex values per Fourier GGSW
   static_assert(XCH_SLOTS <= (int)PBS1024_XCH_SLOTS, "transpose scratch");
+  static_assert(FFT512_TABLE_ENTRIES * sizeof(cplx) == PBS1024_TABLE_BYTES, "table bytes");
   constexpr int NW = 2 * PBS_PAIRS;           // waves per workgroup
   constexpr int GROUP = L * 512;              // complex values per ring group (one row of a slice)
   constexpr int NGRP = K1 * K1 * LIMBS;       // ring groups per CMUX step
@@ -89,9 +90,8 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   static_assert(GROUP % (64 * NW) == 0, "group split");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  cplx* T1 = reinterpret_cast<cplx*>(smem);
-  cplx* T2 = T1 + 8 * T1_STRIDE;
-  cplx* xch_all = T2 + 64;                       // NW x PBS1024_XCH_SLOTS: transpose scratch,
+  cplx* tbl = reinterpret_cast<cplx*>(smem);      // FFT tables (fft512.hpp)
+  cplx* xch_all = tbl + FFT512_TABLE_ENTRIES;     // NW x PBS1024_XCH_SLOTS: transpose scratch,
   cplx* ring = xch_all + NW * PBS1024_XCH_SLOTS;  // also the mailbox; 3 x GROUP key ring
   uint32_t* pflags = reinterpret_cast<uint32_t*>(ring + 3 * GROUP);  // NW pair-sync counters
 
@@ -126,24 +126,27 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   issue_group(0);
   if (total_groups > 1) issue_group(1);
 
-  build_fft512_tables(T1, T2, threadIdx.x, PBS_PAIRS * 128);
+  build_fft512_tables(tbl, threadIdx.x, PBS_PAIRS * 128);
   if (lane == 0) pflags[w] = 0u;
   uint32_t pcnt = 0;
   __syncthreads();
-  const Fft512Tables T{T1, T2};
+  const Fft512Tables T = fft512_tables_at(tbl);
 
   const uint64_t* lwe = in + (active ? (in_idx ? in_idx[s] : s) : 0) * (uint64_t)(n + 1);
   const uint64_t* lut = luts + (active && lut_idx ? lut_idx[s] : 0ull) * (uint64_t)(K1 * N);
 
-  // acc_h = LUT_h * X^{-ms(b)}  (blind_rotate_assign: polynomial_wrapping_monic_monomial_div)
-  uint64_t A[16];
+  // acc_h = LUT_h * X^{-ms(b)}  (blind_rotate_assign: polynomial_wrapping_monic_monomial_div).
+  // The wave keeps the NEGATED accumulator B = -acc_h (16 u64 per lane): the step's
+  // X^a acc - acc = B - X^a B then needs no 64-bit negation, and the recombination adds the
+  // rounded negated products, which the f64 rounding gives for free (MAGIC - v).
+  uint64_t B[16];
   {
     const uint32_t bt = active ? modswitch(lwe[n], LOG2_2N) : 0u;
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       const uint32_t src = (uint32_t)(lane + 64 * m + bt) & (2 * N - 1);
       const uint64_t v = active ? lut[h * N + (src & (N - 1))] : 0ull;
-      A[m] = src < N ? v : 0ull - v;
+      B[m] = src < N ? 0ull - v : v;
     }
   }
 
@@ -169,19 +172,28 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
       acc_t[7] += work;
     }
 
-    // ---- own polynomial: ct1 = acc * X^{at} - acc, decomposer state per coefficient ------
-    // decomposer state < 2^(l * logB): 32-bit when l * logB <= 31 (cfg2: 21 bits)
-    using state_t = typename std::conditional<STATE32, uint32_t, uint64_t>::type;
-    state_t st[16];
+    // ---- own polynomial: ct1 = acc * X^{at} - acc = B - X^{at} B, decomposer state per
+    //      coefficient.  Coefficient j = lane + 64 m reads B[src & (N-1)], src = j - at mod 2N,
+    //      negated when src >= N; o = 8 src + 8N (mod 2^32) carries the byte offset in bits 0..12
+    //      and "src < N" in bit 13, so ct1 = B + (rv ^ s) - s with s = -(bit 13 of o).
+    //      decomp_init(x) = (x >> nrep) + bit(nrep - 1) = (x + 2^(nrep-1)) >> nrep (a wrap of
+    //      x + 2^(nrep-1) past 2^64 gives state 0 instead of 2^(l logB), both decomposing to zero
+    //      digits); nrep >= 37 under the exactness gate, so only the high word is shifted.
+    uint32_t st[16];
     if (work) {
 #pragma unroll
-      for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = A[m];
+      for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = B[m];
       wave_lds_fence();
+      const uint32_t o0 = ((uint32_t)(lane - (int)at) << 3) + 8u * N;
+      const uint32_t khi = 1u << (nrep - 33);  // 2^(nrep-1) in the high word
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
-        const uint32_t src = (uint32_t)(lane + 64 * m - (int)at) & (2 * N - 1);
-        const uint64_t rv = xch64[src & (N - 1)];
-        st[m] = (state_t)decomp_init((src < N ? rv : 0ull - rv) - A[m], nrep);
+        const uint32_t o = o0 + 512u * m;
+        const uint64_t rv = *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(xch64) + (o & 8191u));
+        const uint32_t s32 = (uint32_t)((int32_t)(o << 18) >> 31);
+        const uint64_t rvs = rv ^ (((uint64_t)s32 << 32) | s32);
+        const uint64_t x = B[m] + rvs + (uint64_t)(s32 & 1u);
+        st[m] = ((uint32_t)(x >> 32) + khi) >> (nrep - 32);
       }
       wave_lds_fence();
     }
@@ -251,24 +263,24 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     //      transform of limb li - 1 is spread over the first three key windows of limb li, so
     //      its butterflies run while the key DMA of those windows is in flight. -------------
     const int hi = lane >> 3, lo = lane & 7;
-    // bits(v + MAGIC) = MAGIC_BITS + round(v): limb li's exact integers, shifted into A.  The
-    // constant of all limbs is removed with limb 0 (it must not survive into the next step's
-    // rotation: X^a * const != const).
+    // bits(MAGIC - v) = MAGIC_BITS - round(v): limb li's exact integers, negated (B = -acc),
+    // shifted into B.  The constant of all limbs is removed with limb 0 (it must not survive into
+    // the next step's rotation: X^a * const != const).
     auto recombine = [&](const cplx (&v)[8], auto LIc) __attribute__((always_inline)) {
       constexpr int lr = decltype(LIc)::value;
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
-        const double tr = v[m].re + RND_MAGIC, ti = v[m].im + RND_MAGIC;
+        const double tr = RND_MAGIC - v[m].re, ti = RND_MAGIC - v[m].im;
         if constexpr (RESID) {
-          max_resid = fmax(max_resid, fabs(v[m].re - (tr - RND_MAGIC)));
-          max_resid = fmax(max_resid, fabs(v[m].im - (ti - RND_MAGIC)));
+          max_resid = fmax(max_resid, fabs(v[m].re - (RND_MAGIC - tr)));
+          max_resid = fmax(max_resid, fabs(v[m].im - (RND_MAGIC - ti)));
         }
         if constexpr (lr == 0) {
-          A[m] += (uint64_t)__double_as_longlong(tr) - MAGIC_ALL;
-          A[m + 8] += (uint64_t)__double_as_longlong(ti) - MAGIC_ALL;
+          B[m] += (uint64_t)__double_as_longlong(tr) - MAGIC_ALL;
+          B[m + 8] += (uint64_t)__double_as_longlong(ti) - MAGIC_ALL;
         } else {
-          A[m] += (uint64_t)__double_as_longlong(tr) << limb_shift(lr);
-          A[m + 8] += (uint64_t)__double_as_longlong(ti) << limb_shift(lr);
+          B[m] += (uint64_t)__double_as_longlong(tr) << limb_shift(lr);
+          B[m + 8] += (uint64_t)__double_as_longlong(ti) << limb_shift(lr);
         }
       }
     };
@@ -329,28 +341,15 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
               }
             };
             // deferred inverse transform of limb li - 1 (its pass 1 ran before this limb and
-            // left the data in my scratch): pass 2 in window 0, pass 3 in window 1
+            // left the data in my scratch): passes 2 and 3 in window 0
             auto inv_stage = [&]() __attribute__((always_inline)) {
               if constexpr (li > 0) {
-                const int win = co * K1 + ro;
-                if (win == 0) {
+                if (co == 0 && ro == 0) {
                   cplx vp[8];
                   wave_lds_fence();
                   inv_r1(vp, xch, hi, lo);
                   inv_p2(vp, T, hi, lo);
-#if XPOSE_HI_REGS
                   xpose_hi(vp);
-                  inv_p3(vp);
-                  recombine(vp, std::integral_constant<int, li - 1>{});
-#else
-                  wave_lds_fence();
-                  inv_w2(vp, xch, hi, lo);
-#endif
-                  wave_lds_fence();
-                } else if (win == 1 && !XPOSE_HI_REGS) {
-                  cplx vp[8];
-                  wave_lds_fence();
-                  inv_r2(vp, xch, hi, lo);
                   inv_p3(vp);
                   recombine(vp, std::integral_constant<int, li - 1>{});
                   wave_lds_fence();
@@ -404,7 +403,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
           recombine(vp, LI);
         } else {
           // pass 1 now; passes 2 and 3 ride in the next limb's first two key windows
-          inv_p1(vp, T, lo, hsign);
+          inv_p1(vp, hsign);
           inv_w1(vp, xch, hi, lo);
           wave_lds_fence();
         }
@@ -425,21 +424,22 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     }
   }
 
-  // ---- sample extract (nth = 0): out[j] = -A_0[N - j] (j > 0), A_0[0]; body B[0] -------
+  // ---- sample extract (nth = 0) of acc = -B: out[j] = -acc_0[N - j] (j > 0), acc_0[0]; body acc_1[0]
   uint64_t* o = out + (active ? (out_idx ? out_idx[s] : s) : 0) * (uint64_t)(K * N + 1);
   if (!active) {
   } else if (h == 0) {
+    // acc = -B
 #pragma unroll
-    for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = A[m];
+    for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = B[m];
     wave_lds_fence();
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       const int j = lane + 64 * m;
       const uint64_t v = xch64[(N - j) & (N - 1)];
-      o[j] = j == 0 ? v : 0ull - v;
+      o[j] = j == 0 ? 0ull - v : v;
     }
   } else if (lane == 0) {
-    o[K * N] = A[0];
+    o[K * N] = 0ull - B[0];
   }
 
   if constexpr (RESID && !STAMPS) {
@@ -459,7 +459,7 @@ static int launch_pair_t(const PbsArgs& a) {
     set_error("pbs: N=1024 l=%d logB=%u is outside the exact range", L, a.base_log);
     return -2;
   }
-  auto kern = pbs1024_pair_kernel<L, RESID, STAMPS, true>;
+  auto kern = pbs1024_pair_kernel<L, RESID, STAMPS>;
   CHIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const uint32_t blocks = (a.num_samples + PBS_PAIRS - 1) / PBS_PAIRS;
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(PBS_PAIRS * 128), lds, a.stream, a.out, a.out_idx, a.luts, a.lut_idx,

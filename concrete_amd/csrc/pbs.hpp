@@ -9,7 +9,7 @@ namespace chip {
 // N = 1024 kernel geometry: a workgroup of two waves per ciphertext (one GLWE polynomial and
 // one half of the frequency slots per wave).  LDS: the two pass-1/pass-2 twiddle tables and one
 // 9.2 KB transpose scratch per wave (which doubles as the half-spectrum mailbox).
-constexpr size_t PBS1024_TABLE_BYTES = (8 * 72 + 64) * 16;  // FFT512_TABLE_ENTRIES (fft512.hpp)
+constexpr size_t PBS1024_TABLE_BYTES = (8 * 72 + 4 * (8 + 64 + 8)) * 16;  // FFT512_TABLE_ENTRIES (fft512.hpp)
 constexpr int PBS_PAIRS = 4;                // ciphertexts (wave pairs) per workgroup
 constexpr size_t PBS1024_XCH_SLOTS = 576;  // >= XCH_SLOTS (fft512.hpp), 16-B slots per wave
 constexpr size_t pbs1024_pair_lds_bytes(int level) {

@@ -60,9 +60,8 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   static_assert(GROUP % (64 * NW) == 0 && DIST < RS, "ring geometry");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  cplx* T1 = reinterpret_cast<cplx*>(smem);
-  cplx* T2 = T1 + 8 * T1_STRIDE;
-  cplx* xch_all = T2 + 64;                // NW x XS: transpose scratch and mailboxes
+  cplx* tbl = reinterpret_cast<cplx*>(smem);  // FFT tables (fft512.hpp)
+  cplx* xch_all = tbl + FFT512_TABLE_ENTRIES;  // NW x XS: transpose scratch and mailboxes
   cplx* ring = xch_all + NW * XS;         // RS x GROUP key ring
   uint32_t* qflags = reinterpret_cast<uint32_t*>(ring + RS * GROUP);  // NW sync counters
 
@@ -94,11 +93,11 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   for (int g = 0; g < DIST; ++g)
     if ((uint64_t)g < total_groups) issue_group(g);
 
-  build_fft512_tables(T1, T2, threadIdx.x, NW * 64);
+  build_fft512_tables(tbl, threadIdx.x, NW * 64);
   if (lane == 0) qflags[w] = 0u;
   uint32_t qcnt = 0;
   __syncthreads();
-  const Fft512Tables T{T1, T2};
+  const Fft512Tables T = fft512_tables_at(tbl);
 
   const uint64_t* lwe = in + (active ? (in_idx ? in_idx[s] : s) : 0) * (uint64_t)(n + 1);
   const uint64_t* lut = luts + (active && lut_idx ? lut_idx[s] : 0ull) * (uint64_t)(K1 * N);

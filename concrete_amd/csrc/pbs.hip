@@ -111,20 +111,23 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   // Both waves of a pair read the same group at the same time, each its own half of the slots:
   // group (li, co, ro) holds, for slots 0..3, column co / row ro and, for slots 4..7, column
   // 1 - co / row 1 - ro, i.e. "own"/"other" relative to the reading wave (bsk.hip).
-  const uint64_t total_groups = (uint64_t)n * NGRP;
-  auto issue_group = [&](uint64_t g) {
-    const uint64_t i = g / NGRP;
-    const int r = (int)(g % NGRP);  // (limb, co, ro) in consumption order = storage order
-    const cplx* src = fbsk + i * (uint64_t)PER_I + r * GROUP;
-    cplx* dst = ring + (int)(g % 3) * GROUP;
+  // Within a step every group index r = (li K1 + co) K1 + ro is a compile-time constant and
+  // NGRP is a multiple of 3, so a group's slot (r % 3) and its offset from the step's key base
+  // are constants too: the refill is one wave-uniform base plus immediates, no division.
+  static_assert(NGRP % 3 == 0, "ring slot of a group must not depend on the step");
+  const cplx* key_w = fbsk + (uint64_t)w * GLDS * 64;  // this wave's pieces of every group
+  cplx* ring_w = ring + w * GLDS * 64;
+  auto issue_group = [&](const cplx* key_step, int r) __attribute__((always_inline)) {
+    const cplx* src = key_step + r * GROUP;
+    cplx* dst = ring_w + (r % 3) * GROUP;
 #pragma unroll
-    for (int j = 0; j < GLDS; ++j) {
-      const int piece = w * GLDS + j;
-      __builtin_amdgcn_global_load_lds(src + piece * 64 + lane, (lds_ptr_t)(dst + piece * 64), 16, 0, 0);
-    }
+    for (int j = 0; j < GLDS; ++j)
+      __builtin_amdgcn_global_load_lds(src + j * 64 + lane, (lds_ptr_t)(dst + j * 64), 16, 0, 0);
   };
-  issue_group(0);
-  if (total_groups > 1) issue_group(1);
+  if (n > 0) {
+    issue_group(key_w, 0);
+    issue_group(key_w, 1);
+  }
 
   build_fft512_tables(tbl, threadIdx.x, PBS_PAIRS * 128);
   if (lane == 0) pflags[w] = 0u;
@@ -159,6 +162,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 
   uint64_t a_next = active ? lwe[0] : 0ull;
   for (uint32_t i = 0; i < n; ++i) {
+    const cplx* key_step = key_w + (uint64_t)i * PER_I;
     const uint64_t ai = a_next;
     if (i + 1 < n) a_next = active ? lwe[i + 1] : 0ull;
 
@@ -296,14 +300,15 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         for (int j = 0; j < 4; ++j) Y[j] = {0.0, 0.0};
 #pragma unroll
         for (int ro = 0; ro < K1; ++ro) {
-          const uint64_t g = (uint64_t)i * NGRP + (li * K1 + co) * K1 + ro;
+          const int r = (li * K1 + co) * K1 + ro;  // group within the step (constant)
+          const bool last_step = i + 1 >= n;
           if constexpr (STAMPS) {
             uint64_t t = stamp();
             acc_t[2] += t - tp;
             tp = t;
           }
           // group g landed for this wave's pieces (group g + 1 may stay in flight) ...
-          if (g + 1 < total_groups) wait_vmcnt<GLDS>();
+          if (r + 1 < NGRP || !last_step) wait_vmcnt<GLDS>();
           else wait_vmcnt<0>();
           if constexpr (STAMPS) {
             uint64_t t = stamp();
@@ -319,11 +324,12 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
           }
           // refill the slot of group g - 1 with group g + 2
 #ifndef DIAG_NODMA
-          if (g + 2 < total_groups) issue_group(g + 2);
+          if (r + 2 < NGRP) issue_group(key_step, r + 2);
+          else if (!last_step) issue_group(key_step + PER_I, r + 2 - NGRP);
 #endif
           if (work) {
             auto mac = [&]() __attribute__((always_inline)) {
-              const cplx* G = ring + (int)(g % 3) * GROUP + (4 * h) * 64 + lane;
+              const cplx* G = ring + (r % 3) * GROUP + (4 * h) * 64 + lane;
               // all key values of the window first, then the FMAs
               cplx gv[L][4];
 #pragma unroll

@@ -65,6 +65,17 @@ __device__ __forceinline__ int64_t decomp_next64(uint64_t& state, int logB) {
   return (int64_t)(res - (carry << logB));
 }
 
+// 32-bit state, digit as res + carry * (-2^logB) (one 24-bit multiply-add instead of a shift and
+// a subtraction); valid when level * base_log <= 31
+__device__ __forceinline__ int32_t decomp_next32(uint32_t& state, int logB, int32_t neg_base) {
+  const uint32_t mask = (1u << logB) - 1u;
+  const uint32_t res = state & mask;
+  state >>= logB;
+  const uint32_t carry = (((res - 1u) | state) & res) >> (logB - 1);
+  state += carry;
+  return __mul24((int)carry, neg_base) + (int32_t)res;  // v_mad_i32_i24
+}
+
 // same recurrence on a 32-bit state (valid when level * base_log <= 31)
 template <class U>
 __device__ __forceinline__ int32_t decomp_next_t(U& state, int logB) {

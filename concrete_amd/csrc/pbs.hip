@@ -117,12 +117,14 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   static_assert(NGRP % 3 == 0, "ring slot of a group must not depend on the step");
   const cplx* key_w = fbsk + (uint64_t)w * GLDS * 64;  // this wave's pieces of every group
   cplx* ring_w = ring + w * GLDS * 64;
+  const uint32_t lane_b = (uint32_t)lane * (uint32_t)sizeof(cplx);  // zero-extended lane offset
   auto issue_group = [&](const cplx* key_step, int r) __attribute__((always_inline)) {
-    const cplx* src = key_step + r * GROUP;
+    const char* src = reinterpret_cast<const char*>(key_step + r * GROUP);
     cplx* dst = ring_w + (r % 3) * GROUP;
 #pragma unroll
     for (int j = 0; j < GLDS; ++j)
-      __builtin_amdgcn_global_load_lds(src + j * 64 + lane, (lds_ptr_t)(dst + j * 64), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const cplx*>(src + j * 1024 + lane_b),
+                                       (lds_ptr_t)(dst + j * 64), 16, 0, 0);
   };
   if (n > 0) {
     issue_group(key_w, 0);
@@ -155,6 +157,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 
   const int nrep = 64 - L * (int)base_log;
   const int logB = (int)base_log;
+  const int32_t neg_base = -(1 << logB);
   double max_resid = 0.0;
   uint64_t acc_t[NSTAMP] = {};
   uint64_t t_begin = 0, tp = 0;
@@ -227,7 +230,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             cplx v[8];
             int32_t d[16];
 #pragma unroll
-            for (int m = 0; m < 16; ++m) d[m] = decomp_next_t(st[m], logB);
+            for (int m = 0; m < 16; ++m) d[m] = decomp_next32(st[m], logB, neg_base);
 #pragma unroll
             for (int m = 0; m < 8; ++m) v[m] = {(double)d[m], (double)d[m + 8]};
             fft512_fwd(v, xch, T, lane, hsign);
@@ -295,9 +298,11 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
       // (li, co, ro) holds exactly those spectra for both halves (layout: bsk.hip)
 #pragma unroll
       for (int co = 0; co < K1; ++co) {
-        cplx Y[4];
+        cplx Y[4];  // set by the first product of window ro = 0 (no zeroing)
+        if constexpr (DIAG_NOMAC) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) Y[j] = {0.0, 0.0};
+          for (int j = 0; j < 4; ++j) Y[j] = {0.0, 0.0};
+        }
 #pragma unroll
         for (int ro = 0; ro < K1; ++ro) {
           const int r = (li * K1 + co) * K1 + ro;  // group within the step (constant)
@@ -316,7 +321,9 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             tp = t;
           }
           // ... and for every wave's pieces; everyone is also done with group g - 1
+#ifndef DIAG_NOBAR
           pair_barrier();
+#endif
           if constexpr (STAMPS) {
             uint64_t t = stamp();
             acc_t[5] += t - tp;
@@ -341,8 +348,13 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                   const cplx x = ro == 0 ? Xo[q][j] : Xp[q][j];
-                  Y[j].re = __builtin_fma(x.re, gv[q][j].re, __builtin_fma(-x.im, gv[q][j].im, Y[j].re));
-                  Y[j].im = __builtin_fma(x.re, gv[q][j].im, __builtin_fma(x.im, gv[q][j].re, Y[j].im));
+                  if (ro == 0 && q == 0) {  // fma(a, b, 0) == a * b: same bits as accumulating from 0
+                    Y[j].re = __builtin_fma(x.re, gv[q][j].re, -x.im * gv[q][j].im);
+                    Y[j].im = __builtin_fma(x.re, gv[q][j].im, x.im * gv[q][j].re);
+                  } else {
+                    Y[j].re = __builtin_fma(x.re, gv[q][j].re, __builtin_fma(-x.im, gv[q][j].im, Y[j].re));
+                    Y[j].im = __builtin_fma(x.re, gv[q][j].im, __builtin_fma(x.im, gv[q][j].re, Y[j].im));
+                  }
                 }
               }
             };

@@ -76,6 +76,22 @@ __device__ __forceinline__ int32_t decomp_next32(uint32_t& state, int logB, int3
   return __mul24((int)carry, neg_base) + (int32_t)res;  // v_mad_i32_i24
 }
 
+// The same recurrence on an UNSHIFTED 32-bit state S: level q's raw digit is bits
+// [q logB, (q+1) logB) of S, the tie bit is bit (q+2) logB - 1 (the next level's top bit), and
+// the carry is added back at bit (q+1) logB.  ((res - 1) | next) & res has bit logB-1 set exactly
+// when res + next_top > B/2, i.e. carry = (res + next_top + B/2 - 1) >> logB.  Five or six
+// operations per digit instead of seven; valid when level * base_log <= 31.
+__device__ __forceinline__ int32_t decomp_level32(uint32_t& S, uint32_t off, int logB, uint32_t half_m1,
+                                                  int32_t neg_base, bool update) {
+  const uint32_t res = __builtin_amdgcn_ubfe(S, off, (uint32_t)logB);
+  // bit (q+2) logB - 1; past bit 31 it is zero (S < 2^(level logB + 1) <= 2^28), as is bit 31
+  const uint32_t tb = off + 2u * (uint32_t)logB - 1u;
+  const uint32_t top = __builtin_amdgcn_ubfe(S, tb < 31u ? tb : 31u, 1u);
+  const uint32_t carry = (res + top + half_m1) >> logB;
+  if (update) S += carry << (off + (uint32_t)logB);
+  return __mul24((int)carry, neg_base) + (int32_t)res;  // v_mad_i32_i24
+}
+
 // same recurrence on a 32-bit state (valid when level * base_log <= 31)
 template <class U>
 __device__ __forceinline__ int32_t decomp_next_t(U& state, int logB) {

@@ -47,6 +47,9 @@ constexpr int limb_shift(int li) { return li * 21 + (li > 0 ? 1 : 0); }
 #ifndef FWD_XBATCH
 #define FWD_XBATCH 2  // forward levels traded per exchange (mailbox: 4 KB per level, <= 2)
 #endif
+#ifndef KEY_DMA_POS
+#define KEY_DMA_POS 0  // where a window issues its key refill: 0 after the barrier, 1 after its key reads, 2 after its FMAs
+#endif
 #ifndef PAIR_FLAGS
 #define PAIR_FLAGS 1  // half-spectrum exchanges synchronise the two waves of a pair only
 #endif
@@ -158,6 +161,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   const int nrep = 64 - L * (int)base_log;
   const int logB = (int)base_log;
   const int32_t neg_base = -(1 << logB);
+  const uint32_t half_m1 = (1u << (logB - 1)) - 1u;
   double max_resid = 0.0;
   uint64_t acc_t[NSTAMP] = {};
   uint64_t t_begin = 0, tp = 0;
@@ -230,7 +234,8 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             cplx v[8];
             int32_t d[16];
 #pragma unroll
-            for (int m = 0; m < 16; ++m) d[m] = decomp_next32(st[m], logB, neg_base);
+            for (int m = 0; m < 16; ++m)
+              d[m] = decomp_level32(st[m], (uint32_t)((q0 + t) * logB), logB, half_m1, neg_base, q0 + t + 1 < L);
 #pragma unroll
             for (int m = 0; m < 8; ++m) v[m] = {(double)d[m], (double)d[m + 8]};
             fft512_fwd(v, xch, T, lane, hsign);
@@ -329,11 +334,18 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             acc_t[5] += t - tp;
             tp = t;
           }
-          // refill the slot of group g - 1 with group g + 2
+          // refill the slot of group g - 1 with group g + 2 (KEY_DMA_POS: right after the barrier,
+          // after the window's key reads, or after its FMAs)
+          auto refill = [&]() __attribute__((always_inline)) {
 #ifndef DIAG_NODMA
-          if (r + 2 < NGRP) issue_group(key_step, r + 2);
-          else if (!last_step) issue_group(key_step + PER_I, r + 2 - NGRP);
+            if constexpr (KEY_DMA_POS != 0) __builtin_amdgcn_sched_barrier(0);
+            if (r + 2 < NGRP) issue_group(key_step, r + 2);
+            else if (!last_step) issue_group(key_step + PER_I, r + 2 - NGRP);
+            if constexpr (KEY_DMA_POS != 0) __builtin_amdgcn_sched_barrier(0);
 #endif
+          };
+          if constexpr (KEY_DMA_POS == 0) refill();
+          else if (!work) refill();
           if (work) {
             auto mac = [&]() __attribute__((always_inline)) {
               const cplx* G = ring + (r % 3) * GROUP + (4 * h) * 64 + lane;
@@ -343,6 +355,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
               for (int q = 0; q < L; ++q)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) gv[q][j] = G[(q * 8 + j) * 64];
+              if constexpr (KEY_DMA_POS == 1) refill();
 #pragma unroll
               for (int q = 0; q < (DIAG_NOMAC ? 0 : L); ++q) {
 #pragma unroll
@@ -357,6 +370,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
                   }
                 }
               }
+              if constexpr (KEY_DMA_POS == 2) refill();
             };
             // deferred inverse transform of limb li - 1 (its pass 1 ran before this limb and
             // left the data in my scratch): passes 2 and 3 in window 0

@@ -47,6 +47,12 @@ constexpr int limb_shift(int li) { return li * 21 + (li > 0 ? 1 : 0); }
 #ifndef FWD_XBATCH
 #define FWD_XBATCH 2  // forward levels traded per exchange (mailbox: 4 KB per level, <= 2)
 #endif
+#ifndef DEFER_Y
+#define DEFER_Y 0  // 1/2: whole inverse of limbs 0 .. LIMBS-2 deferred into the next limb's windows 0-1 / 0
+#endif
+#ifndef INV_SPLIT
+#define INV_SPLIT 0  // 1: passes 2 and 3 of limb li's inverse ride in limb li+1's first key window (measured 92.5k vs 93.2k)
+#endif
 #ifndef KEY_DMA_POS
 #define KEY_DMA_POS 0  // where a window issues its key refill: 0 after the barrier, 1 after its key reads, 2 after its FMAs
 #endif
@@ -372,11 +378,37 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
               }
               if constexpr (KEY_DMA_POS == 2) refill();
             };
-            // deferred inverse transform of limb li - 1 (its pass 1 ran before this limb and
-            // left the data in my scratch): passes 2 and 3 in window 0
+            // deferred inverse transform of limb li - 1.  DEFER_Y: its Y spectrum waits in my
+            // scratch (my half parked at slots 256..511, my partner's half in my mailbox) and
+            // the whole transform runs in this limb's first two windows — pass 1 in window 0,
+            // passes 2 and 3 in window 1 — behind workgroup barriers that also order my
+            // partner's mailbox writes, so limbs 0 and 1 need no pair sync.  Otherwise pass 1
+            // ran before this limb and passes 2 and 3 run in window 0.
             auto inv_stage = [&]() __attribute__((always_inline)) {
               if constexpr (li > 0) {
-                if (co == 0 && ro == 0) {
+                if constexpr (DEFER_Y) {
+                  if (co == 0 && ro == 0) {
+                    cplx vp[8];
+                    wave_lds_fence();
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                      vp[j] = xch[(4 + j) * 64 + lane];
+                      vp[4 + j] = mybox[j * 64 + lane];
+                    }
+                    inv_p1(vp, hsign);
+                    inv_w1(vp, xch, hi, lo);
+                    wave_lds_fence();
+                  }
+                  if (co == 0 && ro == (DEFER_Y == 2 ? 0 : 1)) {
+                    cplx vp[8];
+                    inv_r1(vp, xch, hi, lo);
+                    inv_p2(vp, T, hi, lo);
+                    xpose_hi(vp);
+                    inv_p3(vp);
+                    recombine(vp, std::integral_constant<int, li - 1>{});
+                    wave_lds_fence();
+                  }
+                } else if (INV_SPLIT && co == 0 && ro == 0) {
                   cplx vp[8];
                   wave_lds_fence();
                   inv_r1(vp, xch, hi, lo);
@@ -395,7 +427,12 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 
         }
         if (work) {
-          if (co == 0) {
+          if (co == 0 && DEFER_Y && li + 1 < LIMBS) {
+            // park my half until the next limb's first window (after this limb's deferred
+            // inverse read my scratch, window 1)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) xch[(4 + j) * 64 + lane] = Y[j];
+          } else if (co == 0) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) Ymine[j] = Y[j];
           } else {
@@ -411,6 +448,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         acc_t[2] += t - tp;
         tp = t;
       }
+      if constexpr (DEFER_Y && li + 1 < LIMBS) return;  // inverse deferred into the next limb
       xchg_barrier(pflags, w, pcnt, guard);
       // my output polynomial's spectrum, slots in order k2 ^ 4h (undone by the inverse pass 1)
       cplx vp[8];
@@ -430,7 +468,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         tp = t;
       }
       if (work) {
-        if constexpr (li == LIMBS - 1) {
+        if constexpr (li == LIMBS - 1 || !INV_SPLIT) {
           fft512_inv(vp, xch, T, lane, hsign);
           recombine(vp, LI);
         } else {

@@ -315,8 +315,12 @@ __device__ __forceinline__ void fwd_p2(cplx (&v)[8], const Fft512Tables& T, int 
   const cplx tw[4] = {T.GF2[hi], T.GF2[8 + hi], T.GF2[16 + hi], T.GF2[24 + hi]};
   geo8<false>(v, tw);
 }
+__device__ __forceinline__ void fwd_p3_tw(cplx (&tw)[4], const Fft512Tables& T, int lane) {
+  tw[0] = T.GF3[lane], tw[1] = T.GF3[64 + lane], tw[2] = T.GF3[128 + lane], tw[3] = T.GF3[192 + lane];
+}
 __device__ __forceinline__ void fwd_p3(cplx (&v)[8], const Fft512Tables& T, int lane, uint64_t out_xor4) {
-  const cplx tw[4] = {T.GF3[lane], T.GF3[64 + lane], T.GF3[128 + lane], T.GF3[192 + lane]};
+  cplx tw[4];
+  fwd_p3_tw(tw, T, lane);
   geo8<false>(v, tw, out_xor4);
 }
 // transpose 2: writer lane (k0 = hi, t0 = lo) element k1 ; reader lane (k0 = hi, k1 = lo) element t0
@@ -335,11 +339,13 @@ __device__ __forceinline__ void fft512_fwd(cplx (&v)[8], cplx* xch, const Fft512
   fwd_p1(v);
   xpose_hi(v);  // lane (k0 = hi, t0 = lo), element t1
   fwd_p2(v, T, hi);
+  cplx tw3[4];  // pass-3 twiddles read ahead of the transpose: their latency hides in its round trip
+  fwd_p3_tw(tw3, T, lane);
   fwd_w2(v, xch, hi, lo);
   wave_lds_fence();
   fwd_r2(v, xch, hi, lo);
   wave_lds_fence();
-  fwd_p3(v, T, lane, out_xor4);  // out_xor4 = 1 << 63: slots come out in order k2 ^ 4
+  geo8<false>(v, tw3, out_xor4);  // out_xor4 = 1 << 63: slots come out in order k2 ^ 4
 }
 
 // Inverse: v[k2] = Y[k0 + 8 k1 + 64 k2] in lane (k0, k1) -> v[m] = sum_k Y_k w^{-jk} * conj(zeta^j),
@@ -357,12 +363,24 @@ __device__ __forceinline__ void inv_r1(cplx (&v)[8], const cplx* xch, int hi, in
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = xch[xslot(hi, e, lo)];
 }
-__device__ __forceinline__ void inv_p2(cplx (&v)[8], const Fft512Tables& T, int hi, int lo) {
-  // geometric over k1 -> t1 with rho = conj(w64^{t0}); lane (k0 = hi, t0 = lo)
-  const cplx tw[4] = {T.GI2[lo], T.GI2[8 + lo], T.GI2[16 + lo], T.GI2[24 + lo]};
-  geo8<true, true>(v, tw);
+// inverse pass-2 twiddles: tw[0..3] geometric stages, tw[4..11] the output twiddles
+__device__ __forceinline__ void inv_p2_tw(cplx (&tw)[12], const Fft512Tables& T, int hi, int lo) {
 #pragma unroll
-  for (int t1 = 0; t1 < 8; ++t1) v[t1] = cmulc(v[t1], T.T1[hi * T1_STRIDE + 8 * t1 + lo]);
+  for (int j = 0; j < 4; ++j) tw[j] = T.GI2[8 * j + lo];
+#pragma unroll
+  for (int t1 = 0; t1 < 8; ++t1) tw[4 + t1] = T.T1[hi * T1_STRIDE + 8 * t1 + lo];
+}
+__device__ __forceinline__ void inv_p2_with(cplx (&v)[8], const cplx (&tw)[12]) {
+  // geometric over k1 -> t1 with rho = conj(w64^{t0}); lane (k0 = hi, t0 = lo)
+  const cplx g[4] = {tw[0], tw[1], tw[2], tw[3]};
+  geo8<true, true>(v, g);
+#pragma unroll
+  for (int t1 = 0; t1 < 8; ++t1) v[t1] = cmulc(v[t1], tw[4 + t1]);
+}
+__device__ __forceinline__ void inv_p2(cplx (&v)[8], const Fft512Tables& T, int hi, int lo) {
+  cplx tw[12];
+  inv_p2_tw(tw, T, hi, lo);
+  inv_p2_with(v, tw);
 }
 __device__ __forceinline__ void inv_p3(cplx (&v)[8]) {
   dft8<true>(v);  // over k0 -> m ; lane t holds x[t + 64 m] * zeta^t ... times psi^m still to remove
@@ -374,11 +392,13 @@ __device__ __forceinline__ void fft512_inv(cplx (&v)[8], cplx* xch, const Fft512
                                            uint64_t in_xor4 = 0) {
   const int hi = lane >> 3, lo = lane & 7;
   inv_p1(v, in_xor4);
+  cplx tw[12];  // pass-2 twiddles read ahead of the transpose
+  inv_p2_tw(tw, T, hi, lo);
   inv_w1(v, xch, hi, lo);
   wave_lds_fence();
   inv_r1(v, xch, hi, lo);
   wave_lds_fence();
-  inv_p2(v, T, hi, lo);
+  inv_p2_with(v, tw);
   xpose_hi(v);
   inv_p3(v);
 }

@@ -26,7 +26,7 @@ const char* last_error();
 // Sticky per-device status word written by the PBS kernels, read back at synchronisation points
 // (cuda_synchronize_device, concrete_hip_device_status, the runtime's batch completion).
 constexpr uint32_t DEV_STATUS_SYNC_TIMEOUT = 1u;  // a wave-pair/quad sync spin hit its bound
-constexpr uint32_t DEFAULT_SPIN_LIMIT = 1u << 22;  // LDS-counter polls (~s_sleep 1 each) before giving up
+constexpr uint32_t DEFAULT_SPIN_LIMIT = 1u << 22;  // LDS-counter polls (s_sleep 0 each, >= ~30 ms) before giving up
 struct SyncGuard {
   uint32_t* status;     // device word, OR-ed with DEV_STATUS_* bits
   uint32_t spin_limit;  // polls before a sync spin gives up and flags DEV_STATUS_SYNC_TIMEOUT

@@ -14,10 +14,18 @@ start = next(i for i, l in enumerate(lines)
 end = next(i for i in range(start + 1, len(lines)) if lines[i].strip().startswith(".Lfunc_end"))
 body = lines[start:end]
 if loop:
+    # blocks of the outermost loop: its header and every block LLVM annotates
+    # "in Loop: Header=<hdr> Depth=1" (the latch may be laid out before the header); inner
+    # loops (the spin waits) are left out
     h = next(i for i, l in enumerate(body) if "Loop Header: Depth=1" in l)
-    lab = body[h].split(":")[0].strip()
-    last = max(i for i, l in enumerate(body) if re.search(r"s_(cbranch_\w+|branch)\s+" + re.escape(lab) + r"\b", l))
-    body = body[h:last + 1]
+    hdr = body[h].split(":")[0].strip().lstrip(".L")
+    keep, on = [], False
+    for i, l in enumerate(body):
+        if re.match(r"^\.?\w+:", l) or l.startswith("; %bb."):
+            on = i == h or ("Header=" + hdr + " Depth=1") in l
+        if on:
+            keep.append(l)
+    body = keep
 cnt = collections.Counter()
 cls = collections.Counter()
 for l in body:

@@ -50,6 +50,9 @@ struct __attribute__((aligned(16))) cplx {
 
 __device__ __forceinline__ cplx cadd(cplx a, cplx b) { return {a.re + b.re, a.im + b.im}; }
 __device__ __forceinline__ cplx csub(cplx a, cplx b) { return {a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ void pin(cplx& a) {  // optimisation barrier (kernel_util.hpp pin)
+  asm volatile("" : "+v"(a.re), "+v"(a.im));
+}
 __device__ __forceinline__ cplx cmul(cplx a, cplx w) {
   return {__builtin_fma(a.re, w.re, -a.im * w.im), __builtin_fma(a.re, w.im, a.im * w.re)};
 }

@@ -56,6 +56,12 @@ constexpr int NSTAMP = 10;  // rot+decomp, fwd+xchg, mac, y-xchg, inv+recomb, ri
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
+// Optimisation barrier on a register value: the value is computed here and not later (the
+// compiler otherwise sinks pure arithmetic past LDS barriers into later phases, where its
+// operands stay live and push the kernel past 256 VGPRs).  No instruction is emitted.
+__device__ __forceinline__ void pin(uint64_t& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
+
 template <int N_WAIT>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N_WAIT >= 0 && N_WAIT < 64, "vmcnt range");

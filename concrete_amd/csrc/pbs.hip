@@ -180,13 +180,15 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     if (i + 1 < n) a_next = active ? lwe[i + 1] : 0ull;
 
     const uint32_t at = modswitch(ai, LOG2_2N);
-    // tfhe skips a zero mask element; at == 0 gives X^0 acc - acc = 0 whose product is 0.
-    // The condition depends only on the ciphertext (uniform across the pair); a skipping pair
-    // still takes part in every workgroup barrier and key-ring refill.
-    const bool work = ai != 0ull && at != 0u;
+    // tfhe skips a zero mask element (and at == 0 changes nothing): the step still runs, on
+    // ct1 = X^0 acc - acc = 0, whose digits, spectra and products are exact zeros, so the
+    // recombination adds exactly 0 (the limb constants cancel).  Running every step keeps the
+    // compiler from hoisting undefined values of skipped-step arrays out of the loop, where
+    // they pinned ~110 VGPRs.
+    constexpr bool work = true;
     if constexpr (STAMPS) {
       tp = stamp();
-      acc_t[7] += work;
+      acc_t[7] += ai != 0ull && at != 0u;
     }
 
     // ---- own polynomial: ct1 = acc * X^{at} - acc = B - X^{at} B, decomposer state per
@@ -265,6 +267,12 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
           if (t < nq)
 #pragma unroll
             for (int j = 0; j < 4; ++j) Xp[q0 + t][j] = partnerbox[(t * 4 + j) * 64 + lane];
+        // materialise this batch's spectra here (else its transforms sink into the key windows)
+#pragma unroll
+        for (int t = 0; t < XB; ++t)
+          if (t < nq)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pin(Xo[q0 + t][j]), pin(Xp[q0 + t][j]);
       }
       // partner has read my mailbox before my next transform writes the scratch; after the last
       // batch the scratch is next written behind the key windows' workgroup barriers
@@ -377,6 +385,9 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
                 }
               }
               if constexpr (KEY_DMA_POS == 2) refill();
+              // this window's products are done here, not sunk past the next window's barrier
+#pragma unroll
+              for (int j = 0; j < 4; ++j) pin(Y[j]);
             };
             // deferred inverse transform of limb li - 1.  DEFER_Y: its Y spectrum waits in my
             // scratch (my half parked at slots 256..511, my partner's half in my mailbox) and
@@ -471,6 +482,10 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         if constexpr (li == LIMBS - 1 || !INV_SPLIT) {
           fft512_inv(vp, xch, T, lane, hsign);
           recombine(vp, LI);
+          // materialise B here (else the inverse tail sinks into the next limb's key windows)
+#pragma unroll
+          for (int m = 0; m < 16; ++m) pin(B[m]);
+          if constexpr (RESID) pin(max_resid);
         } else {
           // pass 1 now; passes 2 and 3 ride in the next limb's first two key windows
           inv_p1(vp, hsign);

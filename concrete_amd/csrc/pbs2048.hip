@@ -77,21 +77,25 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   const cplx* ctx = xch_all + ctl * 4 * XS;  // the four scratches of this ciphertext
   cplx* ctxw = xch_all + ctl * 4 * XS;
 
-  const uint64_t total_groups = (uint64_t)n * NGRP;
-  auto issue_group = [&](uint64_t g) {
-    const uint64_t i = g / NGRP;
-    const int r = (int)(g % NGRP);
-    const cplx* src = fbsk + i * (uint64_t)PER_I + r * GROUP;
-    cplx* dst = ring + (int)(g % RS) * GROUP;
+  // ---- key ring: group g = (step g / NGRP, r = g % NGRP) -> slot g % RS.  NGRP is a multiple
+  // of RS, so within a step a group's slot (r % RS) and its offset from the step's key base are
+  // compile-time constants: the refill is one wave-uniform base plus immediates.
+  static_assert(NGRP % RS == 0, "ring slot of a group must not depend on the step");
+  const cplx* key_w = fbsk + (uint64_t)w * GLDS * 64;  // this wave's pieces of every group
+  cplx* ring_w = ring + w * GLDS * 64;
+  const uint32_t lane_b = (uint32_t)lane * (uint32_t)sizeof(cplx);  // zero-extended lane offset
+  auto issue_group = [&](const cplx* key_step, int r) __attribute__((always_inline)) {
+    const char* src = reinterpret_cast<const char*>(key_step + r * GROUP);
+    cplx* dst = ring_w + (r % RS) * GROUP;
 #pragma unroll
-    for (int j = 0; j < GLDS; ++j) {
-      const int piece = w * GLDS + j;
-      __builtin_amdgcn_global_load_lds(src + piece * 64 + lane, (lds_ptr_t)(dst + piece * 64), 16, 0, 0);
-    }
+    for (int j = 0; j < GLDS; ++j)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const cplx*>(src + j * 1024 + lane_b),
+                                       (lds_ptr_t)(dst + j * 64), 16, 0, 0);
   };
+  if (n > 0) {
 #pragma unroll
-  for (int g = 0; g < DIST; ++g)
-    if ((uint64_t)g < total_groups) issue_group(g);
+    for (int g = 0; g < DIST; ++g) issue_group(key_w, g);
+  }
 
   build_fft512_tables(tbl, threadIdx.x, NW * 64);
   if (lane == 0) qflags[w] = 0u;
@@ -131,11 +135,16 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 
   uint64_t a_next = active ? lwe[0] : 0ull;
   for (uint32_t i = 0; i < n; ++i) {
+    const cplx* key_step = key_w + (uint64_t)i * PER_I;
+    const bool last_step = i + 1 >= n;
     const uint64_t ai = a_next;
     if (i + 1 < n) a_next = active ? lwe[i + 1] : 0ull;
     const uint32_t at = modswitch(ai, LOG2_2N);
-    // uniform across the ciphertext's four waves; skipping waves still join every barrier
-    const bool work = ai != 0ull && at != 0u;
+    // tfhe skips a zero mask element (and at == 0 changes nothing): the step still runs, on
+    // ct1 = X^0 acc - acc = 0, whose digits, spectra and products are exact zeros, so the
+    // recombination adds exactly 0 (the limb constants cancel).  Running every step keeps the
+    // compiler from hoisting undefined values of skipped-step arrays out of the loop.
+    constexpr bool work = true;
 
     // ---- ct1 = X^{at} acc - acc: the source coefficient may sit in the other parity's wave --
     uint32_t st[16];
@@ -187,6 +196,10 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         for (int vv = 0; vv < 4; ++vv)
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) X[vv][sub][jj] = ctx[vv * XS + (2 * v + jj) * 64 + lane];
+#pragma unroll
+        for (int vv = 0; vv < 4; ++vv)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) pin(X[vv][sub][jj]);
       }
       // everyone has read my spectrum before my next transform writes the scratch; after the
       // last sub-digit the scratches are next written behind the key windows' barriers
@@ -210,13 +223,18 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         for (int row = 0; row < K1; ++row) {
 #pragma unroll
           for (int sub = 0; sub < PBS2_SUBS; ++sub) {
-            const uint64_t g = (uint64_t)i * NGRP + ((li * K1 + cc) * K1 + row) * PBS2_SUBS + sub;
-            if (g + DIST - 1 < total_groups) wait_vmcnt<GLDS * (DIST - 1)>();
-            else wait_vmcnt<0>();
-            pair_barrier();  // group g landed for every wave; everyone is done with group g - 1
-            if (g + DIST < total_groups) issue_group(g + DIST);
+            const int r = ((li * K1 + cc) * K1 + row) * PBS2_SUBS + sub;  // group within the step
+            // group r landed for this wave's pieces (the next DIST - 1 may stay in flight) ...
+            if (r + DIST - 1 < NGRP || !last_step) wait_vmcnt<GLDS * (DIST - 1)>();
+            else if (r + 1 == NGRP) wait_vmcnt<0>();
+            else if (r + 2 == NGRP) wait_vmcnt<GLDS>();
+            else wait_vmcnt<GLDS * 2>();
+            pair_barrier();  // ... for every wave; everyone is done with group r - 1
+            // refill the slot of group r - 1 with group r + DIST (RS = DIST + 1)
+            if (r + DIST < NGRP) issue_group(key_step, r + DIST);
+            else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
             if (work) {
-              const cplx* G = ring + (int)(g % RS) * GROUP + (2 * v) * 64 + lane;
+              const cplx* G = ring + (r % RS) * GROUP + (2 * v) * 64 + lane;
 #pragma unroll
               for (int jj = 0; jj < 2; ++jj) {
                 const cplx ge = G[jj * 64], go = G[512 + jj * 64];
@@ -231,6 +249,9 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
                 Y[cc][1][jj].re = __builtin_fma(xo.re, ge.re, __builtin_fma(-xo.im, ge.im, Y[cc][1][jj].re));
                 Y[cc][1][jj].im = __builtin_fma(xo.re, ge.im, __builtin_fma(xo.im, ge.re, Y[cc][1][jj].im));
               }
+              // this window's products are done here, not sunk past the next window's barrier
+#pragma unroll
+              for (int jj = 0; jj < 2; ++jj) pin(Y[cc][0][jj]), pin(Y[cc][1][jj]), pin(P[cc][jj]);
             }
           }
         }
@@ -273,6 +294,10 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             A[m + 8] += (uint64_t)__double_as_longlong(ti) << (16 * li);
           }
         }
+        // materialise A here (else the inverse tail sinks into the next limb's key windows)
+#pragma unroll
+        for (int m = 0; m < 16; ++m) pin(A[m]);
+        if constexpr (RESID) pin(max_resid);
       }
     });
   }

@@ -47,15 +47,6 @@ constexpr int limb_shift(int li) { return li * 21 + (li > 0 ? 1 : 0); }
 #ifndef FWD_XBATCH
 #define FWD_XBATCH 2  // forward levels traded per exchange (mailbox: 4 KB per level, <= 2)
 #endif
-#ifndef DEFER_Y
-#define DEFER_Y 0  // 1/2: whole inverse of limbs 0 .. LIMBS-2 deferred into the next limb's windows 0-1 / 0
-#endif
-#ifndef INV_SPLIT
-#define INV_SPLIT 0  // 1: passes 2 and 3 of limb li's inverse ride in limb li+1's first key window (measured 92.5k vs 93.2k)
-#endif
-#ifndef KEY_DMA_POS
-#define KEY_DMA_POS 0  // where a window issues its key refill: 0 after the barrier, 1 after its key reads, 2 after its FMAs
-#endif
 #ifndef PAIR_FLAGS
 #define PAIR_FLAGS 1  // half-spectrum exchanges synchronise the two waves of a pair only
 #endif
@@ -185,7 +176,6 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     // recombination adds exactly 0 (the limb constants cancel).  Running every step keeps the
     // compiler from hoisting undefined values of skipped-step arrays out of the loop, where
     // they pinned ~110 VGPRs.
-    constexpr bool work = true;
     if constexpr (STAMPS) {
       tp = stamp();
       acc_t[7] += ai != 0ull && at != 0u;
@@ -199,7 +189,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     //      x + 2^(nrep-1) past 2^64 gives state 0 instead of 2^(l logB), both decomposing to zero
     //      digits); nrep >= 37 under the exactness gate, so only the high word is shifted.
     uint32_t st[16];
-    if (work) {
+    {
 #pragma unroll
       for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = B[m];
       wave_lds_fence();
@@ -234,7 +224,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     for (int q0 = 0; q0 < L; q0 += XB) {
       const int nq = (q0 + XB <= L) ? XB : L - q0;
       cplx out[XB][4];
-      if (work) {
+      {
 #pragma unroll
         for (int t = 0; t < XB; ++t) {
           if (t < nq) {
@@ -261,7 +251,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             for (int j = 0; j < 4; ++j) mybox[(t * 4 + j) * 64 + lane] = out[t][j];
       }
       xchg_barrier(pflags, w, pcnt, guard);
-      if (work) {
+      {
 #pragma unroll
         for (int t = 0; t < XB; ++t)
           if (t < nq)
@@ -285,10 +275,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     }
 
     // ---- per limb: MAC for both output polynomials on my half (key from the LDS ring),
-    //      trade halves through the mailbox, inverse transform of my polynomial.  The inverse
-    //      transform of limb li - 1 is spread over the first three key windows of limb li, so
-    //      its butterflies run while the key DMA of those windows is in flight. -------------
-    const int hi = lane >> 3, lo = lane & 7;
+    //      trade halves through the mailbox, inverse transform of my polynomial. ------------
     // bits(MAGIC - v) = MAGIC_BITS - round(v): limb li's exact integers, negated (B = -acc),
     // shifted into B.  The constant of all limbs is removed with limb 0 (it must not survive into
     // the next step's rotation: X^a * const != const).
@@ -348,110 +335,45 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             acc_t[5] += t - tp;
             tp = t;
           }
-          // refill the slot of group g - 1 with group g + 2 (KEY_DMA_POS: right after the barrier,
-          // after the window's key reads, or after its FMAs)
-          auto refill = [&]() __attribute__((always_inline)) {
+          // refill the slot of group g - 1 with group g + 2, right after the barrier (the DMA
+          // needs the lead time: issued after the window's reads or FMAs it measured slower)
 #ifndef DIAG_NODMA
-            if constexpr (KEY_DMA_POS != 0) __builtin_amdgcn_sched_barrier(0);
-            if (r + 2 < NGRP) issue_group(key_step, r + 2);
-            else if (!last_step) issue_group(key_step + PER_I, r + 2 - NGRP);
-            if constexpr (KEY_DMA_POS != 0) __builtin_amdgcn_sched_barrier(0);
+          if (r + 2 < NGRP) issue_group(key_step, r + 2);
+          else if (!last_step) issue_group(key_step + PER_I, r + 2 - NGRP);
 #endif
-          };
-          if constexpr (KEY_DMA_POS == 0) refill();
-          else if (!work) refill();
-          if (work) {
-            auto mac = [&]() __attribute__((always_inline)) {
-              const cplx* G = ring + (r % 3) * GROUP + (4 * h) * 64 + lane;
-              // all key values of the window first, then the FMAs
-              cplx gv[L][4];
+          const cplx* G = ring + (r % 3) * GROUP + (4 * h) * 64 + lane;
+          // all key values of the window first, then the FMAs
+          cplx gv[L][4];
 #pragma unroll
-              for (int q = 0; q < L; ++q)
+          for (int q = 0; q < L; ++q)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) gv[q][j] = G[(q * 8 + j) * 64];
-              if constexpr (KEY_DMA_POS == 1) refill();
+            for (int j = 0; j < 4; ++j) gv[q][j] = G[(q * 8 + j) * 64];
 #pragma unroll
-              for (int q = 0; q < (DIAG_NOMAC ? 0 : L); ++q) {
+          for (int q = 0; q < (DIAG_NOMAC ? 0 : L); ++q) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                  const cplx x = ro == 0 ? Xo[q][j] : Xp[q][j];
-                  if (ro == 0 && q == 0) {  // fma(a, b, 0) == a * b: same bits as accumulating from 0
-                    Y[j].re = __builtin_fma(x.re, gv[q][j].re, -x.im * gv[q][j].im);
-                    Y[j].im = __builtin_fma(x.re, gv[q][j].im, x.im * gv[q][j].re);
-                  } else {
-                    Y[j].re = __builtin_fma(x.re, gv[q][j].re, __builtin_fma(-x.im, gv[q][j].im, Y[j].re));
-                    Y[j].im = __builtin_fma(x.re, gv[q][j].im, __builtin_fma(x.im, gv[q][j].re, Y[j].im));
-                  }
-                }
+            for (int j = 0; j < 4; ++j) {
+              const cplx x = ro == 0 ? Xo[q][j] : Xp[q][j];
+              if (ro == 0 && q == 0) {  // fma(a, b, 0) == a * b: same bits as accumulating from 0
+                Y[j].re = __builtin_fma(x.re, gv[q][j].re, -x.im * gv[q][j].im);
+                Y[j].im = __builtin_fma(x.re, gv[q][j].im, x.im * gv[q][j].re);
+              } else {
+                Y[j].re = __builtin_fma(x.re, gv[q][j].re, __builtin_fma(-x.im, gv[q][j].im, Y[j].re));
+                Y[j].im = __builtin_fma(x.re, gv[q][j].im, __builtin_fma(x.im, gv[q][j].re, Y[j].im));
               }
-              if constexpr (KEY_DMA_POS == 2) refill();
-              // this window's products are done here, not sunk past the next window's barrier
-#pragma unroll
-              for (int j = 0; j < 4; ++j) pin(Y[j]);
-            };
-            // deferred inverse transform of limb li - 1.  DEFER_Y: its Y spectrum waits in my
-            // scratch (my half parked at slots 256..511, my partner's half in my mailbox) and
-            // the whole transform runs in this limb's first two windows — pass 1 in window 0,
-            // passes 2 and 3 in window 1 — behind workgroup barriers that also order my
-            // partner's mailbox writes, so limbs 0 and 1 need no pair sync.  Otherwise pass 1
-            // ran before this limb and passes 2 and 3 run in window 0.
-            auto inv_stage = [&]() __attribute__((always_inline)) {
-              if constexpr (li > 0) {
-                if constexpr (DEFER_Y) {
-                  if (co == 0 && ro == 0) {
-                    cplx vp[8];
-                    wave_lds_fence();
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                      vp[j] = xch[(4 + j) * 64 + lane];
-                      vp[4 + j] = mybox[j * 64 + lane];
-                    }
-                    inv_p1(vp, hsign);
-                    inv_w1(vp, xch, hi, lo);
-                    wave_lds_fence();
-                  }
-                  if (co == 0 && ro == (DEFER_Y == 2 ? 0 : 1)) {
-                    cplx vp[8];
-                    inv_r1(vp, xch, hi, lo);
-                    inv_p2(vp, T, hi, lo);
-                    xpose_hi(vp);
-                    inv_p3(vp);
-                    recombine(vp, std::integral_constant<int, li - 1>{});
-                    wave_lds_fence();
-                  }
-                } else if (INV_SPLIT && co == 0 && ro == 0) {
-                  cplx vp[8];
-                  wave_lds_fence();
-                  inv_r1(vp, xch, hi, lo);
-                  inv_p2(vp, T, hi, lo);
-                  xpose_hi(vp);
-                  inv_p3(vp);
-                  recombine(vp, std::integral_constant<int, li - 1>{});
-                  wave_lds_fence();
-                }
-              }
-            };
-            mac();
-            inv_stage();
+            }
           }
-
-
+          // this window's products are done here, not sunk past the next window's barrier
+#pragma unroll
+          for (int j = 0; j < 4; ++j) pin(Y[j]);
         }
-        if (work) {
-          if (co == 0 && DEFER_Y && li + 1 < LIMBS) {
-            // park my half until the next limb's first window (after this limb's deferred
-            // inverse read my scratch, window 1)
+        if (co == 0) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) xch[(4 + j) * 64 + lane] = Y[j];
-          } else if (co == 0) {
+          for (int j = 0; j < 4; ++j) Ymine[j] = Y[j];
+        } else {
+          // straight into my partner's mailbox (its scratch has been idle since the key
+          // windows' workgroup barriers), so no "partner has read" sync is needed afterwards
 #pragma unroll
-            for (int j = 0; j < 4; ++j) Ymine[j] = Y[j];
-          } else {
-            // straight into my partner's mailbox (its scratch has been idle since the key
-            // windows' workgroup barriers), so no "partner has read" sync is needed afterwards
-#pragma unroll
-            for (int j = 0; j < 4; ++j) partnermail[j * 64 + lane] = Y[j];
-          }
+          for (int j = 0; j < 4; ++j) partnermail[j * 64 + lane] = Y[j];
         }
       }
       if constexpr (STAMPS) {
@@ -459,16 +381,13 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         acc_t[2] += t - tp;
         tp = t;
       }
-      if constexpr (DEFER_Y && li + 1 < LIMBS) return;  // inverse deferred into the next limb
       xchg_barrier(pflags, w, pcnt, guard);
       // my output polynomial's spectrum, slots in order k2 ^ 4h (undone by the inverse pass 1)
       cplx vp[8];
-      if (work) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          vp[j] = Ymine[j];
-          vp[4 + j] = mybox[j * 64 + lane];
-        }
+      for (int j = 0; j < 4; ++j) {
+        vp[j] = Ymine[j];
+        vp[4 + j] = mybox[j * 64 + lane];
       }
       // no second sync: the only writes into my scratch by my partner are these Y mailboxes,
       // one per limb, always behind key-window workgroup barriers (the forward exchange only
@@ -478,21 +397,12 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         acc_t[3] += t - tp;
         tp = t;
       }
-      if (work) {
-        if constexpr (li == LIMBS - 1 || !INV_SPLIT) {
-          fft512_inv(vp, xch, T, lane, hsign);
-          recombine(vp, LI);
-          // materialise B here (else the inverse tail sinks into the next limb's key windows)
+      fft512_inv(vp, xch, T, lane, hsign);
+      recombine(vp, LI);
+      // materialise B here (else the inverse tail sinks into the next limb's key windows)
 #pragma unroll
-          for (int m = 0; m < 16; ++m) pin(B[m]);
-          if constexpr (RESID) pin(max_resid);
-        } else {
-          // pass 1 now; passes 2 and 3 ride in the next limb's first two key windows
-          inv_p1(vp, hsign);
-          inv_w1(vp, xch, hi, lo);
-          wave_lds_fence();
-        }
-      }
+      for (int m = 0; m < 16; ++m) pin(B[m]);
+      if constexpr (RESID) pin(max_resid);
       if constexpr (STAMPS) {
         uint64_t t = stamp();
         acc_t[4] += t - tp;

@@ -144,16 +144,15 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     // ct1 = X^0 acc - acc = 0, whose digits, spectra and products are exact zeros, so the
     // recombination adds exactly 0 (the limb constants cancel).  Running every step keeps the
     // compiler from hoisting undefined values of skipped-step arrays out of the loop.
-    constexpr bool work = true;
 
     // ---- ct1 = X^{at} acc - acc: the source coefficient may sit in the other parity's wave --
     uint32_t st[16];
-    if (work) {
+    {
 #pragma unroll
       for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = A[m];
     }
     quad_sync(qflags, ctl, v, qcnt, guard);
-    if (work) {
+    {
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const uint32_t sp = (uint32_t)(2 * (lane + 64 * m) + par - (int)at) & (2 * N - 1);
@@ -170,7 +169,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     // frequency slot 2v + jj
     cplx X[4][PBS2_SUBS][2];
     int32_t dlo[16], dhi[16];
-    if (work) {
+    {
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int32_t d = decomp_next_t(st[m], logB);
@@ -181,7 +180,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     }
 #pragma unroll
     for (int sub = 0; sub < PBS2_SUBS; ++sub) {
-      if (work) {
+      {
         cplx vv8[8];
 #pragma unroll
         for (int m = 0; m < 8; ++m)
@@ -191,7 +190,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         for (int k2 = 0; k2 < 8; ++k2) xch[k2 * 64 + lane] = vv8[k2];
       }
       quad_sync(qflags, ctl, v, qcnt, guard);
-      if (work) {
+      {
 #pragma unroll
         for (int vv = 0; vv < 4; ++vv)
 #pragma unroll
@@ -233,7 +232,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             // refill the slot of group r - 1 with group r + DIST (RS = DIST + 1)
             if (r + DIST < NGRP) issue_group(key_step, r + DIST);
             else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
-            if (work) {
+            {
               const cplx* G = ring + (r % RS) * GROUP + (2 * v) * 64 + lane;
 #pragma unroll
               for (int jj = 0; jj < 2; ++jj) {
@@ -257,7 +256,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         }
       }
       cplx V[8];
-      if (work) {
+      {
 #pragma unroll
         for (int cc = 0; cc < K1; ++cc)
 #pragma unroll
@@ -271,13 +270,13 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
           for (int jj = 0; jj < 2; ++jj) ctxw[vo * XS + (v * 2 + jj) * 64 + lane] = Y[vo >> 1][vo & 1][jj];
       }
       quad_sync(qflags, ctl, v, qcnt, guard);
-      if (work) {
+      {
 #pragma unroll
         for (int vv = 0; vv < 4; ++vv)
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) V[2 * vv + jj] = xch[(vv * 2 + jj) * 64 + lane];
       }
-      if (work) {
+      {
         fft512_inv(V, xch, T, lane);
 #pragma unroll
         for (int m = 0; m < 8; ++m) {

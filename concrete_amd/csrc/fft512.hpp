@@ -336,6 +336,23 @@ __device__ __forceinline__ void fwd_r2(cplx (&v)[8], const cplx* xch, int hi, in
   for (int e = 0; e < 8; ++e) v[e] = xch[xslot(hi, lo, e)];
 }
 
+// Forward transform with the pass-3 twiddles supplied (kept in registers by the caller) and a
+// hook run right before the transform's first LDS write (a pair wait in pbs.hip).
+template <class BeforeLds>
+__device__ __forceinline__ void fft512_fwd_tw(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane,
+                                              const cplx (&tw3)[4], uint64_t out_xor4, BeforeLds before_lds) {
+  const int hi = lane >> 3, lo = lane & 7;
+  fwd_p1(v);
+  xpose_hi(v);  // lane (k0 = hi, t0 = lo), element t1
+  fwd_p2(v, T, hi);
+  before_lds();
+  fwd_w2(v, xch, hi, lo);
+  wave_lds_fence();
+  fwd_r2(v, xch, hi, lo);
+  wave_lds_fence();
+  geo8<false>(v, tw3, out_xor4);  // out_xor4 = 1 << 63: slots come out in order k2 ^ 4
+}
+
 __device__ __forceinline__ void fft512_fwd(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane,
                                            uint64_t out_xor4 = 0) {
   const int hi = lane >> 3, lo = lane & 7;

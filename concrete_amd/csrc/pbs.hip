@@ -57,6 +57,24 @@ constexpr int limb_shift(int li) { return li * 21 + (li > 0 ? 1 : 0); }
 // Only LDS traffic is drained (lgkmcnt), never the key DMA (no release fence: that would add
 // vmcnt(0)).  LDS operations are coherent across the waves of a CU.
 // (DIAG_NOXBAR: timing-only builds without any exchange synchronisation.)
+// Split form: pair_signal publishes that this wave has issued its reads of the partner's
+// scratch (LDS operations of a wave execute in issue order, so the count is seen only after
+// them); pair_wait, before this wave next overwrites its own scratch, waits for the partner's.
+__device__ __forceinline__ void pair_signal(uint32_t* flags, int w, uint32_t& cnt) {
+  asm volatile("" ::: "memory");
+  ++cnt;
+#if !defined(DIAG_NOXBAR)
+  __hip_atomic_store(&flags[w], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+}
+__device__ __forceinline__ void pair_wait(uint32_t* flags, int w, uint32_t cnt, const SyncGuard& guard) {
+#if defined(DIAG_NOXBAR)
+  (void)flags, (void)w, (void)cnt, (void)guard;
+#else
+  spin_until_ge(&flags[w ^ 1], cnt, guard);
+#endif
+  asm volatile("" ::: "memory");
+}
 __device__ __forceinline__ void xchg_barrier(uint32_t* flags, int w, uint32_t& cnt, const SyncGuard& guard) {
 #if defined(DIAG_NOXBAR)
   (void)flags, (void)w, (void)cnt, (void)guard;
@@ -164,6 +182,10 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   uint64_t t_begin = 0, tp = 0;
   if constexpr (STAMPS) t_begin = stamp();
 
+  // forward pass-3 twiddles of my lane: constant for the whole kernel, kept in registers
+  cplx tw3[4];
+  fwd_p3_tw(tw3, T, lane);
+
   uint64_t a_next = active ? lwe[0] : 0ull;
   for (uint32_t i = 0; i < n; ++i) {
     const cplx* key_step = key_w + (uint64_t)i * PER_I;
@@ -236,7 +258,11 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
               d[m] = decomp_level32(st[m], (uint32_t)((q0 + t) * logB), logB, half_m1, neg_base, q0 + t + 1 < L);
 #pragma unroll
             for (int m = 0; m < 8; ++m) v[m] = {(double)d[m], (double)d[m + 8]};
-            fft512_fwd(v, xch, T, lane, hsign);
+            // the first transform after a mailbox exchange overwrites my scratch: my partner
+            // must have read the mailbox (it signals right after its reads)
+            fft512_fwd_tw(v, xch, T, lane, tw3, hsign, [&]() __attribute__((always_inline)) {
+              if (q0 > 0 && t == 0) pair_wait(pflags, w, pcnt, guard);
+            });
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               Xo[q0 + t][j] = v[j];
@@ -264,9 +290,10 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
             for (int j = 0; j < 4; ++j) pin(Xo[q0 + t][j]), pin(Xp[q0 + t][j]);
       }
-      // partner has read my mailbox before my next transform writes the scratch; after the last
-      // batch the scratch is next written behind the key windows' workgroup barriers
-      if (q0 + XB < L) xchg_barrier(pflags, w, pcnt, guard);
+      // my partner's mailbox has been read: signal it (it waits before its next transform writes
+      // its scratch).  After the last batch the scratch is next written behind the key windows'
+      // workgroup barriers.
+      if (q0 + XB < L) pair_signal(pflags, w, pcnt);
     }
     if constexpr (STAMPS) {
       uint64_t t = stamp();

@@ -336,15 +336,19 @@ __device__ __forceinline__ void fwd_r2(cplx (&v)[8], const cplx* xch, int hi, in
   for (int e = 0; e < 8; ++e) v[e] = xch[xslot(hi, lo, e)];
 }
 
-// Forward transform with the pass-3 twiddles supplied (kept in registers by the caller) and a
-// hook run right before the transform's first LDS write (a pair wait in pbs.hip).
+// Forward transform with the pass-2 and pass-3 twiddles supplied (kept in registers by the
+// caller: fwd_p2_tw / fwd_p3_tw) and a hook run right before the transform's first LDS write (a
+// pair wait in pbs.hip).
+__device__ __forceinline__ void fwd_p2_tw(cplx (&tw)[4], const Fft512Tables& T, int hi) {
+  tw[0] = T.GF2[hi], tw[1] = T.GF2[8 + hi], tw[2] = T.GF2[16 + hi], tw[3] = T.GF2[24 + hi];
+}
 template <class BeforeLds>
-__device__ __forceinline__ void fft512_fwd_tw(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane,
+__device__ __forceinline__ void fft512_fwd_tw(cplx (&v)[8], cplx* xch, int lane, const cplx (&tw2)[4],
                                               const cplx (&tw3)[4], uint64_t out_xor4, BeforeLds before_lds) {
   const int hi = lane >> 3, lo = lane & 7;
   fwd_p1(v);
   xpose_hi(v);  // lane (k0 = hi, t0 = lo), element t1
-  fwd_p2(v, T, hi);
+  geo8<false>(v, tw2);
   before_lds();
   fwd_w2(v, xch, hi, lo);
   wave_lds_fence();
@@ -406,6 +410,30 @@ __device__ __forceinline__ void inv_p3(cplx (&v)[8]) {
   dft8<true>(v);  // over k0 -> m ; lane t holds x[t + 64 m] * zeta^t ... times psi^m still to remove
 #pragma unroll
   for (int m = 1; m < 8; ++m) v[m] = cmulc(v[m], psi_pow(m));
+}
+
+// Inverse with the pass-2 stage twiddles supplied (registers) and the output twiddles read after
+// the LDS transpose (their latency hides behind the pass-2 butterflies).
+__device__ __forceinline__ void fft512_inv_tw(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane,
+                                              const cplx (&gi2)[4], uint64_t in_xor4) {
+  const int hi = lane >> 3, lo = lane & 7;
+  inv_p1(v, in_xor4);
+  inv_w1(v, xch, hi, lo);
+  wave_lds_fence();
+  inv_r1(v, xch, hi, lo);
+  wave_lds_fence();
+  cplx t1[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) t1[t] = T.T1[hi * T1_STRIDE + 8 * t + lo];
+  geo8<true, true>(v, gi2);
+#pragma unroll
+  for (int t = 0; t < 8; ++t) v[t] = cmulc(v[t], t1[t]);
+  xpose_hi(v);
+  inv_p3(v);
+}
+__device__ __forceinline__ void inv_p2_stage_tw(cplx (&tw)[4], const Fft512Tables& T, int lo) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) tw[j] = T.GI2[8 * j + lo];
 }
 
 __device__ __forceinline__ void fft512_inv(cplx (&v)[8], cplx* xch, const Fft512Tables& T, int lane,

@@ -260,7 +260,9 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             for (int m = 0; m < 8; ++m) v[m] = {(double)d[m], (double)d[m + 8]};
             // the first transform after a mailbox exchange overwrites my scratch: my partner
             // must have read the mailbox (it signals right after its reads)
-            fft512_fwd_tw(v, xch, T, lane, tw3, hsign, [&]() __attribute__((always_inline)) {
+            cplx tw2[4];
+            fwd_p2_tw(tw2, T, lane >> 3);
+            fft512_fwd_tw(v, xch, lane, tw2, tw3, hsign, [&]() __attribute__((always_inline)) {
               if (q0 > 0 && t == 0) pair_wait(pflags, w, pcnt, guard);
             });
 #pragma unroll
@@ -424,7 +426,9 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         acc_t[3] += t - tp;
         tp = t;
       }
-      fft512_inv(vp, xch, T, lane, hsign);
+      cplx gi2[4];  // inverse pass-2 stage twiddles, read ahead of the transpose
+      inv_p2_stage_tw(gi2, T, lane & 7);
+      fft512_inv_tw(vp, xch, T, lane, gi2, hsign);
       recombine(vp, LI);
       // materialise B here (else the inverse tail sinks into the next limb's key windows)
 #pragma unroll

@@ -40,6 +40,9 @@ namespace chip {
 constexpr uint64_t MAGIC_ALL = RND_MAGIC_BITS + (RND_MAGIC_BITS << 22) + (RND_MAGIC_BITS << 43);
 constexpr int limb_shift(int li) { return li * 21 + (li > 0 ? 1 : 0); }
 
+#ifndef FWD_LAST_VIA_WINDOW
+#define FWD_LAST_VIA_WINDOW 1  // last forward exchange published by the first key window's barrier
+#endif
 #ifndef DIAG_NOMAC
 #define DIAG_NOMAC 0  // diagnostic builds only: skip the key MAC (wrong results)
 #endif
@@ -278,20 +281,24 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
             for (int j = 0; j < 4; ++j) mybox[(t * 4 + j) * 64 + lane] = out[t][j];
       }
-      xchg_barrier(pflags, w, pcnt, guard);
-      {
+      // The last batch's halves need no pair sync: the first key window's workgroup barrier
+      // (which drains every wave's LDS writes) publishes them, and they are first used in the
+      // second window (row 1); they are read right after that barrier.
+      const bool last_batch = q0 + XB >= L;
+      if (!last_batch || !FWD_LAST_VIA_WINDOW) {
+        xchg_barrier(pflags, w, pcnt, guard);
 #pragma unroll
         for (int t = 0; t < XB; ++t)
           if (t < nq)
 #pragma unroll
             for (int j = 0; j < 4; ++j) Xp[q0 + t][j] = partnerbox[(t * 4 + j) * 64 + lane];
-        // materialise this batch's spectra here (else its transforms sink into the key windows)
-#pragma unroll
-        for (int t = 0; t < XB; ++t)
-          if (t < nq)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) pin(Xo[q0 + t][j]), pin(Xp[q0 + t][j]);
       }
+      // materialise this batch's spectra here (else its transforms sink into the key windows)
+#pragma unroll
+      for (int t = 0; t < XB; ++t)
+        if (t < nq)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) pin(Xo[q0 + t][j]);
       // my partner's mailbox has been read: signal it (it waits before its next transform writes
       // its scratch).  After the last batch the scratch is next written behind the key windows'
       // workgroup barriers.
@@ -370,6 +377,15 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
           if (r + 2 < NGRP) issue_group(key_step, r + 2);
           else if (!last_step) issue_group(key_step + PER_I, r + 2 - NGRP);
 #endif
+          if constexpr (FWD_LAST_VIA_WINDOW && li == 0) {
+            if (co == 0 && ro == 0) {
+              constexpr int QL = (L - 1) / FWD_XBATCH * FWD_XBATCH;  // first level of the last batch
+#pragma unroll
+              for (int q = QL; q < L; ++q)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) Xp[q][j] = partnerbox[((q - QL) * 4 + j) * 64 + lane];
+            }
+          }
           const cplx* G = ring + (r % 3) * GROUP + (4 * h) * 64 + lane;
           // all key values of the window first, then the FMAs
           cplx gv[L][4];

@@ -220,12 +220,18 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
       wave_lds_fence();
       const uint32_t o0 = ((uint32_t)(lane - (int)at) << 3) + 8u * N;
       const uint32_t khi = 1u << (nrep - 33);  // 2^(nrep-1) in the high word
+      // all 16 reads in flight at once (left to itself the scheduler issues them four at a time,
+      // one LDS round trip each)
+      uint64_t rv[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m)
+        rv[m] = *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(xch64) + ((o0 + 512u * m) & 8191u));
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const uint32_t o = o0 + 512u * m;
-        const uint64_t rv = *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(xch64) + (o & 8191u));
         const uint32_t s32 = (uint32_t)((int32_t)(o << 18) >> 31);
-        const uint64_t rvs = rv ^ (((uint64_t)s32 << 32) | s32);
+        const uint64_t rvs = rv[m] ^ (((uint64_t)s32 << 32) | s32);
         const uint64_t x = B[m] + rvs + (uint64_t)(s32 & 1u);
         st[m] = ((uint32_t)(x >> 32) + khi) >> (nrep - 32);
       }

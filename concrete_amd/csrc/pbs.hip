@@ -144,8 +144,20 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     cplx* dst = ring_w + (r % 3) * GROUP;
 #pragma unroll
     for (int j = 0; j < GLDS; ++j)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const cplx*>(src + j * 1024 + lane_b),
-                                       (lds_ptr_t)(dst + j * 64), 16, 0, 0);
+    {
+      // Issued from inline assembly so that the compiler does not see an LDS write: with the
+      // builtin it treats every window's key reads as possibly aliasing the DMA and waits for
+      // all twelve (lgkmcnt(0)) before the first FMA; here it counts them (lgkmcnt(4) ...):
+      // +1.1 % PBS/s.  The ring is ordered by the explicit vmcnt waits and workgroup barriers
+      // alone.  M0 (the LDS base of the piece) is set inside the statement; nothing else in the
+      // kernel uses M0.
+      const cplx* gp = reinterpret_cast<const cplx*>(src + j * 1024 + lane_b);
+      const uint32_t m0 = (uint32_t)(uintptr_t)(lds_ptr_t)(dst + j * 64);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(gp), "s"(m0) : "m0", "memory");
+#pragma clang diagnostic pop
+    }
   };
   if (n > 0) {
     issue_group(key_w, 0);

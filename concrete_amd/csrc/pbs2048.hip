@@ -189,8 +189,11 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
         for (int k2 = 0; k2 < 8; ++k2) xch[k2 * 64 + lane] = vv8[k2];
       }
-      quad_sync(qflags, ctl, v, qcnt, guard);
-      {
+      // The last sub-digit's spectra need no quad sync: the first key window's workgroup barrier
+      // (which drains every wave's LDS writes) publishes them, and they are first used in the
+      // second window (sub 1); they are read right after that barrier.
+      if (sub + 1 < PBS2_SUBS) {
+        quad_sync(qflags, ctl, v, qcnt, guard);
 #pragma unroll
         for (int vv = 0; vv < 4; ++vv)
 #pragma unroll
@@ -232,6 +235,15 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             // refill the slot of group r - 1 with group r + DIST (RS = DIST + 1)
             if (r + DIST < NGRP) issue_group(key_step, r + DIST);
             else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
+            if constexpr (li == 0) {
+              if (cc == 0 && row == 0 && sub == 0) {  // the last sub-digit's spectra (see above)
+#pragma unroll
+                for (int vv = 0; vv < 4; ++vv)
+#pragma unroll
+                  for (int jj = 0; jj < 2; ++jj)
+                    X[vv][PBS2_SUBS - 1][jj] = ctx[vv * XS + (2 * v + jj) * 64 + lane];
+              }
+            }
             {
               const cplx* G = ring + (r % RS) * GROUP + (2 * v) * 64 + lane;
 #pragma unroll

@@ -139,10 +139,10 @@ __global__ void __launch_bounds__(256) convert_bsk_kernel(cplx* __restrict__ des
   });
 }
 
-// N = 2048, k = 1, l = 1 (pbs2048.hip).  Block = (i, limb, col, row, sub, parity), in the order
-// of the output layout [n][limb][col][row][sub][parity][512]: the parity half p(u) = g[2u + par]
-// of key polynomial g (row, col) times 2^{12 sub} (mod 2^64), limb `limb`, as an N = 1024
-// negacyclic polynomial: folded, twisted, transformed exactly like the N = 1024 key.
+// N = 2048, k = 1, l = 1 (pbs2048.hip).  Block = (i, limb, col, row, parity), in the order of
+// the output layout [n][limb][col][row][parity][512]: the parity half p(u) = g[2u + par] of key
+// polynomial g (row, col), limb `limb`, as an N = 1024 negacyclic polynomial: folded, twisted,
+// transformed exactly like the N = 1024 key.
 template <int LIMBS>
 __global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__ dest, const uint64_t* __restrict__ src,
                                                              const ddc* __restrict__ zeta_t,
@@ -150,15 +150,13 @@ __global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__
   constexpr int M = 512, LOGM = 9;
   __shared__ ddc buf[M];
   const uint64_t blk = blockIdx.x;
-  const uint32_t par = (uint32_t)(blk & 1), sub = (uint32_t)((blk >> 1) & 1);
-  const uint32_t row = (uint32_t)((blk >> 2) & 1), col = (uint32_t)((blk >> 3) & 1);
-  const uint32_t limb = (uint32_t)((blk >> 4) % LIMBS);
-  const uint64_t i = (blk >> 4) / LIMBS;
+  const uint32_t par = (uint32_t)(blk & 1);
+  const uint32_t row = (uint32_t)((blk >> 1) & 1), col = (uint32_t)((blk >> 2) & 1);
+  const uint32_t limb = (uint32_t)((blk >> 3) % LIMBS);
+  const uint64_t i = (blk >> 3) / LIMBS;
   const uint64_t* g = src + (i * 4 + row * 2 + col) * 2048;  // [n][l = 1][row][col][N]
-  const int shift = (int)sub * PBS2_SUB_BITS;
   for (int j = threadIdx.x; j < M; j += blockDim.x) {
-    const uint64_t p0 = g[2 * j + par] << shift, p1 = g[2 * (j + M) + par] << shift;
-    ddc z{dd_from(limb_value<LIMBS>(p0, limb)), dd_from(limb_value<LIMBS>(p1, limb))};
+    ddc z{dd_from(limb_value<LIMBS>(g[2 * j + par], limb)), dd_from(limb_value<LIMBS>(g[2 * (j + M) + par], limb))};
     z = ddc_mul(z, zeta_t[j]);
     const int r = (int)(__builtin_bitreverse32((uint32_t)j) >> (32 - LOGM));
     buf[r] = z;
@@ -223,7 +221,7 @@ int convert_bsk_launch(const ConvertArgs& a) {
   CHIP_CHECK(hipMemcpyAsync(dt, tw.data(), tw.size() * sizeof(ddc), hipMemcpyHostToDevice, a.stream));
   int rc = 0;
   if (n2048) {
-    const uint64_t blocks = (uint64_t)a.n * PBS2_LIMBS * 4 * PBS2_SUBS * 2;
+    const uint64_t blocks = (uint64_t)a.n * PBS2_LIMBS * 4 * 2;
     hipLaunchKernelGGL((convert_bsk2048_kernel<PBS2_LIMBS>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
                        reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt);
     hipError_t e = hipGetLastError();

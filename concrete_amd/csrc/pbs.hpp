@@ -23,8 +23,9 @@ constexpr int PBS2_CTS = 2;
 constexpr int PBS2_RING_SLOTS = 4;
 constexpr int PBS2_RING_DIST = 3;
 constexpr int PBS2_LIMBS = 4;     // 16-bit key limbs
-constexpr int PBS2_SUBS = 2;      // balanced 12-bit sub-digits per decomposition digit
-constexpr int PBS2_SUB_BITS = 12;
+constexpr int PBS2_SUBS = 2;      // sub-digits per decomposition digit: balanced 16-bit d_lo, d_hi
+constexpr int PBS2_SUB_BITS = 16; // on the key-limb grid (pbs2048.hip)
+constexpr int PBS2_MAX_LOGB = 24; // |d_hi| <= 2^(logB-17) + 1 keeps the certified bound < 1/2
 constexpr size_t pbs2048_lds_bytes() {
   return PBS1024_TABLE_BYTES + 4 * PBS2_CTS * PBS1024_XCH_SLOTS * 16 + (size_t)PBS2_RING_SLOTS * 1024 * 16 +
          4 * PBS2_CTS * 4;  // + per-wave sync counters
@@ -66,8 +67,8 @@ inline bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_
   const KeyFormat f = key_format(k, N, level);
   switch (f.kind) {
     case KeyKind::N1024: return pbs1024_exact(k, level, base_log);
-    // one level whose digit splits into two 12-bit sub-digits (pbs2048.hip)
-    case KeyKind::N2048: return base_log >= 1 && base_log <= 2 * PBS2_SUB_BITS;
+    // one level whose digit splits into d_lo + 2^16 d_hi (pbs2048.hip)
+    case KeyKind::N2048: return base_log >= 1 && base_log <= PBS2_MAX_LOGB;
     case KeyKind::GENERIC: return generic_pbs_ok(k, N, level, base_log);
     default: return false;
   }
@@ -75,12 +76,12 @@ inline bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_
 
 // Size in bytes of the device Fourier bootstrapping key.
 //   N1024:   [n][col][limb][row*l + q][512] complex f64
-//   N2048:   [n][limb][col][row][sub][parity][512] complex f64 (pbs2048.hip)
+//   N2048:   [n][limb][col][row][parity][512] complex f64 (pbs2048.hip)
 //   GENERIC: [n][col][limb][row][q][N/2] complex f64 (pbs_generic.hip)
 inline uint64_t fourier_bsk_bytes(uint32_t n, uint32_t k, uint32_t level, uint32_t N) {
   const KeyFormat f = key_format(k, N, level);
   switch (f.kind) {
-    case KeyKind::N2048: return (uint64_t)n * f.limbs * (k + 1) * (k + 1) * PBS2_SUBS * 2 * 512 * 16ull * level;
+    case KeyKind::N2048: return (uint64_t)n * f.limbs * (k + 1) * (k + 1) * 2 * 512 * 16ull * level;
     case KeyKind::N1024:
     case KeyKind::GENERIC: return (uint64_t)n * level * (k + 1) * (k + 1) * f.limbs * (N / 2) * 16ull;
     default: return 0;

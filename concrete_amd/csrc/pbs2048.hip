@@ -10,9 +10,13 @@
 //   where every product is negacyclic in Z modulo Z^1024 + 1: the N = 1024 product of pbs.hip
 //   (512-point folded, twisted transform, fft512.hpp).  Multiplying by Z is pointwise
 //   multiplication by the evaluation point alpha_k = exp(i pi (1 - 4k) / 1024) of frequency k.
-// * Sub-digits.  A 23-bit digit d is split exactly into balanced 12-bit parts,
-//   d = d_lo + 2^12 d_hi, and the key holds the limbs of both g and 2^12 g (mod 2^64), so every
-//   product is (|sub-digit| <= 2^11) x (16-bit limb): 4 limbs keep the certified error < 1/2.
+// * Sub-digits on the limb grid.  The key polynomial g is split into 4 balanced 16-bit limbs,
+//   g = sum_j 2^{16 j} g_j, and a 23-bit digit d exactly into d = d_lo + 2^16 d_hi with d_lo
+//   balanced 16-bit (|d_lo| <= 2^15) and |d_hi| <= 2^(logB-17) + 1.  Then
+//       d g = sum_m 2^{16 m} (d_lo g_m + d_hi g_{m-1})   (mod 2^64, slots m = 0..3)
+//   so every slot is one exact integer convolution sum (certified error < 1/2,
+//   oracle/pyoracle.py:gpu2048_error_bound) and each key limb serves two slots: limb j's key
+//   window adds d_lo g_j to slot j and d_hi g_j to slot j + 1 (carried into the next limb).
 //
 // Mapping: four waves per ciphertext; wave v = 2c + p owns the parity-p half of GLWE polynomial c
 // (16 u64 per lane, lane t holds coefficient 2(t + 64m) + p), runs the forward transforms of its
@@ -51,8 +55,8 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
                     unsigned long long* __restrict__ resid_out, SyncGuard guard) {
   constexpr int N = 2048, LOG2_2N = 12, K1 = 2;
   constexpr int NW = 4 * PBS2_CTS;                          // waves per workgroup
-  constexpr int GROUP = 2 * 512;                            // (limb, col, row, sub): parity e and o spectra
-  constexpr int NGRP = PBS2_LIMBS * K1 * K1 * PBS2_SUBS;    // ring groups per CMUX step
+  constexpr int GROUP = 2 * 512;                            // (limb, col, row): parity e and o spectra
+  constexpr int NGRP = PBS2_LIMBS * K1 * K1;                // ring groups per CMUX step
   constexpr int PER_I = NGRP * GROUP;                       // complex values per Fourier GGSW
   constexpr int RS = PBS2_RING_SLOTS, DIST = PBS2_RING_DIST;
   constexpr int GLDS = GROUP / 64 / NW;                     // 1 KB LDS-DMA pieces per wave per group
@@ -175,7 +179,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         const int32_t d = decomp_next_t(st[m], logB);
         const int32_t lo = ((d + (1 << (PBS2_SUB_BITS - 1))) & ((1 << PBS2_SUB_BITS) - 1)) - (1 << (PBS2_SUB_BITS - 1));
         dlo[m] = lo;
-        dhi[m] = (d - lo) >> PBS2_SUB_BITS;  // exact: d - lo is a multiple of 2^12
+        dhi[m] = (d - lo) >> PBS2_SUB_BITS;  // exact: d - lo is a multiple of 2^16
       }
     }
 #pragma unroll
@@ -209,78 +213,103 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     }
 
     // ---- per limb: MAC for the four outputs on my quarter, trade quarters, inverse ---------
+    // Slot li = sum over rows of d_lo * g_li + d_hi * g_{li-1}: Ya/Pa hold slot li (its d_hi part
+    // from the previous limb's windows), Yb/Pb start slot li + 1 with d_hi * g_li.  Y[cc][par][jj]:
+    // output (column cc, parity par) at my frequency slot 2v + jj; P: the odd x odd products, times
+    // alpha when the slot is folded (after its windows: once for the d_hi part, once for d_lo).
+    cplx Ya[2][2][2], Pa[2][2];
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) Ya[cc][0][jj] = Ya[cc][1][jj] = Pa[cc][jj] = {0.0, 0.0};
     static_for<0, PBS2_LIMBS>([&](auto LI) __attribute__((always_inline)) {
       constexpr int li = decltype(LI)::value;
-      cplx Y[2][2][2];  // [col][parity][slot]
-      cplx P[2][2];     // [col][slot]: sum of odd x odd products, times alpha at the end
+      constexpr bool HI = li + 1 < PBS2_LIMBS;  // d_hi * g_3 lands at 2^64: vanishes
+      cplx Yb[2][2][2], Pb[2][2];
 #pragma unroll
       for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          Y[cc][0][jj] = Y[cc][1][jj] = P[cc][jj] = {0.0, 0.0};
-        }
+        for (int jj = 0; jj < 2; ++jj) Yb[cc][0][jj] = Yb[cc][1][jj] = Pb[cc][jj] = {0.0, 0.0};
+      // (a_e b_e + Z a_o b_o) and (a_e b_o + a_o b_e) of one row into (Y, P)
+      auto mac = [&](cplx (&Y)[2][2], cplx (&P)[2], const cplx& xe, const cplx& xo, const cplx& ge, const cplx& go,
+                     int jj) __attribute__((always_inline)) {
+        Y[0][jj].re = __builtin_fma(xe.re, ge.re, __builtin_fma(-xe.im, ge.im, Y[0][jj].re));
+        Y[0][jj].im = __builtin_fma(xe.re, ge.im, __builtin_fma(xe.im, ge.re, Y[0][jj].im));
+        P[jj].re = __builtin_fma(xo.re, go.re, __builtin_fma(-xo.im, go.im, P[jj].re));
+        P[jj].im = __builtin_fma(xo.re, go.im, __builtin_fma(xo.im, go.re, P[jj].im));
+        Y[1][jj].re = __builtin_fma(xe.re, go.re, __builtin_fma(-xe.im, go.im, Y[1][jj].re));
+        Y[1][jj].im = __builtin_fma(xe.re, go.im, __builtin_fma(xe.im, go.re, Y[1][jj].im));
+        Y[1][jj].re = __builtin_fma(xo.re, ge.re, __builtin_fma(-xo.im, ge.im, Y[1][jj].re));
+        Y[1][jj].im = __builtin_fma(xo.re, ge.im, __builtin_fma(xo.im, ge.re, Y[1][jj].im));
+      };
 #pragma unroll
       for (int cc = 0; cc < K1; ++cc) {
 #pragma unroll
         for (int row = 0; row < K1; ++row) {
+          const int r = (li * K1 + cc) * K1 + row;  // group within the step
+          // group r landed for this wave's pieces (the next DIST - 1 may stay in flight) ...
+          if (r + DIST - 1 < NGRP || !last_step) wait_vmcnt<GLDS * (DIST - 1)>();
+          else if (r + 1 == NGRP) wait_vmcnt<0>();
+          else if (r + 2 == NGRP) wait_vmcnt<GLDS>();
+          else wait_vmcnt<GLDS * 2>();
+          pair_barrier();  // ... for every wave; everyone is done with group r - 1
+          // refill the slot of group r - 1 with group r + DIST (RS = DIST + 1)
+          if (r + DIST < NGRP) issue_group(key_step, r + DIST);
+          else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
+          if constexpr (li == 0) {
+            if (cc == 0 && row == 0) {  // the last sub-digit's spectra (see above)
 #pragma unroll
-          for (int sub = 0; sub < PBS2_SUBS; ++sub) {
-            const int r = ((li * K1 + cc) * K1 + row) * PBS2_SUBS + sub;  // group within the step
-            // group r landed for this wave's pieces (the next DIST - 1 may stay in flight) ...
-            if (r + DIST - 1 < NGRP || !last_step) wait_vmcnt<GLDS * (DIST - 1)>();
-            else if (r + 1 == NGRP) wait_vmcnt<0>();
-            else if (r + 2 == NGRP) wait_vmcnt<GLDS>();
-            else wait_vmcnt<GLDS * 2>();
-            pair_barrier();  // ... for every wave; everyone is done with group r - 1
-            // refill the slot of group r - 1 with group r + DIST (RS = DIST + 1)
-            if (r + DIST < NGRP) issue_group(key_step, r + DIST);
-            else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
-            if constexpr (li == 0) {
-              if (cc == 0 && row == 0 && sub == 0) {  // the last sub-digit's spectra (see above)
+              for (int vv = 0; vv < 4; ++vv)
 #pragma unroll
-                for (int vv = 0; vv < 4; ++vv)
-#pragma unroll
-                  for (int jj = 0; jj < 2; ++jj)
-                    X[vv][PBS2_SUBS - 1][jj] = ctx[vv * XS + (2 * v + jj) * 64 + lane];
-              }
+                for (int jj = 0; jj < 2; ++jj)
+                  X[vv][PBS2_SUBS - 1][jj] = ctx[vv * XS + (2 * v + jj) * 64 + lane];
             }
-            {
-              const cplx* G = ring + (r % RS) * GROUP + (2 * v) * 64 + lane;
+          }
+          {
+            const cplx* G = ring + (r % RS) * GROUP + (2 * v) * 64 + lane;
+            cplx ge[2], go[2];
 #pragma unroll
-              for (int jj = 0; jj < 2; ++jj) {
-                const cplx ge = G[jj * 64], go = G[512 + jj * 64];
-                const cplx xe = X[2 * row][sub][jj], xo = X[2 * row + 1][sub][jj];
-                // (a_e b_e + Z a_o b_o) and (a_e b_o + a_o b_e)
-                Y[cc][0][jj].re = __builtin_fma(xe.re, ge.re, __builtin_fma(-xe.im, ge.im, Y[cc][0][jj].re));
-                Y[cc][0][jj].im = __builtin_fma(xe.re, ge.im, __builtin_fma(xe.im, ge.re, Y[cc][0][jj].im));
-                P[cc][jj].re = __builtin_fma(xo.re, go.re, __builtin_fma(-xo.im, go.im, P[cc][jj].re));
-                P[cc][jj].im = __builtin_fma(xo.re, go.im, __builtin_fma(xo.im, go.re, P[cc][jj].im));
-                Y[cc][1][jj].re = __builtin_fma(xe.re, go.re, __builtin_fma(-xe.im, go.im, Y[cc][1][jj].re));
-                Y[cc][1][jj].im = __builtin_fma(xe.re, go.im, __builtin_fma(xe.im, go.re, Y[cc][1][jj].im));
-                Y[cc][1][jj].re = __builtin_fma(xo.re, ge.re, __builtin_fma(-xo.im, ge.im, Y[cc][1][jj].re));
-                Y[cc][1][jj].im = __builtin_fma(xo.re, ge.im, __builtin_fma(xo.im, ge.re, Y[cc][1][jj].im));
-              }
-              // this window's products are done here, not sunk past the next window's barrier
+            for (int jj = 0; jj < 2; ++jj) ge[jj] = G[jj * 64], go[jj] = G[512 + jj * 64];
 #pragma unroll
-              for (int jj = 0; jj < 2; ++jj) pin(Y[cc][0][jj]), pin(Y[cc][1][jj]), pin(P[cc][jj]);
+            for (int jj = 0; jj < 2; ++jj) mac(Ya[cc], Pa[cc], X[2 * row][0][jj], X[2 * row + 1][0][jj], ge[jj], go[jj], jj);
+            if constexpr (HI) {
+#pragma unroll
+              for (int jj = 0; jj < 2; ++jj)
+                mac(Yb[cc], Pb[cc], X[2 * row][1][jj], X[2 * row + 1][1][jj], ge[jj], go[jj], jj);
+            }
+            // this window's products are done here, not sunk past the next window's barrier
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+              pin(Ya[cc][0][jj]), pin(Ya[cc][1][jj]), pin(Pa[cc][jj]);
+              if constexpr (HI) pin(Yb[cc][0][jj]), pin(Yb[cc][1][jj]), pin(Pb[cc][jj]);
             }
           }
         }
+        // column cc of slot li is complete: fold Z a_o b_o in and send my quarter of outputs
+        // vo = 2 cc + par straight into wave vo's mailbox, slot pair (v, jj).  Every scratch has been
+        // idle since this limb's first key-window barrier (the last sub-digit's spectra were read
+        // before the second), and nobody writes it again before the next limb's windows.
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          Ya[cc][0][jj] = cadd(Ya[cc][0][jj], cmul(Pa[cc][jj], alpha[jj]));
+          ctxw[(2 * cc) * XS + (v * 2 + jj) * 64 + lane] = Ya[cc][0][jj];
+          ctxw[(2 * cc + 1) * XS + (v * 2 + jj) * 64 + lane] = Ya[cc][1][jj];
+        }
+      }
+      // slot li + 1 so far (d_hi * g_li): fold its odd products now, so that only the Y values are
+      // carried across the inverse; the next limb's d_lo products restart P from zero
+      if constexpr (HI) {
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            Ya[cc][0][jj] = cadd(Yb[cc][0][jj], cmul(Pb[cc][jj], alpha[jj]));
+            Ya[cc][1][jj] = Yb[cc][1][jj];
+            Pa[cc][jj] = {0.0, 0.0};
+            pin(Ya[cc][0][jj]), pin(Ya[cc][1][jj]);
+          }
       }
       cplx V[8];
-      {
-#pragma unroll
-        for (int cc = 0; cc < K1; ++cc)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj) Y[cc][0][jj] = cadd(Y[cc][0][jj], cmul(P[cc][jj], alpha[jj]));
-        // my quarter of output vo goes straight into wave vo's mailbox, slot pair (v, jj): every
-        // scratch has been idle since the key windows' workgroup barriers, and nobody writes it
-        // again before the next limb's windows, so one sync suffices
-#pragma unroll
-        for (int vo = 0; vo < 4; ++vo)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj) ctxw[vo * XS + (v * 2 + jj) * 64 + lane] = Y[vo >> 1][vo & 1][jj];
-      }
       quad_sync(qflags, ctl, v, qcnt, guard);
       {
 #pragma unroll
@@ -358,7 +387,7 @@ static int launch2048_t(const PbsArgs& a) {
 
 int pbs2048_launch(const PbsArgs& a) {
   if (!(a.N == 2048 && a.k == 1 && a.level == 1 && a.limbs == (uint32_t)PBS2_LIMBS && a.base_log >= 1 &&
-        a.base_log <= 2 * PBS2_SUB_BITS)) {
+        a.base_log <= (uint32_t)PBS2_MAX_LOGB)) {
     set_error("unsupported PBS parameters: N=%u k=%u level=%u base_log=%u limbs=%u", a.N, a.k, a.level, a.base_log,
               a.limbs);
     return -2;

@@ -103,11 +103,11 @@ def signed_limb(x, limb, limbs=4):
 
 
 def test_fourier_key_2048_layout(B, small4, torch_cuda):
-    """Device key [n][limb][col][row][sub][parity][slot][lane] == numpy complex128 transform of the
-    parity halves of g * 2^(12 sub) (folded, twisted by zeta^t, zeta = e^{i pi/1024}), frequency
+    """Device key [n][limb][col][row][parity][slot][lane] == numpy complex128 transform of the
+    parity halves of g's 16-bit limbs (folded, twisted by zeta^t, zeta = e^{i pi/1024}), frequency
     order fft512_freq, scaled 1/512.  (numpy's FFT is not correctly rounded: tolerance 1e-13.)"""
     p = small4.p
-    got = B.to_host(small4.fbsk).view(np.float64).reshape(p.n, 4, 2, 2, 2, 2, 8, 64, 2)
+    got = B.to_host(small4.fbsk).view(np.float64).reshape(p.n, 4, 2, 2, 2, 8, 64, 2)
     bsk = small4.bsk.reshape(p.n, 1, 2, 2, 2048)
     lane = np.arange(64)
     slot = np.arange(8)
@@ -119,15 +119,13 @@ def test_fourier_key_2048_layout(B, small4, torch_cuda):
         for li in range(4):
             for col in range(2):
                 for row in range(2):
-                    for sub in range(2):
-                        for par in range(2):
-                            g = bsk[i, 0, row, col, par::2] << np.uint64(12 * sub)
-                            lv = signed_limb(g, li)
-                            z = (lv[:512] + 1j * lv[512:]) * tw
-                            ref = np.fft.fft(z)[K] / 512.0
-                            gg = got[i, li, col, row, sub, par]
-                            err = np.max(np.abs(gg[..., 0] + 1j * gg[..., 1] - ref))
-                            worst = max(worst, err / np.max(np.abs(ref)))
+                    for par in range(2):
+                        lv = signed_limb(bsk[i, 0, row, col, par::2], li)
+                        z = (lv[:512] + 1j * lv[512:]) * tw
+                        ref = np.fft.fft(z)[K] / 512.0
+                        gg = got[i, li, col, row, par]
+                        err = np.max(np.abs(gg[..., 0] + 1j * gg[..., 1] - ref))
+                        worst = max(worst, err / np.max(np.abs(ref)))
     assert worst < 1e-13, worst
 
 
@@ -146,6 +144,21 @@ def test_pbs2048_bit_exact_small(B, oracle, small4, torch_cuda, batch):
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
 
 
+@pytest.mark.parametrize("logB", [8, 16, 17, 24])
+def test_pbs2048_other_base_logs(B, oracle, torch_cuda, logB):
+    """The digit split d = d_lo + 2^16 d_hi at its edges: d_hi == 0 (logB <= 16), |d_hi| <= 2
+    (17) and the largest accepted digit (24, |d_hi| <= 129); bit-exact, residual under the bound."""
+    S = Setup(B, oracle, torch_cuda, replace(B.CFG4, n=12, base_log=logB), 6000 + logB)
+    width = 3
+    rng = np.random.RandomState(logB)
+    msgs = rng.randint(0, 8, size=6)
+    cts = encrypt(B, S, msgs, width, 50 + logB, std=2.0 ** -30)
+    acc = lut_acc(B, S, rng.randint(0, 8, size=8), width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    assert np.array_equal(got, run_oracle(oracle, S, cts, acc))
+    assert resid < oracle.gpu2048_error_bound(B.to_host(S.fbsk).view(np.float64), logB) < 0.5
+
+
 def test_pbs2048_cfg4_bit_exact_and_bound(B, oracle, cfg4, torch_cuda):
     """Full cfg4 (n = 742): bit-exact vs the oracle; the measured rounding residual stays below
     the GPU scheme's certified bound, itself < 1/2."""
@@ -158,7 +171,7 @@ def test_pbs2048_cfg4_bit_exact_and_bound(B, oracle, cfg4, torch_cuda):
     got, resid = run_gpu(B, cfg4, cts, acc, torch_cuda, resid=True)
     ref = run_oracle(oracle, cfg4, cts, acc)
     assert np.array_equal(got, ref)
-    bound = oracle.gpu2048_error_bound(B.to_host(cfg4.fbsk).view(np.float64))
+    bound = oracle.gpu2048_error_bound(B.to_host(cfg4.fbsk).view(np.float64), cfg4.p.base_log)
     assert resid < bound < 0.5, (resid, bound)
     dec = B.lwe_decrypt(cfg4.glwe_sk, got, cfg4.p.big_n)
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]

@@ -96,6 +96,10 @@ def test_key_formats_and_exact_range():
 
     assert fmt(1, 1024, 3) == (1, 3, 22)
     assert fmt(1, 2048, 1) == (2, 4, 16)
+    # cfg4 key: 4 limbs of g only (the digit is split on the limb grid, pbs2048.hip)
+    assert L.concrete_hip_fourier_bsk_size_bytes(742, 1, 1, 2048) == 742 * 4 * 4 * 1024 * 16
+    assert L.concrete_hip_pbs_supported(1, 2048, 1, 24) == 1
+    assert L.concrete_hip_pbs_supported(1, 2048, 1, 25) == 0
     for k, N, l, logB in [(5, 256, 1, 15), (6, 256, 1, 18), (3, 512, 1, 18), (2, 1024, 1, 23), (1, 4096, 1, 22),
                           (1, 8192, 1, 22), (1, 16384, 2, 15), (1, 2048, 2, 10)]:
         kind, limbs, bits = fmt(k, N, l)

@@ -270,6 +270,9 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             cplx ge[2], go[2];
 #pragma unroll
             for (int jj = 0; jj < 2; ++jj) ge[jj] = G[jj * 64], go[jj] = G[512 + jj * 64];
+            // all four reads in flight before the first FMA (left to itself the scheduler issues
+            // them one at a time, each behind its own LDS round trip): +1.1 %, 255 VGPRs
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int jj = 0; jj < 2; ++jj) mac(Ya[cc], Pa[cc], X[2 * row][0][jj], X[2 * row + 1][0][jj], ge[jj], go[jj], jj);
             if constexpr (HI) {

@@ -40,11 +40,33 @@ constexpr uint64_t P2_MAGIC_ALL =
 // key DMA is not.
 __device__ __forceinline__ void quad_sync(uint32_t* flags, int ctl, int v, uint32_t& cnt, const SyncGuard& guard) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if defined(D4_NOQS) && D4_NOQS
+  return;
+#endif
   ++cnt;
   __hip_atomic_store(&flags[ctl * 4 + v], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
   for (int o = 1; o < 4; ++o) spin_until_ge(&flags[ctl * 4 + ((v + o) & 3)], cnt, guard);
 }
+
+// Diagnostic builds only (timing, wrong results): D4_NOBAR (no key-window barriers), D4_NOMAC
+// (no key MAC FMAs), D4_NOINV (no inverse transforms), D4_NOFWD (no forward transforms),
+// D4_NOQS (no quad syncs).
+#ifndef D4_NOBAR
+#define D4_NOBAR 0
+#endif
+#ifndef D4_NOMAC
+#define D4_NOMAC 0
+#endif
+#ifndef D4_NOINV
+#define D4_NOINV 0
+#endif
+#ifndef D4_NOFWD
+#define D4_NOFWD 0
+#endif
+#ifndef D4_NOQS
+#define D4_NOQS 0
+#endif
 
 template <bool RESID>
 __global__ void __launch_bounds__(PBS2_CTS * 256, 2)
@@ -189,7 +211,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
         for (int m = 0; m < 8; ++m)
           vv8[m] = sub == 0 ? cplx{(double)dlo[m], (double)dlo[m + 8]} : cplx{(double)dhi[m], (double)dhi[m + 8]};
-        fft512_fwd(vv8, xch, T, lane);
+        if (!D4_NOFWD) fft512_fwd(vv8, xch, T, lane);
 #pragma unroll
         for (int k2 = 0; k2 < 8; ++k2) xch[k2 * 64 + lane] = vv8[k2];
       }
@@ -252,7 +274,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
           else if (r + 1 == NGRP) wait_vmcnt<0>();
           else if (r + 2 == NGRP) wait_vmcnt<GLDS>();
           else wait_vmcnt<GLDS * 2>();
-          pair_barrier();  // ... for every wave; everyone is done with group r - 1
+          if (!D4_NOBAR) pair_barrier();  // ... for every wave; everyone is done with group r - 1
           // refill the slot of group r - 1 with group r + DIST (RS = DIST + 1)
           if (r + DIST < NGRP) issue_group(key_step, r + DIST);
           else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
@@ -274,10 +296,10 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             // them one at a time, each behind its own LDS round trip): +1.1 %, 255 VGPRs
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int jj = 0; jj < 2; ++jj) mac(Ya[cc], Pa[cc], X[2 * row][0][jj], X[2 * row + 1][0][jj], ge[jj], go[jj], jj);
+            for (int jj = 0; jj < (D4_NOMAC ? 0 : 2); ++jj) mac(Ya[cc], Pa[cc], X[2 * row][0][jj], X[2 * row + 1][0][jj], ge[jj], go[jj], jj);
             if constexpr (HI) {
 #pragma unroll
-              for (int jj = 0; jj < 2; ++jj)
+              for (int jj = 0; jj < (D4_NOMAC ? 0 : 2); ++jj)
                 mac(Yb[cc], Pb[cc], X[2 * row][1][jj], X[2 * row + 1][1][jj], ge[jj], go[jj], jj);
             }
             // this window's products are done here, not sunk past the next window's barrier
@@ -321,7 +343,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
           for (int jj = 0; jj < 2; ++jj) V[2 * vv + jj] = xch[(vv * 2 + jj) * 64 + lane];
       }
       {
-        fft512_inv(V, xch, T, lane);
+        if (!D4_NOINV) fft512_inv(V, xch, T, lane);
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
           const double tr = V[m].re + RND_MAGIC, ti = V[m].im + RND_MAGIC;

@@ -43,6 +43,9 @@ constexpr int limb_shift(int li) { return li * 21 + (li > 0 ? 1 : 0); }
 #ifndef FWD_LAST_VIA_WINDOW
 #define FWD_LAST_VIA_WINDOW 1  // last forward exchange published by the first key window's barrier
 #endif
+#ifndef FWD_TW2_EARLY
+#define FWD_TW2_EARLY 1  // forward pass-2 twiddles issued ahead of pass 1 (+0.4 %)
+#endif
 #ifndef DIAG_NOMAC
 #define DIAG_NOMAC 0  // diagnostic builds only: skip the key MAC (wrong results)
 #endif
@@ -283,6 +286,10 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             // must have read the mailbox (it signals right after its reads)
             cplx tw2[4];
             fwd_p2_tw(tw2, T, lane >> 3);
+            // issued here, ahead of pass 1 and the register transpose that hide their latency
+            // (left alone the scheduler sinks each read to its butterfly stage, one exposed LDS
+            // round trip per stage)
+            if (FWD_TW2_EARLY) __builtin_amdgcn_sched_barrier(0);
             fft512_fwd_tw(v, xch, lane, tw2, tw3, hsign, [&]() __attribute__((always_inline)) {
               if (q0 > 0 && t == 0) pair_wait(pflags, w, pcnt, guard);
             });

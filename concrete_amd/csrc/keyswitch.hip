@@ -23,6 +23,9 @@ constexpr int KS_ICHUNK = 32;
 constexpr int KS_MAX_U = 4;                       // output words per thread per sample
 constexpr int KS_MAX_OUT = KS_MAX_U * KS_THREADS;  // n_out + 1 <= 1024 (the optimizer's n <= 1006 rows)
 constexpr int KS_MAX_L = 8;
+// batches from this size take the MFMA path when it is exact (CONCRETE_HIP_KS_PATH: 0 = never,
+// 1 = always when exact; A/B and test switch)
+constexpr uint32_t KS_MFMA_MIN_BATCH = 64;
 
 // Split-K (SPLIT): blockIdx.y takes mask positions [i_begin, i_end) and adds its partial sums
 // into pre-zeroed outputs with 64-bit atomics (wrapping addition is exact and order-free, so
@@ -154,6 +157,140 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// MFMA path (base_log <= 7): the digit x key-word products as exact int8 matrix products.
+// Every KSK word k is split into 8 balanced signed bytes, k = sum_c 2^{8c} k_c (mod 2^64),
+// k_c in [-128, 127]; every digit fits int8 (|d| <= 2^(logB-1) <= 64).  With A[b][r] the digit
+// of KSK row r = i l + t of sample b and B_c[r][j] = k_c of KSK[r][j], the int32 products
+//     S_c = A B_c   (|S_c| <= K 2^(logB-1) 128 < 2^31, checked by the host)
+// are exact on the i8 matrix cores (v_mfma_i32_32x32x32_i8), and
+//     out[b][j] = (j == n_out ? b_in : 0) - sum_c 2^{8c} S_c[b][j]   (mod 2^64)
+// is the keyswitch bit for bit.  Operands are K-contiguous rows (digits [Bp][Kp], key chunks
+// [8][NP][Kp], zero padded): a lane's 16-byte load is its fragment for both A and B, and since
+// A and B use the same lane/element -> k map the products sum over exactly the 32 k of a step.
+// ------------------------------------------------------------------------------------------
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+constexpr int KSM_TILE = 64;  // rows (samples) and columns (output words) per 4-wave workgroup
+
+__global__ void __launch_bounds__(256) ks_digits_i8_kernel(int8_t* __restrict__ A, const uint64_t* __restrict__ in,
+                                                         const uint64_t* __restrict__ in_idx, uint32_t n_in,
+                                                         uint32_t level, uint32_t base_log, uint32_t num_samples,
+                                                         uint32_t Kp, uint32_t ipr) {
+  // thread = (sample row b, mask position i); rows past the batch and positions past n_in: zeros
+  const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint32_t b = (uint32_t)(g / ipr), i = (uint32_t)(g % ipr);
+  const int nrep = 64 - (int)(level * base_log);
+  uint64_t a = 0ull;
+  if (b < num_samples && i < n_in) a = in[(in_idx ? in_idx[b] : b) * (uint64_t)(n_in + 1) + i];
+  uint64_t st = decomp_init(a, nrep);
+  int8_t* row = A + (uint64_t)b * Kp;
+  for (uint32_t t = 0; t < level; ++t) {
+    const int8_t d = (int8_t)decomp_next64(st, (int)base_log);
+    const uint32_t k = i * level + t;
+    if (k < Kp) row[k] = d;
+  }
+}
+
+// thread = (output word j, 16 consecutive KSK rows): 16 coalesced u64 reads (lanes along j),
+// then one 16-byte store per chunk c into B_c[j][k0 .. k0 + 15]
+__global__ void __launch_bounds__(256) ks_chunks_i8_kernel(int8_t* __restrict__ Bt, const uint64_t* __restrict__ ksk,
+                                                         uint32_t K, uint32_t W, uint32_t NP, uint32_t Kp) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t k0 = blockIdx.y * 16;
+  if (j >= NP) return;
+  uint32_t w[8][4] = {};
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const uint32_t k = k0 + e;
+    uint64_t v = (j < W && k < K) ? ksk[(uint64_t)k * W + j] : 0ull;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int32_t kc = (int32_t)(int8_t)(uint8_t)(v & 0xffull);  // balanced byte
+      v = (v - (uint64_t)(int64_t)kc) >> 8;
+      w[c][e >> 2] |= ((uint32_t)(uint8_t)kc) << (8 * (e & 3));
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+    *reinterpret_cast<uint4*>(Bt + ((uint64_t)c * NP + j) * Kp + k0) = make_uint4(w[c][0], w[c][1], w[c][2], w[c][3]);
+}
+
+// one wave = 32 samples x 32 output words, all 8 chunks (8 int32 accumulator tiles); 4 waves
+// per workgroup cover 64 x 64 (they share A and B rows through L1)
+__global__ void __launch_bounds__(256) ks_mfma_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx,
+                                                    const uint64_t* __restrict__ in, const uint64_t* __restrict__ in_idx,
+                                                    const int8_t* __restrict__ A, const int8_t* __restrict__ Bt,
+                                                    uint32_t n_in, uint32_t n_out, uint32_t num_samples, uint32_t NP,
+                                                    uint32_t Kp) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t row0 = blockIdx.y * KSM_TILE + 32 * (w >> 1), col0 = blockIdx.x * KSM_TILE + 32 * (w & 1);
+  const int8_t* ap = A + (uint64_t)(row0 + (lane & 31)) * Kp + 16 * (lane >> 5);
+  const int8_t* bp = Bt + (uint64_t)(col0 + (lane & 31)) * Kp + 16 * (lane >> 5);
+  const uint64_t cstride = (uint64_t)NP * Kp;
+  v16i acc[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[c][r] = 0;
+  for (uint32_t k0 = 0; k0 < Kp; k0 += 32) {
+    const v4i av = *reinterpret_cast<const v4i*>(ap + k0);
+    v4i bv[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) bv[c] = *reinterpret_cast<const v4i*>(bp + c * cstride + k0);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv[c], acc[c], 0, 0, 0);
+  }
+  // C/D map (gfx950, dtype-independent): col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+  const uint32_t W = n_out + 1;
+  const uint32_t j = col0 + (lane & 31);
+  if (j >= W) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const uint32_t b = row0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (b >= num_samples) continue;
+    uint64_t sum = 0ull;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) sum += (uint64_t)(int64_t)acc[c][r] << (8 * c);
+    uint64_t v = 0ull - sum;
+    if (j == n_out) v += in[(in_idx ? in_idx[b] : b) * (uint64_t)(n_in + 1) + n_in];
+    out[(out_idx ? out_idx[b] : b) * (uint64_t)W + j] = v;
+  }
+}
+
+// Whether the MFMA path is exact for these parameters (int8 digits, int32 sums).
+static bool ks_mfma_ok(const KsArgs& a) {
+  if (a.base_log > 7) return false;
+  const uint64_t K = (uint64_t)a.n_in * a.level;
+  const uint64_t Kp = (K + 31) / 32 * 32;
+  return Kp * (1ull << (a.base_log - 1)) * 128ull <= 0x7fffffffull;
+}
+
+static int keyswitch_mfma_launch(const KsArgs& a) {
+  const uint32_t K = a.n_in * a.level, Kp = (K + 31) / 32 * 32;
+  const uint32_t W = a.n_out + 1, NP = (W + KSM_TILE - 1) / KSM_TILE * KSM_TILE;
+  const uint32_t Bp = (a.num_samples + KSM_TILE - 1) / KSM_TILE * KSM_TILE;
+  int8_t *A = nullptr, *Bt = nullptr;
+  CHIP_CHECK(hipMallocAsync((void**)&A, (size_t)Bp * Kp, a.stream));
+  CHIP_CHECK(hipMallocAsync((void**)&Bt, (size_t)8 * NP * Kp, a.stream));
+  const uint32_t ipr = (Kp + a.level - 1) / a.level;  // positions per digit row (covers the padding)
+  const uint64_t nd = (uint64_t)Bp * ipr;
+  hipLaunchKernelGGL(ks_digits_i8_kernel, dim3((uint32_t)((nd + 255) / 256)), dim3(256), 0, a.stream, A, a.in,
+                     a.in_idx, a.n_in, a.level, a.base_log, a.num_samples, Kp, ipr);
+  hipLaunchKernelGGL(ks_chunks_i8_kernel, dim3((NP + 255) / 256, Kp / 16), dim3(256), 0, a.stream, Bt, a.ksk, K, W, NP,
+                     Kp);
+  hipLaunchKernelGGL(ks_mfma_kernel, dim3(NP / KSM_TILE, Bp / KSM_TILE), dim3(256), 0, a.stream, a.out, a.out_idx,
+                     a.in, a.in_idx, A, Bt, a.n_in, a.n_out, a.num_samples, NP, Kp);
+  hipError_t e = hipGetLastError();
+  CHIP_CHECK(hipFreeAsync(A, a.stream));
+  CHIP_CHECK(hipFreeAsync(Bt, a.stream));
+  if (e != hipSuccess) {
+    set_error("keyswitch launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
 int keyswitch_launch(const KsArgs& a) {
   if (a.n_out + 1 > (uint32_t)KS_MAX_OUT || a.level > (uint32_t)KS_MAX_L || a.level == 0 ||
       a.level * a.base_log >= 64 || a.base_log == 0) {
@@ -162,6 +299,8 @@ int keyswitch_launch(const KsArgs& a) {
   }
   const uint32_t blocks = (a.num_samples + KS_TILE - 1) / KS_TILE;
   if (blocks == 0) return 0;
+  static const int ks_path = getenv("CONCRETE_HIP_KS_PATH") ? atoi(getenv("CONCRETE_HIP_KS_PATH")) : -1;
+  if (ks_path != 0 && ks_mfma_ok(a) && (ks_path == 1 || a.num_samples >= KS_MFMA_MIN_BATCH)) return keyswitch_mfma_launch(a);
   const uint32_t U = (a.n_out + 1 + KS_THREADS - 1) / KS_THREADS;
   // enough workgroups for 256 CUs: split the mask positions when the batch alone is short
   uint32_t splits = 1;

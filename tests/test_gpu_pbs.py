@@ -348,6 +348,39 @@ def test_keyswitch_decompositions(B, oracle, torch_cuda, ks_l, ks_logB):
     assert np.array_equal(B.to_host(out), oracle.keyswitch_batch(op, cts, ksk))
 
 
+@pytest.mark.parametrize("ks_l,ks_logB,nb", [(4, 3, 64), (4, 3, 300), (7, 3, 129), (3, 4, 200), (5, 3, 96),
+                                             (2, 7, 70), (1, 7, 65)])
+def test_keyswitch_mfma_path(B, oracle, torch_cuda, ks_l, ks_logB, nb):
+    """The int8 matrix-core keyswitch (keyswitch.hip ks_mfma_kernel: 8 balanced key bytes x int8
+    digits, int32 sums, taken from 64 samples on when base_log <= 7): bit-exact vs the oracle,
+    ragged batches (partial 64-row tiles), n + 1 = 631 output words (partial column tile), the
+    widest accepted digits (logB = 7), and permuted in_idx / out_idx."""
+    p = replace(B.CFG2, ks_level=ks_l, ks_base_log=ks_logB)
+    glwe_sk = B.binary_key(p.big_n, 8400 + ks_logB + ks_l)
+    lwe_sk = B.binary_key(p.n, 8500 + ks_logB + ks_l)
+    ksk = B.ksk_generate(p, glwe_sk, lwe_sk, 8600 + ks_logB + ks_l)
+    rng = np.random.RandomState(nb)
+    cts = rng.randint(0, 2 ** 63, size=(nb, p.big_n + 1), dtype=np.int64).astype(np.uint64) * np.uint64(2) + \
+        np.uint64(1)
+    cts[0] = 0
+    cts[1] = np.uint64(0xFFFFFFFFFFFFFFFF)
+    dev = "cuda:0"
+    d_ksk = B.to_device(ksk, dev)
+    op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, ks_l=ks_l, ks_logB=ks_logB)
+    ref = oracle.keyswitch_batch(op, cts, ksk)
+    out = B.keyswitch(p, d_ksk, B.to_device(cts, dev))
+    torch_cuda.cuda.synchronize()
+    assert np.array_equal(B.to_host(out), ref)
+    in_idx = rng.permutation(nb).astype(np.uint64)
+    out_idx = rng.permutation(nb).astype(np.uint64)
+    out2 = B.keyswitch(p, d_ksk, B.to_device(cts, dev), in_idx=B.to_device(in_idx, dev),
+                       out_idx=B.to_device(out_idx, dev))
+    torch_cuda.cuda.synchronize()
+    exp = np.zeros_like(ref)
+    exp[out_idx.astype(np.int64)] = ref[in_idx.astype(np.int64)]
+    assert np.array_equal(B.to_host(out2), exp)
+
+
 def test_configs2_total_batch_65536(B, oracle, cfg2, torch_cuda):
     """BASELINE configs[2]'s whole batch (65,536 PBS) in one launch on one GPU: every sample
     decrypts to LUT[m], 8 random rows bit-exact, outputs of identical inputs identical."""

@@ -166,12 +166,14 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
 // are exact on the i8 matrix cores (v_mfma_i32_32x32x32_i8), and
 //     out[b][j] = (j == n_out ? b_in : 0) - sum_c 2^{8c} S_c[b][j]   (mod 2^64)
 // is the keyswitch bit for bit.  Operands are K-contiguous rows (digits [Bp][Kp], key chunks
-// [8][NP][Kp], zero padded): a lane's 16-byte load is its fragment for both A and B, and since
-// A and B use the same lane/element -> k map the products sum over exactly the 32 k of a step.
+// [8][NP][Kp], zero padded); A and B fragments use the same lane/element -> k map, so the
+// products sum over exactly the k of each step whatever order the hardware gives them.
 // ------------------------------------------------------------------------------------------
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
-constexpr int KSM_TILE = 64;  // rows (samples) and columns (output words) per 4-wave workgroup
+constexpr int KSM_ROWS = 128;  // rows (samples) per 4-wave workgroup
+constexpr int KSM_COLS = 64;   // columns (output words) per 4-wave workgroup
+constexpr int KSM_KB = 64;     // K per register block (Kp is padded to a multiple of it)
 
 __global__ void __launch_bounds__(256) ks_digits_i8_kernel(int8_t* __restrict__ A, const uint64_t* __restrict__ in,
                                                          const uint64_t* __restrict__ in_idx, uint32_t n_in,
@@ -216,60 +218,93 @@ __global__ void __launch_bounds__(256) ks_chunks_i8_kernel(int8_t* __restrict__ 
     *reinterpret_cast<uint4*>(Bt + ((uint64_t)c * NP + j) * Kp + k0) = make_uint4(w[c][0], w[c][1], w[c][2], w[c][3]);
 }
 
-// one wave = 32 samples x 32 output words, all 8 chunks (8 int32 accumulator tiles); 4 waves
-// per workgroup cover 64 x 64 (they share A and B rows through L1)
+// one wave = 64 samples (two 32-row tiles) x 32 output words, all 8 chunks: 16 int32
+// accumulator tiles (256 AGPRs), so each key-chunk fragment it loads serves two MFMAs; 4 waves
+// per workgroup cover 128 x 64.  K in register blocks of KSM_KB = 64: lane half h reads the 32
+// contiguous bytes [32 h, 32 h + 32) of the block for its row / column and feeds bytes
+// 16 s .. 16 s + 15 to step s (any k order is exact as long as A and B use the same one); the
+// next block's 20 fragments are loaded while the current block's 32 MFMAs run.
 __global__ void __launch_bounds__(256) ks_mfma_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx,
                                                     const uint64_t* __restrict__ in, const uint64_t* __restrict__ in_idx,
                                                     const int8_t* __restrict__ A, const int8_t* __restrict__ Bt,
                                                     uint32_t n_in, uint32_t n_out, uint32_t num_samples, uint32_t NP,
                                                     uint32_t Kp) {
+  constexpr int RT = 2, SPB = KSM_KB / 32;  // row tiles per wave, MFMA k-steps per block
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t row0 = blockIdx.y * KSM_TILE + 32 * (w >> 1), col0 = blockIdx.x * KSM_TILE + 32 * (w & 1);
-  const int8_t* ap = A + (uint64_t)(row0 + (lane & 31)) * Kp + 16 * (lane >> 5);
-  const int8_t* bp = Bt + (uint64_t)(col0 + (lane & 31)) * Kp + 16 * (lane >> 5);
-  const uint64_t cstride = (uint64_t)NP * Kp;
-  v16i acc[8];
+  const uint32_t row0 = blockIdx.y * KSM_ROWS + 64 * (w >> 1), col0 = blockIdx.x * KSM_COLS + 32 * (w & 1);
+  const int8_t* ap = A + (uint64_t)(row0 + (lane & 31)) * Kp + (KSM_KB / 2) * (lane >> 5);
+  const int8_t* bp = Bt + (uint64_t)(col0 + (lane & 31)) * Kp + (KSM_KB / 2) * (lane >> 5);
+  const uint64_t cstride = (uint64_t)NP * Kp, rstride = 32ull * Kp;
+  v16i acc[RT][8];
 #pragma unroll
-  for (int c = 0; c < 8; ++c)
+  for (int t = 0; t < RT; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[c][r] = 0;
-  for (uint32_t k0 = 0; k0 < Kp; k0 += 32) {
-    const v4i av = *reinterpret_cast<const v4i*>(ap + k0);
-    v4i bv[8];
+    for (int c = 0; c < 8; ++c)
 #pragma unroll
-    for (int c = 0; c < 8; ++c) bv[c] = *reinterpret_cast<const v4i*>(bp + c * cstride + k0);
+      for (int r = 0; r < 16; ++r) acc[t][c][r] = 0;
+  v4i av[RT][SPB], bv[8][SPB];
+  auto load_block = [&](uint32_t k0, v4i (&a4)[RT][SPB], v4i (&b4)[8][SPB]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int c = 0; c < 8; ++c) acc[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv[c], acc[c], 0, 0, 0);
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int s4 = 0; s4 < SPB; ++s4) a4[t][s4] = *reinterpret_cast<const v4i*>(ap + t * rstride + k0 + 16 * s4);
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int s4 = 0; s4 < SPB; ++s4) b4[c][s4] = *reinterpret_cast<const v4i*>(bp + c * cstride + k0 + 16 * s4);
+  };
+  load_block(0, av, bv);
+  for (uint32_t k0 = 0; k0 < Kp; k0 += KSM_KB) {
+    v4i an[RT][SPB], bn[8][SPB];
+    const uint32_t kn = k0 + KSM_KB < Kp ? k0 + KSM_KB : k0;  // last block: a harmless reload
+    load_block(kn, an, bn);
+    __builtin_amdgcn_sched_barrier(0);  // all next-block loads issued before this block's MFMAs
+#pragma unroll
+    for (int s4 = 0; s4 < SPB; ++s4)
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+          acc[t][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[t][s4], bv[c][s4], acc[t][c], 0, 0, 0);
+#pragma unroll
+    for (int s4 = 0; s4 < SPB; ++s4) {
+#pragma unroll
+      for (int t = 0; t < RT; ++t) av[t][s4] = an[t][s4];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) bv[c][s4] = bn[c][s4];
+    }
   }
   // C/D map (gfx950, dtype-independent): col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
   const uint32_t W = n_out + 1;
   const uint32_t j = col0 + (lane & 31);
   if (j >= W) return;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const uint32_t b = row0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (b >= num_samples) continue;
-    uint64_t sum = 0ull;
+  for (int t = 0; t < RT; ++t)
 #pragma unroll
-    for (int c = 0; c < 8; ++c) sum += (uint64_t)(int64_t)acc[c][r] << (8 * c);
-    uint64_t v = 0ull - sum;
-    if (j == n_out) v += in[(in_idx ? in_idx[b] : b) * (uint64_t)(n_in + 1) + n_in];
-    out[(out_idx ? out_idx[b] : b) * (uint64_t)W + j] = v;
-  }
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t b = row0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (b >= num_samples) continue;
+      uint64_t sum = 0ull;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) sum += (uint64_t)(int64_t)acc[t][c][r] << (8 * c);
+      uint64_t v = 0ull - sum;
+      if (j == n_out) v += in[(in_idx ? in_idx[b] : b) * (uint64_t)(n_in + 1) + n_in];
+      out[(out_idx ? out_idx[b] : b) * (uint64_t)W + j] = v;
+    }
 }
 
 // Whether the MFMA path is exact for these parameters (int8 digits, int32 sums).
 static bool ks_mfma_ok(const KsArgs& a) {
   if (a.base_log > 7) return false;
   const uint64_t K = (uint64_t)a.n_in * a.level;
-  const uint64_t Kp = (K + 31) / 32 * 32;
+  const uint64_t Kp = (K + KSM_KB - 1) / KSM_KB * KSM_KB;
   return Kp * (1ull << (a.base_log - 1)) * 128ull <= 0x7fffffffull;
 }
 
 static int keyswitch_mfma_launch(const KsArgs& a) {
-  const uint32_t K = a.n_in * a.level, Kp = (K + 31) / 32 * 32;
-  const uint32_t W = a.n_out + 1, NP = (W + KSM_TILE - 1) / KSM_TILE * KSM_TILE;
-  const uint32_t Bp = (a.num_samples + KSM_TILE - 1) / KSM_TILE * KSM_TILE;
+  const uint32_t K = a.n_in * a.level, Kp = (K + KSM_KB - 1) / KSM_KB * KSM_KB;
+  const uint32_t W = a.n_out + 1, NP = (W + KSM_COLS - 1) / KSM_COLS * KSM_COLS;
+  const uint32_t Bp = (a.num_samples + KSM_ROWS - 1) / KSM_ROWS * KSM_ROWS;
   int8_t *A = nullptr, *Bt = nullptr;
   CHIP_CHECK(hipMallocAsync((void**)&A, (size_t)Bp * Kp, a.stream));
   CHIP_CHECK(hipMallocAsync((void**)&Bt, (size_t)8 * NP * Kp, a.stream));
@@ -279,7 +314,7 @@ static int keyswitch_mfma_launch(const KsArgs& a) {
                      a.in_idx, a.n_in, a.level, a.base_log, a.num_samples, Kp, ipr);
   hipLaunchKernelGGL(ks_chunks_i8_kernel, dim3((NP + 255) / 256, Kp / 16), dim3(256), 0, a.stream, Bt, a.ksk, K, W, NP,
                      Kp);
-  hipLaunchKernelGGL(ks_mfma_kernel, dim3(NP / KSM_TILE, Bp / KSM_TILE), dim3(256), 0, a.stream, a.out, a.out_idx,
+  hipLaunchKernelGGL(ks_mfma_kernel, dim3(NP / KSM_COLS, Bp / KSM_ROWS), dim3(256), 0, a.stream, a.out, a.out_idx,
                      a.in, a.in_idx, A, Bt, a.n_in, a.n_out, a.num_samples, NP, Kp);
   hipError_t e = hipGetLastError();
   CHIP_CHECK(hipFreeAsync(A, a.stream));

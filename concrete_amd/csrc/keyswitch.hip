@@ -228,8 +228,13 @@ __global__ void __launch_bounds__(256) ks_mfma_kernel(uint64_t* __restrict__ out
                                                     const uint64_t* __restrict__ in, const uint64_t* __restrict__ in_idx,
                                                     const int8_t* __restrict__ A, const int8_t* __restrict__ Bt,
                                                     uint32_t n_in, uint32_t n_out, uint32_t num_samples, uint32_t NP,
-                                                    uint32_t Kp) {
+                                                    uint32_t Kp, uint32_t k_per_split) {
   constexpr int RT = 2, SPB = KSM_KB / 32;  // row tiles per wave, MFMA k-steps per block
+  // split-K (gridDim.z > 1): this workgroup sums k in [k_begin, k_end) and adds its partial
+  // result into pre-zeroed outputs with 64-bit atomics (wrapping addition: exact, order-free);
+  // split 0 adds the body
+  const uint32_t k_begin = blockIdx.z * k_per_split, k_end = min(Kp, k_begin + k_per_split);
+  const bool split = gridDim.z > 1;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t row0 = blockIdx.y * KSM_ROWS + 64 * (w >> 1), col0 = blockIdx.x * KSM_COLS + 32 * (w & 1);
   const int8_t* ap = A + (uint64_t)(row0 + (lane & 31)) * Kp + (KSM_KB / 2) * (lane >> 5);
@@ -253,10 +258,10 @@ __global__ void __launch_bounds__(256) ks_mfma_kernel(uint64_t* __restrict__ out
 #pragma unroll
       for (int s4 = 0; s4 < SPB; ++s4) b4[c][s4] = *reinterpret_cast<const v4i*>(bp + c * cstride + k0 + 16 * s4);
   };
-  load_block(0, av, bv);
-  for (uint32_t k0 = 0; k0 < Kp; k0 += KSM_KB) {
+  load_block(k_begin, av, bv);
+  for (uint32_t k0 = k_begin; k0 < k_end; k0 += KSM_KB) {
     v4i an[RT][SPB], bn[8][SPB];
-    const uint32_t kn = k0 + KSM_KB < Kp ? k0 + KSM_KB : k0;  // last block: a harmless reload
+    const uint32_t kn = k0 + KSM_KB < k_end ? k0 + KSM_KB : k0;  // last block: a harmless reload
     load_block(kn, an, bn);
     __builtin_amdgcn_sched_barrier(0);  // all next-block loads issued before this block's MFMAs
 #pragma unroll
@@ -288,8 +293,10 @@ __global__ void __launch_bounds__(256) ks_mfma_kernel(uint64_t* __restrict__ out
 #pragma unroll
       for (int c = 0; c < 8; ++c) sum += (uint64_t)(int64_t)acc[t][c][r] << (8 * c);
       uint64_t v = 0ull - sum;
-      if (j == n_out) v += in[(in_idx ? in_idx[b] : b) * (uint64_t)(n_in + 1) + n_in];
-      out[(out_idx ? out_idx[b] : b) * (uint64_t)W + j] = v;
+      if (j == n_out && blockIdx.z == 0) v += in[(in_idx ? in_idx[b] : b) * (uint64_t)(n_in + 1) + n_in];
+      uint64_t* o = out + (out_idx ? out_idx[b] : b) * (uint64_t)W + j;
+      if (split) atomicAdd((unsigned long long*)o, (unsigned long long)v);
+      else *o = v;
     }
 }
 
@@ -297,14 +304,21 @@ __global__ void __launch_bounds__(256) ks_mfma_kernel(uint64_t* __restrict__ out
 static bool ks_mfma_ok(const KsArgs& a) {
   if (a.base_log > 7) return false;
   const uint64_t K = (uint64_t)a.n_in * a.level;
-  const uint64_t Kp = (K + KSM_KB - 1) / KSM_KB * KSM_KB;
+  const uint64_t Kp = (K + 8 * KSM_KB - 1) / (8 * KSM_KB) * (8 * KSM_KB);  // worst split padding
   return Kp * (1ull << (a.base_log - 1)) * 128ull <= 0x7fffffffull;
 }
 
 static int keyswitch_mfma_launch(const KsArgs& a) {
-  const uint32_t K = a.n_in * a.level, Kp = (K + KSM_KB - 1) / KSM_KB * KSM_KB;
   const uint32_t W = a.n_out + 1, NP = (W + KSM_COLS - 1) / KSM_COLS * KSM_COLS;
   const uint32_t Bp = (a.num_samples + KSM_ROWS - 1) / KSM_ROWS * KSM_ROWS;
+  // split K until the grid has >= 2 waves per SIMD slot (1 wave per SIMD at 512 registers):
+  // 320 workgroups at cfg2 batch 4096 would leave the second round of the chip a quarter busy
+  const uint32_t wgs = (NP / KSM_COLS) * (Bp / KSM_ROWS);
+  const uint32_t K = a.n_in * a.level, kb = (K + KSM_KB - 1) / KSM_KB;
+  uint32_t splits = std::max<uint32_t>(1, std::min<uint32_t>((2 * 256 + wgs - 1) / wgs, std::min<uint32_t>(8, kb / 4)));
+  const uint32_t k_per_split = (kb + splits - 1) / splits * KSM_KB;
+  splits = (kb * KSM_KB + k_per_split - 1) / k_per_split;
+  const uint32_t Kp = splits * k_per_split;  // zero padded: whole blocks in every split
   int8_t *A = nullptr, *Bt = nullptr;
   CHIP_CHECK(hipMallocAsync((void**)&A, (size_t)Bp * Kp, a.stream));
   CHIP_CHECK(hipMallocAsync((void**)&Bt, (size_t)8 * NP * Kp, a.stream));
@@ -314,8 +328,13 @@ static int keyswitch_mfma_launch(const KsArgs& a) {
                      a.in_idx, a.n_in, a.level, a.base_log, a.num_samples, Kp, ipr);
   hipLaunchKernelGGL(ks_chunks_i8_kernel, dim3((NP + 255) / 256, Kp / 16), dim3(256), 0, a.stream, Bt, a.ksk, K, W, NP,
                      Kp);
-  hipLaunchKernelGGL(ks_mfma_kernel, dim3(NP / KSM_COLS, Bp / KSM_ROWS), dim3(256), 0, a.stream, a.out, a.out_idx,
-                     a.in, a.in_idx, A, Bt, a.n_in, a.n_out, a.num_samples, NP, Kp);
+  if (splits > 1) {
+    const uint64_t total = (uint64_t)W * a.num_samples;
+    hipLaunchKernelGGL(keyswitch_zero_kernel, dim3((uint32_t)std::min<uint64_t>((total + 255) / 256, 4096)), dim3(256),
+                       0, a.stream, a.out, a.out_idx, W, a.num_samples);
+  }
+  hipLaunchKernelGGL(ks_mfma_kernel, dim3(NP / KSM_COLS, Bp / KSM_ROWS, splits), dim3(256), 0, a.stream, a.out,
+                     a.out_idx, a.in, a.in_idx, A, Bt, a.n_in, a.n_out, a.num_samples, NP, Kp, k_per_split);
   hipError_t e = hipGetLastError();
   CHIP_CHECK(hipFreeAsync(A, a.stream));
   CHIP_CHECK(hipFreeAsync(Bt, a.stream));

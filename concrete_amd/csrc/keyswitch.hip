@@ -310,31 +310,47 @@ static bool ks_mfma_ok(const KsArgs& a) {
 
 static int keyswitch_mfma_launch(const KsArgs& a) {
   const uint32_t W = a.n_out + 1, NP = (W + KSM_COLS - 1) / KSM_COLS * KSM_COLS;
-  const uint32_t Bp = (a.num_samples + KSM_ROWS - 1) / KSM_ROWS * KSM_ROWS;
+  const uint32_t K = a.n_in * a.level, kb = (K + KSM_KB - 1) / KSM_KB;
+  // samples per pass: the int8 digit matrix of a pass stays <= 1 GiB (8-bit rows: K = 81,920)
+  const uint64_t kmax = (uint64_t)(kb + 7) / 8 * 8 * KSM_KB;
+  // (CONCRETE_HIP_KS_CHUNK: a smaller pass size, read per call — the multi-pass test uses it)
+  const char* cap_env = getenv("CONCRETE_HIP_KS_CHUNK");
+  const uint64_t cap = cap_env && atoll(cap_env) > 0 ? (uint64_t)atoll(cap_env) : (1ull << 30) / kmax;
+  const uint32_t chunk = (uint32_t)std::max<uint64_t>(
+      KSM_ROWS, std::min<uint64_t>((uint64_t)(a.num_samples + KSM_ROWS - 1) / KSM_ROWS * KSM_ROWS,
+                                   cap / KSM_ROWS * KSM_ROWS));
   // split K until the grid has >= 2 waves per SIMD slot (1 wave per SIMD at 512 registers):
   // 320 workgroups at cfg2 batch 4096 would leave the second round of the chip a quarter busy
-  const uint32_t wgs = (NP / KSM_COLS) * (Bp / KSM_ROWS);
-  const uint32_t K = a.n_in * a.level, kb = (K + KSM_KB - 1) / KSM_KB;
+  const uint32_t wgs = (NP / KSM_COLS) * (chunk / KSM_ROWS);
   uint32_t splits = std::max<uint32_t>(1, std::min<uint32_t>((2 * 256 + wgs - 1) / wgs, std::min<uint32_t>(8, kb / 4)));
   const uint32_t k_per_split = (kb + splits - 1) / splits * KSM_KB;
   splits = (kb * KSM_KB + k_per_split - 1) / k_per_split;
   const uint32_t Kp = splits * k_per_split;  // zero padded: whole blocks in every split
   int8_t *A = nullptr, *Bt = nullptr;
-  CHIP_CHECK(hipMallocAsync((void**)&A, (size_t)Bp * Kp, a.stream));
+  CHIP_CHECK(hipMallocAsync((void**)&A, (size_t)chunk * Kp, a.stream));
   CHIP_CHECK(hipMallocAsync((void**)&Bt, (size_t)8 * NP * Kp, a.stream));
-  const uint32_t ipr = (Kp + a.level - 1) / a.level;  // positions per digit row (covers the padding)
-  const uint64_t nd = (uint64_t)Bp * ipr;
-  hipLaunchKernelGGL(ks_digits_i8_kernel, dim3((uint32_t)((nd + 255) / 256)), dim3(256), 0, a.stream, A, a.in,
-                     a.in_idx, a.n_in, a.level, a.base_log, a.num_samples, Kp, ipr);
   hipLaunchKernelGGL(ks_chunks_i8_kernel, dim3((NP + 255) / 256, Kp / 16), dim3(256), 0, a.stream, Bt, a.ksk, K, W, NP,
                      Kp);
-  if (splits > 1) {
-    const uint64_t total = (uint64_t)W * a.num_samples;
-    hipLaunchKernelGGL(keyswitch_zero_kernel, dim3((uint32_t)std::min<uint64_t>((total + 255) / 256, 4096)), dim3(256),
-                       0, a.stream, a.out, a.out_idx, W, a.num_samples);
+  const uint32_t ipr = (Kp + a.level - 1) / a.level;  // positions per digit row (covers the padding)
+  for (uint32_t s0 = 0; s0 < a.num_samples; s0 += chunk) {
+    const uint32_t cn = std::min(chunk, a.num_samples - s0);
+    const uint32_t Bp = (cn + KSM_ROWS - 1) / KSM_ROWS * KSM_ROWS;
+    // this pass's rows: shift the index arrays when given, else the row pointers
+    const uint64_t* in_idx = a.in_idx ? a.in_idx + s0 : nullptr;
+    const uint64_t* out_idx = a.out_idx ? a.out_idx + s0 : nullptr;
+    const uint64_t* in = a.in_idx ? a.in : a.in + (uint64_t)s0 * (a.n_in + 1);
+    uint64_t* out = a.out_idx ? a.out : a.out + (uint64_t)s0 * W;
+    const uint64_t nd = (uint64_t)Bp * ipr;
+    hipLaunchKernelGGL(ks_digits_i8_kernel, dim3((uint32_t)((nd + 255) / 256)), dim3(256), 0, a.stream, A, in, in_idx,
+                       a.n_in, a.level, a.base_log, cn, Kp, ipr);
+    if (splits > 1) {
+      const uint64_t total = (uint64_t)W * cn;
+      hipLaunchKernelGGL(keyswitch_zero_kernel, dim3((uint32_t)std::min<uint64_t>((total + 255) / 256, 4096)),
+                         dim3(256), 0, a.stream, out, out_idx, W, cn);
+    }
+    hipLaunchKernelGGL(ks_mfma_kernel, dim3(NP / KSM_COLS, Bp / KSM_ROWS, splits), dim3(256), 0, a.stream, out, out_idx,
+                       in, in_idx, A, Bt, a.n_in, a.n_out, cn, NP, Kp, k_per_split);
   }
-  hipLaunchKernelGGL(ks_mfma_kernel, dim3(NP / KSM_COLS, Bp / KSM_ROWS, splits), dim3(256), 0, a.stream, a.out,
-                     a.out_idx, a.in, a.in_idx, A, Bt, a.n_in, a.n_out, a.num_samples, NP, Kp, k_per_split);
   hipError_t e = hipGetLastError();
   CHIP_CHECK(hipFreeAsync(A, a.stream));
   CHIP_CHECK(hipFreeAsync(Bt, a.stream));

@@ -381,6 +381,35 @@ def test_keyswitch_mfma_path(B, oracle, torch_cuda, ks_l, ks_logB, nb):
     assert np.array_equal(B.to_host(out2), exp)
 
 
+def test_keyswitch_mfma_multi_pass(B, oracle, torch_cuda, monkeypatch):
+    """The matrix-core keyswitch in several passes over the batch (the digit matrix of one pass
+    is capped; CONCRETE_HIP_KS_CHUNK lowers the cap to 128 rows): 300 samples = 3 passes, with
+    and without index arrays, bit-exact vs the oracle."""
+    p = B.CFG2
+    glwe_sk = B.binary_key(p.big_n, 8701)
+    lwe_sk = B.binary_key(p.n, 8702)
+    ksk = B.ksk_generate(p, glwe_sk, lwe_sk, 8703)
+    rng = np.random.RandomState(8704)
+    nb = 300
+    cts = rng.randint(0, 2 ** 63, size=(nb, p.big_n + 1), dtype=np.int64).astype(np.uint64) * np.uint64(2) + \
+        np.uint64(1)
+    dev = "cuda:0"
+    d_ksk = B.to_device(ksk, dev)
+    op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, ks_l=p.ks_level, ks_logB=p.ks_base_log)
+    ref = oracle.keyswitch_batch(op, cts, ksk)
+    monkeypatch.setenv("CONCRETE_HIP_KS_CHUNK", "128")
+    out = B.keyswitch(p, d_ksk, B.to_device(cts, dev))
+    in_idx = rng.permutation(nb).astype(np.uint64)
+    out_idx = rng.permutation(nb).astype(np.uint64)
+    out2 = B.keyswitch(p, d_ksk, B.to_device(cts, dev), in_idx=B.to_device(in_idx, dev),
+                       out_idx=B.to_device(out_idx, dev))
+    torch_cuda.cuda.synchronize()
+    assert np.array_equal(B.to_host(out), ref)
+    exp = np.zeros_like(ref)
+    exp[out_idx.astype(np.int64)] = ref[in_idx.astype(np.int64)]
+    assert np.array_equal(B.to_host(out2), exp)
+
+
 def test_configs2_total_batch_65536(B, oracle, cfg2, torch_cuda):
     """BASELINE configs[2]'s whole batch (65,536 PBS) in one launch on one GPU: every sample
     decrypts to LUT[m], 8 random rows bit-exact, outputs of identical inputs identical."""

@@ -68,6 +68,14 @@ __device__ __forceinline__ void quad_sync(uint32_t* flags, int ctl, int v, uint3
 #define D4_NOQS 0
 #endif
 
+// The same counters for the two parity waves of one polynomial (v, v ^ 1) only.
+__device__ __forceinline__ void pair_sync2048(uint32_t* flags, int ctl, int v, uint32_t& cnt, const SyncGuard& guard) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  ++cnt;
+  __hip_atomic_store(&flags[ctl * 4 + v], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  spin_until_ge(&flags[ctl * 4 + (v ^ 1)], cnt, guard);
+}
+
 template <bool RESID>
 __global__ void __launch_bounds__(PBS2_CTS * 256, 2)
 pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx,
@@ -177,7 +185,14 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
       for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = A[m];
     }
-    quad_sync(qflags, ctl, v, qcnt, guard);
+    // An even shift keeps every coefficient in its parity class: the sources are my own
+    // scratch, no other wave is involved.  An odd one swaps the classes: the sources are my
+    // parity partner's (v ^ 1) scratch — a pair sync before the reads and one after (before my
+    // next transform overwrites my scratch, which my partner reads).  `at` is the same for all
+    // four waves, so the four sync counters stay equal.
+    const bool odd = (at & 1u) != 0u;
+    if (odd) pair_sync2048(qflags, ctl, v, qcnt, guard);
+    else wave_lds_fence();
     {
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
@@ -188,7 +203,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         st[m] = (uint32_t)decomp_init((sp < N ? rv : 0ull - rv) - A[m], nrep);
       }
     }
-    quad_sync(qflags, ctl, v, qcnt, guard);  // every wave has read its sources: scratches are free again
+    if (odd) pair_sync2048(qflags, ctl, v, qcnt, guard);  // my partner has read my scratch
 
     // ---- one decomposition level, two sub-digit polynomials, forward transforms ----------
     // X[vv][sub][jj]: spectrum of sub-digit polynomial (virtual poly vv = 2 row + parity) at

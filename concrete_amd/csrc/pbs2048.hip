@@ -68,6 +68,23 @@ __device__ __forceinline__ void quad_sync(uint32_t* flags, int ctl, int v, uint3
 #define D4_NOQS 0
 #endif
 
+#ifndef P2_SPLIT_XSYNC
+#define P2_SPLIT_XSYNC 1  // split second sync of the sub-0 exchange (+1.1 %)
+#endif
+// Split form of quad_sync: quad_signal publishes that this wave's reads of the partners'
+// scratches have been issued (LDS operations of a wave execute in order, so the count is seen
+// after them); quad_wait, before this wave next overwrites its scratch, waits for the partners.
+__device__ __forceinline__ void quad_signal(uint32_t* flags, int ctl, int v, uint32_t& cnt) {
+  asm volatile("" ::: "memory");
+  ++cnt;
+  __hip_atomic_store(&flags[ctl * 4 + v], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void quad_wait(uint32_t* flags, int ctl, int v, uint32_t cnt, const SyncGuard& guard) {
+#pragma unroll
+  for (int o = 1; o < 4; ++o) spin_until_ge(&flags[ctl * 4 + ((v + o) & 3)], cnt, guard);
+  asm volatile("" ::: "memory");
+}
+
 // The same counters for the two parity waves of one polynomial (v, v ^ 1) only.
 __device__ __forceinline__ void pair_sync2048(uint32_t* flags, int ctl, int v, uint32_t& cnt, const SyncGuard& guard) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -226,7 +243,20 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
         for (int m = 0; m < 8; ++m)
           vv8[m] = sub == 0 ? cplx{(double)dlo[m], (double)dlo[m + 8]} : cplx{(double)dhi[m], (double)dhi[m + 8]};
+#if P2_SPLIT_XSYNC
+        if (!D4_NOFWD) {
+          cplx tw2[4], tw3[4];
+          fwd_p2_tw(tw2, T, lane >> 3);
+          fwd_p3_tw(tw3, T, lane);
+          // the sub-0 exchange's "everyone has read my spectrum" wait, right before this
+          // transform's first LDS write (the partners signalled right after their reads)
+          fft512_fwd_tw(vv8, xch, lane, tw2, tw3, 0, [&]() __attribute__((always_inline)) {
+            if (sub > 0) quad_wait(qflags, ctl, v, qcnt, guard);
+          });
+        }
+#else
         if (!D4_NOFWD) fft512_fwd(vv8, xch, T, lane);
+#endif
 #pragma unroll
         for (int k2 = 0; k2 < 8; ++k2) xch[k2 * 64 + lane] = vv8[k2];
       }
@@ -246,7 +276,11 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
       }
       // everyone has read my spectrum before my next transform writes the scratch; after the
       // last sub-digit the scratches are next written behind the key windows' barriers
+#if P2_SPLIT_XSYNC
+      if (sub + 1 < PBS2_SUBS) quad_signal(qflags, ctl, v, qcnt);
+#else
       if (sub + 1 < PBS2_SUBS) quad_sync(qflags, ctl, v, qcnt, guard);
+#endif
     }
 
     // ---- per limb: MAC for the four outputs on my quarter, trade quarters, inverse ---------

@@ -835,7 +835,7 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
   // measured 34.1k (33.5k with prefetch) vs 35.9k.  N = 256 with CP = 3 (512 items): 55.4k.
   constexpr int CP = !TILE_GROUPS ? 0 : (M == 128 && K1 == 6 && C == 4) ? TILE128_CP : (M == 512 && K1 == 3 && C == 2) ? 3 : 0;
 #ifndef TILE_GPF
-#define TILE_GPF 1
+#define TILE_GPF 1  // re-measured round 2: 18.8k with (10 VGPRs spilled) vs 18.3k without
 #endif
   constexpr bool GPF = TILE_GPF && M == 512 && CP == 3;  // N = 1024: next-limb key values prefetched (18.5k -> 18.8k)
   constexpr int LCS = M == 128 ? 2 : 1;

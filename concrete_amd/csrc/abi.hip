@@ -15,6 +15,20 @@
 
 namespace chip {
 
+void keep_pool_memory() {
+  static std::atomic<uint64_t> done{0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
+  const uint64_t bit = 1ull << dev;
+  if (done.load(std::memory_order_acquire) & bit) return;
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+    uint64_t thr = ~0ull;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+  }
+  done.fetch_or(bit, std::memory_order_acq_rel);
+}
+
 static thread_local char g_err[512] = "";
 void set_error(const char* fmt, ...) {
   va_list ap;

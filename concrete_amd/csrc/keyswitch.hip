@@ -13,9 +13,15 @@
 #include <type_traits>
 
 #include "common.hpp"
+#include "kernel_util.hpp"
 #include "pbs.hpp"
 
 namespace chip {
+
+// abi.hip: raise the device's default memory-pool release threshold once, so stream-ordered
+// scratch freed by one call stays pooled for the next (each keyswitch call at cfg2 otherwise paid
+// ~0.1 ms of allocation).
+void keep_pool_memory();
 
 constexpr int KS_TILE = 8;
 constexpr int KS_THREADS = 256;
@@ -300,6 +306,103 @@ __global__ void __launch_bounds__(256) ks_mfma_kernel(uint64_t* __restrict__ out
     }
 }
 
+// LDS-staged form (KS_LDS): 8 waves share a 128-sample x 64-word tile; each 64-k block of the
+// tile's operands (digits 8 KB + key bytes 32 KB) is brought into an LDS ring of 3 stages by
+// LDS-DMA (2 stages in flight), so every operand byte crosses L2 -> CU once per workgroup instead
+// of once per wave.  LDS layout of a stage: A[kc][row] and B[c][kc][col], 16-byte cells, kc =
+// 16-byte k chunk: each DMA piece (64 lanes x 16 B) is one (kc, 64 rows / cols) run, and a
+// fragment read (lanes along rows / columns) is conflict-free.
+#ifndef KS_LDS
+#define KS_LDS 1
+#endif
+constexpr int KSL_ROWS = 128, KSL_COLS = 64, KSL_KB = 64, KSL_RS = 3;
+constexpr int KSL_A_CELLS = (KSL_KB / 16) * KSL_ROWS;                 // 512 cells = 8 KB
+constexpr int KSL_STAGE_CELLS = KSL_A_CELLS + 8 * (KSL_KB / 16) * KSL_COLS;  // + 2048 cells = 32 KB
+constexpr int KSL_PIECES = KSL_STAGE_CELLS / 64;                      // 40 DMA pieces per stage
+constexpr int KSL_PPW = KSL_PIECES / 8;                               // 5 per wave
+constexpr size_t KSL_LDS = (size_t)KSL_RS * KSL_STAGE_CELLS * 16;     // 120 KB
+
+__global__ void __launch_bounds__(512) ks_mfma_lds_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx,
+                                                        const uint64_t* __restrict__ in,
+                                                        const uint64_t* __restrict__ in_idx, const int8_t* __restrict__ A,
+                                                        const int8_t* __restrict__ Bt, uint32_t n_in, uint32_t n_out,
+                                                        uint32_t num_samples, uint32_t NP, uint32_t Kp,
+                                                        uint32_t k_per_split) {
+  extern __shared__ __attribute__((aligned(16))) v4i lds[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int rt = w & 3, ct = w >> 2;
+  const uint32_t row_base = blockIdx.y * KSL_ROWS, col_base = blockIdx.x * KSL_COLS;
+  const uint32_t k_begin = blockIdx.z * k_per_split, k_end = min(Kp, k_begin + k_per_split);
+  const uint32_t nst = (k_end - k_begin) / KSL_KB;
+  const bool split = gridDim.z > 1;
+  const uint64_t cstride = (uint64_t)NP * Kp;
+  // this wave's DMA pieces of a stage: global source of its lane and LDS cell offset of the piece
+  const int8_t* src[KSL_PPW];
+  int dst[KSL_PPW];
+#pragma unroll
+  for (int q = 0; q < KSL_PPW; ++q) {
+    const int p = w * KSL_PPW + q;
+    if (p < 8) {  // A: kc = p >> 1, rows 64 (p & 1) .. + 63
+      const int kc = p >> 1, rh = p & 1;
+      src[q] = A + (uint64_t)(row_base + 64 * rh + lane) * Kp + 16 * kc;
+      dst[q] = kc * KSL_ROWS + 64 * rh;
+    } else {  // B: c, kc
+      const int pb = p - 8, c = pb >> 2, kc = pb & 3;
+      src[q] = Bt + c * cstride + (uint64_t)(col_base + lane) * Kp + 16 * kc;
+      dst[q] = KSL_A_CELLS + (c * 4 + kc) * KSL_COLS;
+    }
+  }
+  auto issue = [&](uint32_t t) __attribute__((always_inline)) {
+    const uint32_t kb = k_begin + t * KSL_KB;
+    v4i* stage = lds + (t % KSL_RS) * KSL_STAGE_CELLS;
+#pragma unroll
+    for (int q = 0; q < KSL_PPW; ++q)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[q] + kb), (lds_ptr_t)(stage + dst[q]), 16, 0, 0);
+  };
+  v16i acc[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[c][r] = 0;
+  if (nst > 0) issue(0);
+  if (nst > 1) issue(1);
+  const int r32 = lane & 31, h = lane >> 5;
+  for (uint32_t t = 0; t < nst; ++t) {
+    // stage t landed for this wave (stage t + 1 may stay in flight) ...
+    if (t + 1 < nst) wait_vmcnt<KSL_PPW>();
+    else wait_vmcnt<0>();
+    pair_barrier();  // ... and for every wave; everyone is done with stage t - 1
+    if (t + 2 < nst) issue(t + 2);  // into the slot of stage t - 1
+    const v4i* stage = lds + (t % KSL_RS) * KSL_STAGE_CELLS;
+#pragma unroll
+    for (int s4 = 0; s4 < KSL_KB / 32; ++s4) {
+      const int kc = 2 * s4 + h;
+      const v4i av = stage[kc * KSL_ROWS + 32 * rt + r32];
+      v4i bv[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) bv[c] = stage[KSL_A_CELLS + (c * 4 + kc) * KSL_COLS + 32 * ct + r32];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv[c], acc[c], 0, 0, 0);
+    }
+  }
+  const uint32_t W = n_out + 1;
+  const uint32_t j = col_base + 32 * ct + r32;
+  if (j >= W) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const uint32_t b = row_base + 32 * rt + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (b >= num_samples) continue;
+    uint64_t sum = 0ull;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) sum += (uint64_t)(int64_t)acc[c][r] << (8 * c);
+    uint64_t v = 0ull - sum;
+    if (j == n_out && blockIdx.z == 0) v += in[(in_idx ? in_idx[b] : b) * (uint64_t)(n_in + 1) + n_in];
+    uint64_t* o = out + (out_idx ? out_idx[b] : b) * (uint64_t)W + j;
+    if (split) atomicAdd((unsigned long long*)o, (unsigned long long)v);
+    else *o = v;
+  }
+}
+
 // Whether the MFMA path is exact for these parameters (int8 digits, int32 sums).
 static bool ks_mfma_ok(const KsArgs& a) {
   if (a.base_log > 7) return false;
@@ -319,13 +422,25 @@ static int keyswitch_mfma_launch(const KsArgs& a) {
   const uint32_t chunk = (uint32_t)std::max<uint64_t>(
       KSM_ROWS, std::min<uint64_t>((uint64_t)(a.num_samples + KSM_ROWS - 1) / KSM_ROWS * KSM_ROWS,
                                    cap / KSM_ROWS * KSM_ROWS));
-  // split K until the grid has >= 2 waves per SIMD slot (1 wave per SIMD at 512 registers):
-  // 320 workgroups at cfg2 batch 4096 would leave the second round of the chip a quarter busy
+  // split K over s workgroups so that the rounds of the chip (one workgroup per CU: 512 registers
+  // x 4 waves, or 120 KB of LDS) come out even: time ~ ceil(wgs s / 256) / s, smallest s on ties
+  // (cfg2 batch 4096: 320 workgroups -> s = 4, 5 full rounds)
   const uint32_t wgs = (NP / KSM_COLS) * (chunk / KSM_ROWS);
-  uint32_t splits = std::max<uint32_t>(1, std::min<uint32_t>((2 * 256 + wgs - 1) / wgs, std::min<uint32_t>(8, kb / 4)));
+  uint32_t splits = 1;
+  {
+    double best = 1e30;
+    for (uint32_t sp = 1; sp <= std::min<uint32_t>(8, std::max<uint32_t>(1, kb / 2)); ++sp) {
+      const double t = (double)((wgs * sp + 255) / 256) / sp;
+      if (t < best - 1e-9) best = t, splits = sp;
+    }
+  }
   const uint32_t k_per_split = (kb + splits - 1) / splits * KSM_KB;
   splits = (kb * KSM_KB + k_per_split - 1) / k_per_split;
   const uint32_t Kp = splits * k_per_split;  // zero padded: whole blocks in every split
+  static_assert(KSL_ROWS == KSM_ROWS && KSL_COLS == KSM_COLS && KSL_KB == KSM_KB, "one padding for both kernels");
+  if (KS_LDS) CHIP_CHECK(hipFuncSetAttribute((const void*)ks_mfma_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)KSL_LDS));
+  keep_pool_memory();
   int8_t *A = nullptr, *Bt = nullptr;
   CHIP_CHECK(hipMallocAsync((void**)&A, (size_t)chunk * Kp, a.stream));
   CHIP_CHECK(hipMallocAsync((void**)&Bt, (size_t)8 * NP * Kp, a.stream));
@@ -348,8 +463,12 @@ static int keyswitch_mfma_launch(const KsArgs& a) {
       hipLaunchKernelGGL(keyswitch_zero_kernel, dim3((uint32_t)std::min<uint64_t>((total + 255) / 256, 4096)),
                          dim3(256), 0, a.stream, out, out_idx, W, cn);
     }
-    hipLaunchKernelGGL(ks_mfma_kernel, dim3(NP / KSM_COLS, Bp / KSM_ROWS, splits), dim3(256), 0, a.stream, out, out_idx,
-                       in, in_idx, A, Bt, a.n_in, a.n_out, cn, NP, Kp, k_per_split);
+    if (KS_LDS)
+      hipLaunchKernelGGL(ks_mfma_lds_kernel, dim3(NP / KSL_COLS, Bp / KSL_ROWS, splits), dim3(512), KSL_LDS, a.stream,
+                         out, out_idx, in, in_idx, A, Bt, a.n_in, a.n_out, cn, NP, Kp, k_per_split);
+    else
+      hipLaunchKernelGGL(ks_mfma_kernel, dim3(NP / KSM_COLS, Bp / KSM_ROWS, splits), dim3(256), 0, a.stream, out,
+                         out_idx, in, in_idx, A, Bt, a.n_in, a.n_out, cn, NP, Kp, k_per_split);
   }
   hipError_t e = hipGetLastError();
   CHIP_CHECK(hipFreeAsync(A, a.stream));

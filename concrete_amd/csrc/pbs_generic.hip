@@ -39,6 +39,11 @@
 
 namespace chip {
 
+// abi.hip: raise the device's default memory-pool release threshold once, so stream-ordered
+// scratch freed by one call stays pooled for the next (each keyswitch call at cfg2 otherwise paid
+// ~0.1 ms of allocation).
+void keep_pool_memory();
+
 // ------------------------------------------------------------------------------------------
 // key format and exactness gate (host)
 // ------------------------------------------------------------------------------------------
@@ -1316,6 +1321,7 @@ int pbs_generic_launch(const PbsArgs& a) {
   const uint32_t chunk = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(a.num_samples, 65536),
                                                       std::max<uint64_t>(1, budget / per_ct));
   void* scratch = nullptr;
+  keep_pool_memory();
   CHIP_CHECK(hipMallocAsync(&scratch, per_ct * chunk, a.stream));
   cplx* X = reinterpret_cast<cplx*>(scratch);
   cplx* Y = X + (uint64_t)chunk * K1 * a.level * T * M;

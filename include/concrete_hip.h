@@ -74,7 +74,10 @@ void cuda_programmable_bootstrap_lwe_ciphertext_vector_64(
     uint32_t base_log, uint32_t level_count, uint32_t num_samples, uint32_t num_many_lut, uint32_t lut_stride);
 
 /* lib/Runtime/wrappers.cpp:149-151, GPUDFG.cpp:1098-1101: batched LWE keyswitch; ksk is the
- * standard u64 key [n_in][l][n_out+1] copied verbatim to the device (context.h:117-145). */
+ * standard u64 key [n_in][l][n_out+1] copied verbatim to the device (context.h:117-145).
+ * Exact u64 result.  For base_log <= 7 and >= 64 samples it runs on the int8 matrix cores
+ * (key words split into bytes, exact int32 sums) with stream-ordered scratch: the key bytes
+ * (8 (n_out+1) n_in l B) and the batch's int8 digits (<= 1 GiB per pass). */
 void cuda_keyswitch_lwe_ciphertext_vector_64(void *stream, uint32_t gpu_index, void *lwe_array_out,
                                              void *lwe_output_indexes, void *lwe_array_in,
                                              void *lwe_input_indexes, void *ksk, uint32_t lwe_dimension_in,

@@ -23,6 +23,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# FP64 vector peak: AMD's published MI355X figure (78.6 TFLOP/s; MI355X_MICROARCH.md has no FP64 row).
+# The issue rate measured on gfx950 (~5 cycles per f64 wave-instruction per SIMD)
+# puts the reachable ceiling near 256 CU x 4 SIMD x 64 lanes x 2 flop / 5 cycles x 2.4 GHz = 63 TFLOP/s.
+FP64_PEAK_TFS = 78.6
 METRIC = "PBS/sec (whole node) at N=1024 batch=4096; achieved HBM GB/s"
 
 
@@ -39,17 +43,60 @@ def kernel_source_hash() -> str:
     return h.hexdigest()[:16]
 
 
-def pmc_traffic(batch: int, config: str):
-    """Per-launch HBM bytes from the committed PMC record (tools/pmc_traffic.py) when it was
-    measured on these kernel sources at this batch; else None."""
+def pmc_records(config: str):
+    """Committed PMC records (tools/pmc_record.py, older tools/pmc_traffic.py) measured on these
+    kernel sources for this config, newest first."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pbs_traffic.json")), reverse=True):
+    out = []
+    files = glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")) + \
+        glob.glob(os.path.join(ROOT, "profiles", "*_pbs_traffic.json"))
+    for f in sorted(files, key=os.path.basename, reverse=True):
         with open(f) as fh:
             rec = json.load(fh)
-        if (rec.get("source_hash") == kernel_source_hash() and rec.get("batch") == batch
-                and rec.get("config", "cfg2") == config):
-            return rec["traffic_bytes"], os.path.relpath(f, ROOT)
+        if rec.get("source_hash") == kernel_source_hash() and rec.get("config", "cfg2") == config:
+            rec["src"] = os.path.relpath(f, ROOT)
+            out.append(rec)
+    return out
+
+
+def pmc_traffic(batch: int, config: str):
+    """Per-launch HBM bytes from a committed PMC record measured at this batch; else None."""
+    for rec in pmc_records(config):
+        if rec.get("batch") == batch and "traffic_bytes" in rec:
+            return rec["traffic_bytes"], rec["src"]
     return None, None
+
+
+def pmc_f64_flop(batch: int, config: str):
+    """f64 FLOP per launch from a committed PMC record (SQ f64 instruction mix); the work is per
+    ciphertext, so a record at another batch is scaled by the batch ratio (and says so)."""
+    for rec in pmc_records(config):
+        if "f64_flop" in rec:
+            scale = batch / rec["batch"]
+            return rec["f64_flop"] * scale, rec["src"] + ("" if scale == 1 else f" (scaled from batch {rec['batch']})")
+    return None, None
+
+
+def host_cpus():
+    """CPUs this process may use on this host: the affinity mask, capped by a cgroup CPU quota."""
+    n_aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except Exception:
+        pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    usable = n_aff if quota is None else max(1, min(n_aff, int(quota)))
+    return {"nproc": os.cpu_count(), "affinity": n_aff, "cgroup_quota": quota, "usable": usable, "model": model}
 
 
 def parse():
@@ -60,11 +107,15 @@ def parse():
                          "optB: the optimizer's B-bit row of v0_last_128 (backend.OPTIMIZER_SETS)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=4096, help="PBS per GPU per step")
+    ap.add_argument("--batch", type=int, default=4096, help="PBS per GPU per step (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling: this many PBS per step for the whole job, split over the ranks "
+                         "(e.g. the metric's whole-node batch 4096 = 512 per GPU on 8 GPUs)")
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="PBS in the bounded CPU-baseline sample (default: cfg2 4096 = one full batch, "
                          "cfg4 1024; ~10-20 s)")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the CPU baseline (default: every CPU this job may use on the host)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", type=int, default=8, help="rows checked bit-exactly against the oracle (rank 0)")
     ap.add_argument("--no-ks", action="store_true", help="skip the secondary keyswitch measurement")
@@ -84,6 +135,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    strong = args.global_batch > 0
+    if strong:
+        # contiguous shards of the job's batch (the first global % world ranks get one more)
+        base, extra = divmod(args.global_batch, world)
+        args.batch = base + (1 if rank < extra else 0)
+        if args.batch == 0:
+            raise SystemExit(f"--global-batch {args.global_batch} leaves rank {rank} without work")
     # one process per GPU; CONCRETE_HIP_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
     backend = os.environ.get("CONCRETE_HIP_DIST_BACKEND", "nccl")
     local = local % max(1, torch.cuda.device_count())
@@ -156,16 +214,24 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    total_done = args.batch * args.steps
     if world > 1:
         t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall, kern_ms = float(t[0]), float(t[1])
+        t = torch.tensor([total_done, args.batch], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        total_done, global_batch = int(t[0]), int(t[1])
+    else:
+        global_batch = args.batch
 
     # ---- secondary row: batched keyswitch kN -> n of this batch, after the PBS
     ks_res = None
     if not args.no_ks:
         ksk = B.ksk_generate(p, glwe_sk, lwe_sk, 6)
-        d_ksk = B.to_device(ksk, dev)
+        # allocated the runtime's way (cuda_malloc_async, context.h:134-139): the int8 key bytes of
+        # the matrix-core path are then built once and reused across calls
+        d_ksk = B.RuntimeBuffer(ksk, gpu=local)
         d_small = torch.empty((args.batch, p.n + 1), dtype=torch.int64, device=dev)
         for _ in range(max(1, args.warmup)):
             B.keyswitch(p, d_ksk, d_out, out=d_small)
@@ -198,6 +264,7 @@ def main():
             rows = B.to_host(d_out[: args.verify])
             ks_res["bitexact"] = bool(np.array_equal(B.to_host(d_small[: args.verify]),
                                                      O.keyswitch_batch(op, rows, ksk)))
+        d_ksk.free()
         del d_ksk, d_small
 
     # ---- end-to-end including PCIe: host inputs -> H2D -> PBS -> D2H -> host outputs (DESIGN.md §6;
@@ -218,7 +285,7 @@ def main():
     if world > 1:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        full = D.gather_rows(d_out, args.batch * world, dst=0)
+        full = D.gather_rows(d_out, global_batch, dst=0)
         torch.cuda.synchronize()
         t_gather = time.perf_counter() - t0
         del full
@@ -232,16 +299,27 @@ def main():
         t = torch.tensor([ok], dtype=torch.int64, device=dev)
         dist.all_reduce(t)
         ok_all = int(t.item())
+    cpu_threads = args.cpu_threads or host_cpus()["usable"]
 
     result = None
     if rank == 0:
-        total = args.batch * world * args.steps
-        value = total / wall
+        value = total_done / wall
         bytes_per_pbs = p.bsk_bytes_per_pbs()
         achieved = bytes_per_pbs * args.batch / (kern_ms * 1e-3) / 1e9
         bitexact = None
         cpu = None
         traffic, traffic_src = pmc_traffic(args.batch, args.config)
+        flop, flop_src = pmc_f64_flop(args.batch, args.config)
+        kern_s = kern_ms * 1e-3
+        valu = None if flop is None else {
+            "achieved": round(flop / kern_s / 1e12, 2), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+            "frac": round(flop / kern_s / 1e12 / FP64_PEAK_TFS, 4), "f64_flop_per_launch": flop, "src": flop_src,
+            "note": "f64 FLOP = 64 x (2 FMA + ADD + MUL) wave-instructions (SQ_INSTS_VALU_*_F64) per launch / "
+                    "kernel time; peak = AMD's FP64 vector figure (~63 TFLOP/s at the measured issue rate)"}
+        dram = None if traffic is None else {
+            "achieved": round(traffic / kern_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(traffic / kern_s / 1e9 / HBM_PEAK_GBS, 4),
+            "note": "measured DRAM bytes (roofline.traffic) per launch / kernel time"}
         # the CPU baseline is timed at N = 1 only (a reported baseline, not part of the scaling runs)
         cpu_leg = not args.no_cpu_baseline and world == 1
         if args.verify or cpu_leg:
@@ -260,19 +338,26 @@ def main():
                 kw = {"fbsk": O.bsk_to_fourier(op, bsk)}
                 desc = f"exact-limb f64 FFT restatement, {op.limbs} limbs"
             if args.verify:
-                ref, _ = O.pbs_batch(op, cts[: args.verify], acc[None, :], nthreads=args.cpu_threads, **kw)
+                ref, _ = O.pbs_batch(op, cts[: args.verify], acc[None, :], nthreads=cpu_threads, **kw)
                 bitexact = bool(np.array_equal(ref, out[: args.verify]))
             if cpu_leg:
                 sample = cts[: args.cpu_sample]
                 t1 = time.perf_counter()
-                O.pbs_batch(op, sample, acc[None, :], nthreads=args.cpu_threads, **kw)
+                O.pbs_batch(op, sample, acc[None, :], nthreads=cpu_threads, **kw)
                 dt = time.perf_counter() - t1
-                cpu = {"value": round(len(sample) / dt, 2), "unit": "PBS/s", "cores": args.cpu_threads,
+                hc = host_cpus()
+                work = ("" if opt else " (~3x the MAC / inverse-transform work of concrete-cpu's fft64)"
+                        if op.limbs == 3 else f" (~{op.limbs}x fft64's key-limb work)")
+                cpu = {"value": round(len(sample) / dt, 2), "unit": "PBS/s", "cores": cpu_threads,
                        "kind": "port",
+                       "label": f"concrete-cpu semantics, restated: {desc}{work}",
+                       "host": hc,
                        "sample": f"{len(sample)} PBS of the same {args.config} workload ({desc}, OpenMP over "
-                                 f"ciphertexts), {dt:.2f} s wall"}
+                                 f"ciphertexts on {cpu_threads} threads = every CPU this job may use: affinity "
+                                 f"{hc['affinity']}, cgroup quota {hc['cgroup_quota']}, nproc {hc['nproc']}), "
+                                 f"{dt:.2f} s wall"}
         result = {
-            "metric": METRIC if args.config == "cfg2" else f"PBS/sec (whole node) at N={p.N} batch={args.batch}",
+            "metric": METRIC if args.config == "cfg2" else f"PBS/sec (whole node) at N={p.N} batch={global_batch}",
             "value": round(value, 1),
             "unit": "PBS/s",
             "n_gpus": world,
@@ -280,21 +365,22 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(wall / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "u64",
             "data": f"synthetic (seeded keygen + fresh LWE encryptions of random {width}-bit messages)",
             "config": {"workload": f"batched PBS {args.config}: N={p.N} k={p.k} n={p.n} l={p.level} logB={p.base_log}",
-                       "batch_per_gpu": args.batch, "global_batch": args.batch * world,
+                       "batch_per_gpu": args.batch, "global_batch": global_batch,
                        "parallelism": f"shard{world}", "key_bcast_s": round(t_bcast, 4), "gather_s": round(t_gather, 4),
                        "key_convert_s": round(t_key, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_src": traffic_src,
-                         "kernel_ms": round(kern_ms, 3), "bytes_per_pbs": bytes_per_pbs},
+                         "kernel_ms": round(kern_ms, 3), "bytes_per_pbs": bytes_per_pbs,
+                         "dram": dram, "valu": valu},
             "cpu_baseline": cpu,
             "secondary": {"keyswitch": ks_res,
                           "pcie_inclusive_pbs_per_s": round(e2e * world, 1)},
-            "checks": {"decrypt_ok": f"{ok_all}/{args.batch * world}", "bitexact_rows": args.verify,
+            "checks": {"decrypt_ok": f"{ok_all}/{global_batch}", "bitexact_rows": args.verify,
                        "bitexact": bitexact},
         }
         print(json.dumps(result), flush=True)

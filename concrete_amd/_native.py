@@ -74,6 +74,56 @@ SIGNATURES = {
     "memref_batched_mapped_bootstrap_lwe_hip_u64": (None, [vp, vp, u64, u64, u64, u64, u64, vp, vp, u64, u64, u64, u64,
                                                            u64, vp, vp, u64, u64, u64, u64, u64, u32, u32, u32, u32,
                                                            u32, u32, vp]),
+    "concrete_hip_keyset_set_timing": (None, [vp, i32]),
+    "concrete_hip_keyset_timeline": (u32, [vp, vp, u32]),
+    "concrete_hip_context_bind": (i32, [vp, vp]),
+    "concrete_hip_set_context_resolver": (None, [vp, vp]),
+    "concrete_hip_release_device_buffer": (i32, [vp]),
+    "concrete_hip_encode_expand_lut_device": (i32, [vp, u32, vp, u64, vp, u64, u64, u32, i32]),
+    "concrete_hip_build_accumulators": (i32, [vp, u32, vp, vp, u64, u32, u32]),
+    # the reference's names, context pointer last (wrappers.h:246-300)
+    "memref_keyswitch_lwe_cuda_u64": (None, [vp, vp, u64, u64, u64, vp, vp, u64, u64, u64, u32, u32, u32, u32, u32, vp]),
+    "memref_bootstrap_lwe_cuda_u64": (None, [vp, vp, u64, u64, u64, vp, vp, u64, u64, u64, vp, vp, u64, u64, u64,
+                                             u32, u32, u32, u32, u32, u32, vp]),
+    "memref_batched_keyswitch_lwe_cuda_u64": (None, [vp, vp, u64, u64, u64, u64, u64, vp, vp, u64, u64, u64, u64, u64,
+                                                     u32, u32, u32, u32, u32, vp]),
+    "memref_batched_bootstrap_lwe_cuda_u64": (None, [vp, vp, u64, u64, u64, u64, u64, vp, vp, u64, u64, u64, u64, u64,
+                                                     vp, vp, u64, u64, u64, u32, u32, u32, u32, u32, u32, vp]),
+    "memref_batched_mapped_bootstrap_lwe_cuda_u64": (None, [vp, vp, u64, u64, u64, u64, u64, vp, vp, u64, u64, u64,
+                                                            u64, u64, vp, vp, u64, u64, u64, u64, u64, u32, u32, u32,
+                                                            u32, u32, u32, vp]),
+    # Part 5: stream emulator (stream_emulator_api.h:30-106)
+    "stream_emulator_init": (vp, []),
+    "stream_emulator_run": (None, [vp]),
+    "stream_emulator_delete": (None, [vp]),
+    "stream_emulator_make_memref_add_lwe_ciphertexts_u64_process": (None, [vp, vp, vp, vp]),
+    "stream_emulator_make_memref_add_plaintext_lwe_ciphertext_u64_process": (None, [vp, vp, vp, vp]),
+    "stream_emulator_make_memref_mul_cleartext_lwe_ciphertext_u64_process": (None, [vp, vp, vp, vp]),
+    "stream_emulator_make_memref_negate_lwe_ciphertext_u64_process": (None, [vp, vp, vp]),
+    "stream_emulator_make_memref_keyswitch_lwe_u64_process": (None, [vp, vp, vp, u32, u32, u32, u32, u32, u32, vp]),
+    "stream_emulator_make_memref_bootstrap_lwe_u64_process": (None, [vp, vp, vp, vp, u32, u32, u32, u32, u32, u32, u32,
+                                                                     vp]),
+    "stream_emulator_make_memref_batched_add_lwe_ciphertexts_u64_process": (None, [vp, vp, vp, vp]),
+    "stream_emulator_make_memref_batched_add_plaintext_lwe_ciphertext_u64_process": (None, [vp, vp, vp, vp]),
+    "stream_emulator_make_memref_batched_add_plaintext_cst_lwe_ciphertext_u64_process": (None, [vp, vp, vp, vp]),
+    "stream_emulator_make_memref_batched_mul_cleartext_lwe_ciphertext_u64_process": (None, [vp, vp, vp, vp]),
+    "stream_emulator_make_memref_batched_mul_cleartext_cst_lwe_ciphertext_u64_process": (None, [vp, vp, vp, vp]),
+    "stream_emulator_make_memref_batched_negate_lwe_ciphertext_u64_process": (None, [vp, vp, vp]),
+    "stream_emulator_make_memref_batched_keyswitch_lwe_u64_process": (None, [vp, vp, vp, u32, u32, u32, u32, u32, u32,
+                                                                             vp]),
+    "stream_emulator_make_memref_batched_bootstrap_lwe_u64_process": (None, [vp, vp, vp, vp, u32, u32, u32, u32, u32,
+                                                                             u32, u32, vp]),
+    "stream_emulator_make_memref_batched_mapped_bootstrap_lwe_u64_process": (None, [vp, vp, vp, vp, u32, u32, u32, u32,
+                                                                                    u32, u32, u32, vp]),
+    "stream_emulator_make_uint64_stream": (vp, [C.c_char_p, i32]),
+    "stream_emulator_put_uint64": (None, [vp, u64]),
+    "stream_emulator_get_uint64": (u64, [vp]),
+    "stream_emulator_make_memref_stream": (vp, [C.c_char_p, i32]),
+    "stream_emulator_put_memref": (None, [vp, vp, vp, u64, u64, u64, u64]),
+    "stream_emulator_get_memref": (None, [vp, vp, vp, u64, u64, u64]),
+    "stream_emulator_make_memref_batch_stream": (vp, [C.c_char_p, i32]),
+    "stream_emulator_put_memref_batch": (None, [vp, vp, vp, u64, u64, u64, u64, u64, u64]),
+    "stream_emulator_get_memref_batch": (None, [vp, vp, vp, u64, u64, u64, u64, u64]),
 }
 
 _lib = None

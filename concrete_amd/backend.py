@@ -185,6 +185,39 @@ def _gpu_index(device) -> int:
     return torch.device(device).index or 0
 
 
+class RuntimeBuffer:
+    """A device buffer allocated and filled the way the reference runtime does it
+    (cuda_malloc_async + cuda_memcpy_async_to_gpu, include/concretelang/Runtime/context.h:134-139),
+    released by cuda_drop: the backend sees its lifetime, so derived data (the matrix-core
+    keyswitch's key bytes) may be cached for it.  Has data_ptr() like a torch tensor."""
+
+    def __init__(self, host: np.ndarray, gpu: int = 0):
+        L = _native.lib()
+        host = np.ascontiguousarray(host)
+        self.gpu = gpu
+        self.stream = L.cuda_create_stream(gpu)
+        self.nbytes = host.nbytes
+        self.ptr = L.cuda_malloc_async(self.nbytes, self.stream, gpu)
+        self.write(host)
+
+    def write(self, host: np.ndarray):
+        L = _native.lib()
+        host = np.ascontiguousarray(host)
+        assert host.nbytes == self.nbytes
+        L.cuda_memcpy_async_to_gpu(self.ptr, host.ctypes.data, self.nbytes, self.stream, self.gpu)
+        L.cuda_synchronize_device(self.gpu)
+
+    def data_ptr(self) -> int:
+        return self.ptr
+
+    def free(self):
+        if self.ptr:
+            L = _native.lib()
+            L.cuda_drop(self.ptr, self.gpu)
+            L.cuda_destroy_stream(self.stream, self.gpu)
+            self.ptr = None
+
+
 def pbs_supported(p: PbsParams) -> bool:
     """Whether the kernels take this parameter set (and compute it exactly: pbs.hpp)."""
     return bool(_native.lib().concrete_hip_pbs_supported(p.k, p.N, p.level, p.base_log))

@@ -15,6 +15,16 @@
 
 namespace chip {
 
+// Every stream-ordered allocation of the library (cuda_malloc_async, key-conversion and keyswitch
+// scratch, the general PBS path's spectra) comes from the device's default pool, whose release
+// threshold is raised to "never" before the first one: freed blocks stay mapped and are reused.
+// Measured on gfx950 / ROCm 7.2 (tools/microbench/pool_copy.hip): with the default threshold (0) the
+// pool hands memory back to the driver at each synchronisation, and a later allocation of >= ~20 MB
+// on the same stream then reads / writes stale pages — 19 of 20 rounds of "allocate, H2D copy,
+// kernel, D2H, free, sync" returned wrong data, pinned or pageable, async or blocking copies; with
+// the threshold raised, 0 of 20.  The cost: the pool keeps the library's peak stream-ordered usage
+// (e.g. <= 1 GiB of keyswitch digits per pass, <= 2 GB of general-path spectra) reserved for the
+// process; trimming it (hipMemPoolTrimTo) would bring the failure back, so it is not offered.
 void keep_pool_memory() {
   static std::atomic<uint64_t> done{0};
   int dev = 0;
@@ -88,12 +98,15 @@ int take_device_status(int gpu) {
     w = (gpu >= 0 && gpu < STATUS_MAX_DEV) ? g_status[gpu] : nullptr;
   }
   if (!w) return 0;  // no PBS kernel has run on this device
+  int prev = 0;
+  CHIP_CHECK(hipGetDevice(&prev));  // the caller's current device is restored (torch shares it)
   CHIP_CHECK(hipSetDevice(gpu));
   CHIP_CHECK(hipDeviceSynchronize());
   uint32_t v = 0;
   CHIP_CHECK(hipMemcpy(&v, w, sizeof v, hipMemcpyDeviceToHost));
+  if (v != 0) CHIP_CHECK(hipMemset(w, 0, sizeof(uint32_t)));
+  CHIP_CHECK(hipSetDevice(prev));
   if (v == 0) return 0;
-  CHIP_CHECK(hipMemset(w, 0, sizeof(uint32_t)));
   if (v & DEV_STATUS_SYNC_TIMEOUT) {
     set_error("device %d: a PBS wave synchronisation exceeded its spin bound; that launch's outputs are wrong",
               gpu);
@@ -129,13 +142,16 @@ void* cuda_malloc_async(uint64_t size, void* stream, uint32_t gpu_index) {
   set_device(gpu_index);
   void* p = nullptr;
   if (size == 0) return nullptr;
+  keep_pool_memory();
   CHIP_CHECK(hipMallocAsync(&p, size, (hipStream_t)stream));
+  track_device_buffer(p);
   return p;
 }
 
 void cuda_memcpy_async_to_gpu(void* dest, void* src, uint64_t size, void* stream, uint32_t gpu_index) {
   if (size == 0) return;
   set_device(gpu_index);
+  release_key_bytes(dest, nullptr, false);  // new contents: derived key bytes are stale
   CHIP_CHECK(hipMemcpyAsync(dest, src, size, hipMemcpyHostToDevice, (hipStream_t)stream));
 }
 
@@ -162,6 +178,7 @@ void cuda_drop(void* ptr, uint32_t gpu_index) {
   if (!ptr) return;
   set_device(gpu_index);
   release_registered(ptr);
+  release_key_bytes(ptr, nullptr, true);
   CHIP_CHECK(hipFree(ptr));
 }
 
@@ -169,7 +186,14 @@ void cuda_drop_async(void* ptr, void* stream, uint32_t gpu_index) {
   if (!ptr) return;
   set_device(gpu_index);
   release_registered(ptr);
+  release_key_bytes(ptr, (hipStream_t)stream, true);
   CHIP_CHECK(hipFreeAsync(ptr, (hipStream_t)stream));
+}
+
+int concrete_hip_release_device_buffer(const void* ptr) {
+  if (!ptr) return 0;
+  release_registered((void*)ptr);
+  return release_key_bytes(ptr, nullptr, false);
 }
 
 void cuda_synchronize_device(uint32_t gpu_index) {
@@ -183,7 +207,7 @@ void cuda_synchronize_device(uint32_t gpu_index) {
 // ----------------------------------------------------------------------------------------
 // extensions
 // ----------------------------------------------------------------------------------------
-uint32_t concrete_hip_abi_version(void) { return 1u; }
+uint32_t concrete_hip_abi_version(void) { return 2u; }
 const char* concrete_hip_last_error(void) { return last_error(); }
 int concrete_hip_device_status(uint32_t gpu_index) { return take_device_status((int)gpu_index); }
 
@@ -244,6 +268,7 @@ int concrete_hip_convert_bsk(void* stream, uint32_t gpu_index, void* dest_fourie
       (uint64_t)input_lwe_dim * level_count * (glwe_dim + 1) * (glwe_dim + 1) * polynomial_size * 8ull;
   const uint64_t* src_dev = (const uint64_t*)src;
   void* tmp = nullptr;
+  keep_pool_memory();
   if (!src_is_device) {
     CHIP_CHECK(hipMallocAsync(&tmp, std_bytes, s));
     CHIP_CHECK(hipMemcpyAsync(tmp, src, std_bytes, hipMemcpyHostToDevice, s));
@@ -365,6 +390,7 @@ void scratch_cuda_programmable_bootstrap_64(void* stream, uint32_t gpu_index, in
     return;
   }
   set_device(gpu_index);
+  keep_pool_memory();
   void* p = nullptr;
   CHIP_CHECK(hipMallocAsync(&p, 256, (hipStream_t)stream));
   CHIP_CHECK(hipMemsetAsync(p, 0, 256, (hipStream_t)stream));

@@ -22,6 +22,8 @@
 
 namespace chip {
 
+void keep_pool_memory();  // abi.hip: the default pool never releases (see there)
+
 struct dd {
   double hi, lo;
 };
@@ -215,6 +217,7 @@ int convert_bsk_launch(const ConvertArgs& a) {
   std::vector<ddc> zeta, tw;
   make_tables(1024, zeta, tw);  // both paths transform N = 1024 negacyclic polynomials
   ddc *dz = nullptr, *dt = nullptr;
+  keep_pool_memory();
   CHIP_CHECK(hipMallocAsync((void**)&dz, zeta.size() * sizeof(ddc), a.stream));
   CHIP_CHECK(hipMallocAsync((void**)&dt, tw.size() * sizeof(ddc), a.stream));
   CHIP_CHECK(hipMemcpyAsync(dz, zeta.data(), zeta.size() * sizeof(ddc), hipMemcpyHostToDevice, a.stream));

@@ -10,7 +10,10 @@
 // is read once per tile with 2 KB coalesced loads and applied to all KS_TILE samples, so
 // the 20.7 MB (cfg2) key is streamed B / KS_TILE times instead of B times.
 #include <algorithm>
+#include <mutex>
 #include <type_traits>
+#include <unordered_set>
+#include <vector>
 
 #include "common.hpp"
 #include "kernel_util.hpp"
@@ -18,9 +21,8 @@
 
 namespace chip {
 
-// abi.hip: raise the device's default memory-pool release threshold once, so stream-ordered
-// scratch freed by one call stays pooled for the next (each keyswitch call at cfg2 otherwise paid
-// ~0.1 ms of allocation).
+// abi.hip: raise the device's default memory-pool release threshold once (released and re-reserved
+// pool memory reads stale data on this stack; pooled scratch also saves ~0.1 ms per call at cfg2).
 void keep_pool_memory();
 
 constexpr int KS_TILE = 8;
@@ -171,8 +173,8 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
 //     S_c = A B_c   (|S_c| <= K 2^(logB-1) 128 < 2^31, checked by the host)
 // are exact on the i8 matrix cores (v_mfma_i32_32x32x32_i8), and
 //     out[b][j] = (j == n_out ? b_in : 0) - sum_c 2^{8c} S_c[b][j]   (mod 2^64)
-// is the keyswitch bit for bit.  Operands are K-contiguous rows (digits [Bp][Kp], key chunks
-// [8][NP][Kp], zero padded); A and B fragments use the same lane/element -> k map, so the
+// is the keyswitch bit for bit.  Operands are K-contiguous rows (digits [Bp][Ks], key chunks
+// [8][NP][Ks], zero padded; a launch sums k < Kp <= Ks); A and B fragments use the same lane/element -> k map, so the
 // products sum over exactly the k of each step whatever order the hardware gives them.
 // ------------------------------------------------------------------------------------------
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -184,7 +186,7 @@ constexpr int KSM_KB = 64;     // K per register block (Kp is padded to a multip
 __global__ void __launch_bounds__(256) ks_digits_i8_kernel(int8_t* __restrict__ A, const uint64_t* __restrict__ in,
                                                          const uint64_t* __restrict__ in_idx, uint32_t n_in,
                                                          uint32_t level, uint32_t base_log, uint32_t num_samples,
-                                                         uint32_t Kp, uint32_t ipr) {
+                                                         uint32_t Ks, uint32_t ipr) {
   // thread = (sample row b, mask position i); rows past the batch and positions past n_in: zeros
   const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint32_t b = (uint32_t)(g / ipr), i = (uint32_t)(g % ipr);
@@ -192,18 +194,18 @@ __global__ void __launch_bounds__(256) ks_digits_i8_kernel(int8_t* __restrict__ 
   uint64_t a = 0ull;
   if (b < num_samples && i < n_in) a = in[(in_idx ? in_idx[b] : b) * (uint64_t)(n_in + 1) + i];
   uint64_t st = decomp_init(a, nrep);
-  int8_t* row = A + (uint64_t)b * Kp;
+  int8_t* row = A + (uint64_t)b * Ks;
   for (uint32_t t = 0; t < level; ++t) {
     const int8_t d = (int8_t)decomp_next64(st, (int)base_log);
     const uint32_t k = i * level + t;
-    if (k < Kp) row[k] = d;
+    if (k < Ks) row[k] = d;
   }
 }
 
 // thread = (output word j, 16 consecutive KSK rows): 16 coalesced u64 reads (lanes along j),
 // then one 16-byte store per chunk c into B_c[j][k0 .. k0 + 15]
 __global__ void __launch_bounds__(256) ks_chunks_i8_kernel(int8_t* __restrict__ Bt, const uint64_t* __restrict__ ksk,
-                                                         uint32_t K, uint32_t W, uint32_t NP, uint32_t Kp) {
+                                                         uint32_t K, uint32_t W, uint32_t NP, uint32_t Ks) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t k0 = blockIdx.y * 16;
   if (j >= NP) return;
@@ -221,7 +223,7 @@ __global__ void __launch_bounds__(256) ks_chunks_i8_kernel(int8_t* __restrict__ 
   }
 #pragma unroll
   for (int c = 0; c < 8; ++c)
-    *reinterpret_cast<uint4*>(Bt + ((uint64_t)c * NP + j) * Kp + k0) = make_uint4(w[c][0], w[c][1], w[c][2], w[c][3]);
+    *reinterpret_cast<uint4*>(Bt + ((uint64_t)c * NP + j) * Ks + k0) = make_uint4(w[c][0], w[c][1], w[c][2], w[c][3]);
 }
 
 // one wave = 64 samples (two 32-row tiles) x 32 output words, all 8 chunks: 16 int32
@@ -234,7 +236,7 @@ __global__ void __launch_bounds__(256) ks_mfma_kernel(uint64_t* __restrict__ out
                                                     const uint64_t* __restrict__ in, const uint64_t* __restrict__ in_idx,
                                                     const int8_t* __restrict__ A, const int8_t* __restrict__ Bt,
                                                     uint32_t n_in, uint32_t n_out, uint32_t num_samples, uint32_t NP,
-                                                    uint32_t Kp, uint32_t k_per_split) {
+                                                    uint32_t Kp, uint32_t Ks, uint32_t k_per_split) {
   constexpr int RT = 2, SPB = KSM_KB / 32;  // row tiles per wave, MFMA k-steps per block
   // split-K (gridDim.z > 1): this workgroup sums k in [k_begin, k_end) and adds its partial
   // result into pre-zeroed outputs with 64-bit atomics (wrapping addition: exact, order-free);
@@ -243,9 +245,9 @@ __global__ void __launch_bounds__(256) ks_mfma_kernel(uint64_t* __restrict__ out
   const bool split = gridDim.z > 1;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t row0 = blockIdx.y * KSM_ROWS + 64 * (w >> 1), col0 = blockIdx.x * KSM_COLS + 32 * (w & 1);
-  const int8_t* ap = A + (uint64_t)(row0 + (lane & 31)) * Kp + (KSM_KB / 2) * (lane >> 5);
-  const int8_t* bp = Bt + (uint64_t)(col0 + (lane & 31)) * Kp + (KSM_KB / 2) * (lane >> 5);
-  const uint64_t cstride = (uint64_t)NP * Kp, rstride = 32ull * Kp;
+  const int8_t* ap = A + (uint64_t)(row0 + (lane & 31)) * Ks + (KSM_KB / 2) * (lane >> 5);
+  const int8_t* bp = Bt + (uint64_t)(col0 + (lane & 31)) * Ks + (KSM_KB / 2) * (lane >> 5);
+  const uint64_t cstride = (uint64_t)NP * Ks, rstride = 32ull * Ks;
   v16i acc[RT][8];
 #pragma unroll
   for (int t = 0; t < RT; ++t)
@@ -327,7 +329,7 @@ __global__ void __launch_bounds__(512) ks_mfma_lds_kernel(uint64_t* __restrict__
                                                         const uint64_t* __restrict__ in_idx, const int8_t* __restrict__ A,
                                                         const int8_t* __restrict__ Bt, uint32_t n_in, uint32_t n_out,
                                                         uint32_t num_samples, uint32_t NP, uint32_t Kp,
-                                                        uint32_t k_per_split) {
+                                                        uint32_t Ks, uint32_t k_per_split) {
   extern __shared__ __attribute__((aligned(16))) v4i lds[];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int rt = w & 3, ct = w >> 2;
@@ -335,7 +337,7 @@ __global__ void __launch_bounds__(512) ks_mfma_lds_kernel(uint64_t* __restrict__
   const uint32_t k_begin = blockIdx.z * k_per_split, k_end = min(Kp, k_begin + k_per_split);
   const uint32_t nst = (k_end - k_begin) / KSL_KB;
   const bool split = gridDim.z > 1;
-  const uint64_t cstride = (uint64_t)NP * Kp;
+  const uint64_t cstride = (uint64_t)NP * Ks;
   // this wave's DMA pieces of a stage: global source of its lane and LDS cell offset of the piece
   const int8_t* src[KSL_PPW];
   int dst[KSL_PPW];
@@ -344,11 +346,11 @@ __global__ void __launch_bounds__(512) ks_mfma_lds_kernel(uint64_t* __restrict__
     const int p = w * KSL_PPW + q;
     if (p < 8) {  // A: kc = p >> 1, rows 64 (p & 1) .. + 63
       const int kc = p >> 1, rh = p & 1;
-      src[q] = A + (uint64_t)(row_base + 64 * rh + lane) * Kp + 16 * kc;
+      src[q] = A + (uint64_t)(row_base + 64 * rh + lane) * Ks + 16 * kc;
       dst[q] = kc * KSL_ROWS + 64 * rh;
     } else {  // B: c, kc
       const int pb = p - 8, c = pb >> 2, kc = pb & 3;
-      src[q] = Bt + c * cstride + (uint64_t)(col_base + lane) * Kp + 16 * kc;
+      src[q] = Bt + c * cstride + (uint64_t)(col_base + lane) * Ks + 16 * kc;
       dst[q] = KSL_A_CELLS + (c * 4 + kc) * KSL_COLS;
     }
   }
@@ -403,19 +405,114 @@ __global__ void __launch_bounds__(512) ks_mfma_lds_kernel(uint64_t* __restrict__
   }
 }
 
-// Whether the MFMA path is exact for these parameters (int8 digits, int32 sums).
+// Whether the MFMA path is exact for these parameters (int8 digits, int32 sums): a sum has K =
+// n_in l products of |d| <= 2^(logB-1) and |k_c| <= 128 (the zero padding adds nothing).
 static bool ks_mfma_ok(const KsArgs& a) {
   if (a.base_log > 7) return false;
   const uint64_t K = (uint64_t)a.n_in * a.level;
-  const uint64_t Kp = (K + 8 * KSM_KB - 1) / (8 * KSM_KB) * (8 * KSM_KB);  // worst split padding
-  return Kp * (1ull << (a.base_log - 1)) * 128ull <= 0x7fffffffull;
+  return K * (1ull << (a.base_log - 1)) * 128ull <= 0x7fffffffull;
+}
+
+// Key bytes B_c of a KSK, [8][NP][Ks] int8 (zero padded in j and k), built from the caller's u64 key.
+// Cached per (key pointer, device, shape) so that the runtime's repeated keyswitches with one key
+// (context.h:117-145 uploads it once) split it once — but only for buffers whose lifetime the
+// backend sees: allocated by cuda_malloc_async (how the runtime allocates its KSK, context.h:134)
+// or by the keyset (runtime.hip).  cuda_drop / cuda_drop_async / a cuda_memcpy_async_to_gpu onto the
+// buffer release the entry (concrete_hip_release_device_buffer).  Any other pointer (e.g. memory of
+// a caching allocator, which hands the same address to the next tensor) gets fresh key bytes on
+// every call.  CONCRETE_HIP_KS_KEY_CACHE=0 disables the cache.
+struct KeyBytes {
+  const uint64_t* ksk;
+  int dev;
+  uint32_t K, W, NP, Ks;
+  int8_t* bt;
+  hipEvent_t built;  // other streams wait on the build
+};
+static std::mutex g_kb_mu;
+static std::vector<KeyBytes> g_kb;
+static std::unordered_set<const void*> g_tracked;  // buffers whose release the backend sees
+
+void track_device_buffer(const void* p) {
+  std::lock_guard<std::mutex> g(g_kb_mu);
+  g_tracked.insert(p);
+}
+
+static bool key_cache_on() {
+  static const bool on = !getenv("CONCRETE_HIP_KS_KEY_CACHE") || atoi(getenv("CONCRETE_HIP_KS_KEY_CACHE")) != 0;
+  return on;
+}
+
+// nullptr when the device memory could not be allocated (the caller falls back to the VALU kernel)
+static int8_t* key_bytes(const KsArgs& a, uint32_t K, uint32_t W, uint32_t NP, uint32_t Ks, bool& owned) {
+  int dev = 0;
+  CHIP_CHECK(hipGetDevice(&dev));
+  keep_pool_memory();
+  bool cache = key_cache_on();
+  if (cache) {
+    std::lock_guard<std::mutex> g(g_kb_mu);
+    cache = g_tracked.count(a.ksk) > 0;
+  }
+  std::unique_lock<std::mutex> lk(g_kb_mu, std::defer_lock);
+  if (cache) {
+    lk.lock();
+    for (const KeyBytes& e : g_kb)
+      if (e.ksk == a.ksk && e.dev == dev && e.K == K && e.W == W && e.NP == NP && e.Ks == Ks) {
+        CHIP_CHECK(hipStreamWaitEvent(a.stream, e.built, 0));
+        owned = false;
+        return e.bt;
+      }
+  }
+  int8_t* bt = nullptr;
+  const size_t bytes = (size_t)8 * NP * Ks;
+  if ((cache ? hipMalloc((void**)&bt, bytes) : hipMallocAsync((void**)&bt, bytes, a.stream)) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  hipLaunchKernelGGL(ks_chunks_i8_kernel, dim3((NP + 255) / 256, Ks / 16), dim3(256), 0, a.stream, bt, a.ksk, K, W,
+                     NP, Ks);
+  owned = !cache;
+  if (cache) {
+    KeyBytes e{a.ksk, dev, K, W, NP, Ks, bt, nullptr};
+    CHIP_CHECK(hipEventCreateWithFlags(&e.built, hipEventDisableTiming));
+    CHIP_CHECK(hipEventRecord(e.built, a.stream));
+    g_kb.push_back(e);
+  }
+  return bt;
+}
+
+// drop the cached key bytes derived from device buffer `p` (any device); returns how many.
+// untrack: p is being freed (its address may come back for other data)
+int release_key_bytes(const void* p, hipStream_t s, bool untrack) {
+  std::vector<KeyBytes> gone;
+  {
+    std::lock_guard<std::mutex> g(g_kb_mu);
+    if (untrack) g_tracked.erase(p);
+    for (auto it = g_kb.begin(); it != g_kb.end();)
+      if ((const void*)it->ksk == p) {
+        gone.push_back(*it);
+        it = g_kb.erase(it);
+      } else {
+        ++it;
+      }
+  }
+  int prev = 0;
+  if (!gone.empty()) CHIP_CHECK(hipGetDevice(&prev));
+  for (KeyBytes& e : gone) {
+    CHIP_CHECK(hipSetDevice(e.dev));
+    if (s) CHIP_CHECK(hipFreeAsync(e.bt, s));
+    else CHIP_CHECK(hipFree(e.bt));
+    CHIP_CHECK(hipEventDestroy(e.built));
+  }
+  if (!gone.empty()) CHIP_CHECK(hipSetDevice(prev));
+  return (int)gone.size();
 }
 
 static int keyswitch_mfma_launch(const KsArgs& a) {
   const uint32_t W = a.n_out + 1, NP = (W + KSM_COLS - 1) / KSM_COLS * KSM_COLS;
   const uint32_t K = a.n_in * a.level, kb = (K + KSM_KB - 1) / KSM_KB;
-  // samples per pass: the int8 digit matrix of a pass stays <= 1 GiB (8-bit rows: K = 81,920)
-  const uint64_t kmax = (uint64_t)(kb + 7) / 8 * 8 * KSM_KB;
+  // samples per pass: the int8 digit matrix of a pass stays <= 1 GiB (8-bit rows: K = 81,920);
+  // rows are Ks = (kb + 7) KSM_KB bytes apart (below)
+  const uint64_t kmax = (uint64_t)(kb + 7) * KSM_KB;
   // (CONCRETE_HIP_KS_CHUNK: a smaller pass size, read per call — the multi-pass test uses it)
   const char* cap_env = getenv("CONCRETE_HIP_KS_CHUNK");
   const uint64_t cap = cap_env && atoll(cap_env) > 0 ? (uint64_t)atoll(cap_env) : (1ull << 30) / kmax;
@@ -437,16 +534,26 @@ static int keyswitch_mfma_launch(const KsArgs& a) {
   const uint32_t k_per_split = (kb + splits - 1) / splits * KSM_KB;
   splits = (kb * KSM_KB + k_per_split - 1) / k_per_split;
   const uint32_t Kp = splits * k_per_split;  // zero padded: whole blocks in every split
+  // operand row stride: covers the padding of any split count (<= 8), so one key-byte layout
+  // serves every batch size
+  const uint32_t Ks = (kb + 7) * KSM_KB;
   static_assert(KSL_ROWS == KSM_ROWS && KSL_COLS == KSM_COLS && KSL_KB == KSM_KB, "one padding for both kernels");
   if (KS_LDS) CHIP_CHECK(hipFuncSetAttribute((const void*)ks_mfma_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                              (int)KSL_LDS));
   keep_pool_memory();
-  int8_t *A = nullptr, *Bt = nullptr;
-  CHIP_CHECK(hipMallocAsync((void**)&A, (size_t)chunk * Kp, a.stream));
-  CHIP_CHECK(hipMallocAsync((void**)&Bt, (size_t)8 * NP * Kp, a.stream));
-  hipLaunchKernelGGL(ks_chunks_i8_kernel, dim3((NP + 255) / 256, Kp / 16), dim3(256), 0, a.stream, Bt, a.ksk, K, W, NP,
-                     Kp);
-  const uint32_t ipr = (Kp + a.level - 1) / a.level;  // positions per digit row (covers the padding)
+  // test hook: refuse operand scratch above this many bytes (the VALU fallback then runs)
+  if (const char* lim = getenv("CONCRETE_HIP_KS_SCRATCH_LIMIT"))
+    if ((uint64_t)chunk * Ks + 8ull * NP * Ks > strtoull(lim, nullptr, 10)) return -5;
+  bool bt_owned = false;
+  int8_t* Bt = key_bytes(a, K, W, NP, Ks, bt_owned);
+  int8_t* A = nullptr;
+  if (!Bt || hipMallocAsync((void**)&A, (size_t)chunk * Ks, a.stream) != hipSuccess) {
+    // not enough device memory for the matrix-core operands: the scratch-free VALU kernel
+    (void)hipGetLastError();
+    if (Bt && bt_owned) CHIP_CHECK(hipFreeAsync(Bt, a.stream));
+    return -5;
+  }
+  const uint32_t ipr = (Ks + a.level - 1) / a.level;  // positions per digit row (covers the padding)
   for (uint32_t s0 = 0; s0 < a.num_samples; s0 += chunk) {
     const uint32_t cn = std::min(chunk, a.num_samples - s0);
     const uint32_t Bp = (cn + KSM_ROWS - 1) / KSM_ROWS * KSM_ROWS;
@@ -457,7 +564,7 @@ static int keyswitch_mfma_launch(const KsArgs& a) {
     uint64_t* out = a.out_idx ? a.out : a.out + (uint64_t)s0 * W;
     const uint64_t nd = (uint64_t)Bp * ipr;
     hipLaunchKernelGGL(ks_digits_i8_kernel, dim3((uint32_t)((nd + 255) / 256)), dim3(256), 0, a.stream, A, in, in_idx,
-                       a.n_in, a.level, a.base_log, cn, Kp, ipr);
+                       a.n_in, a.level, a.base_log, cn, Ks, ipr);
     if (splits > 1) {
       const uint64_t total = (uint64_t)W * cn;
       hipLaunchKernelGGL(keyswitch_zero_kernel, dim3((uint32_t)std::min<uint64_t>((total + 255) / 256, 4096)),
@@ -465,14 +572,14 @@ static int keyswitch_mfma_launch(const KsArgs& a) {
     }
     if (KS_LDS)
       hipLaunchKernelGGL(ks_mfma_lds_kernel, dim3(NP / KSL_COLS, Bp / KSL_ROWS, splits), dim3(512), KSL_LDS, a.stream,
-                         out, out_idx, in, in_idx, A, Bt, a.n_in, a.n_out, cn, NP, Kp, k_per_split);
+                         out, out_idx, in, in_idx, A, Bt, a.n_in, a.n_out, cn, NP, Kp, Ks, k_per_split);
     else
       hipLaunchKernelGGL(ks_mfma_kernel, dim3(NP / KSM_COLS, Bp / KSM_ROWS, splits), dim3(256), 0, a.stream, out,
-                         out_idx, in, in_idx, A, Bt, a.n_in, a.n_out, cn, NP, Kp, k_per_split);
+                         out_idx, in, in_idx, A, Bt, a.n_in, a.n_out, cn, NP, Kp, Ks, k_per_split);
   }
   hipError_t e = hipGetLastError();
   CHIP_CHECK(hipFreeAsync(A, a.stream));
-  CHIP_CHECK(hipFreeAsync(Bt, a.stream));
+  if (bt_owned) CHIP_CHECK(hipFreeAsync(Bt, a.stream));
   if (e != hipSuccess) {
     set_error("keyswitch launch failed: %s", hipGetErrorString(e));
     return -1;
@@ -489,7 +596,10 @@ int keyswitch_launch(const KsArgs& a) {
   const uint32_t blocks = (a.num_samples + KS_TILE - 1) / KS_TILE;
   if (blocks == 0) return 0;
   static const int ks_path = getenv("CONCRETE_HIP_KS_PATH") ? atoi(getenv("CONCRETE_HIP_KS_PATH")) : -1;
-  if (ks_path != 0 && ks_mfma_ok(a) && (ks_path == 1 || a.num_samples >= KS_MFMA_MIN_BATCH)) return keyswitch_mfma_launch(a);
+  if (ks_path != 0 && ks_mfma_ok(a) && (ks_path == 1 || a.num_samples >= KS_MFMA_MIN_BATCH)) {
+    const int rc = keyswitch_mfma_launch(a);
+    if (rc != -5) return rc;  // -5: operand memory unavailable, run the VALU kernel below
+  }
   const uint32_t U = (a.n_out + 1 + KS_THREADS - 1) / KS_THREADS;
   // enough workgroups for 256 CUs: split the mask positions when the batch alone is short
   uint32_t splits = 1;

@@ -125,5 +125,11 @@ struct KsArgs {
   uint32_t n_in, n_out, base_log, level, num_samples;
 };
 int keyswitch_launch(const KsArgs& a);
+// keyswitch.hip: drop the int8 key bytes cached for the KSK at device pointer p (freed on stream s,
+// or synchronously when s is null; untrack when p itself is being freed); returns the number of
+// entries released.  track_device_buffer: p's lifetime is visible to the backend (cuda_malloc_async,
+// keyset keys), so key bytes derived from it may be cached.
+int release_key_bytes(const void* p, hipStream_t s, bool untrack);
+void track_device_buffer(const void* p);
 
 }  // namespace chip

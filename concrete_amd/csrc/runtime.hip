@@ -1,59 +1,47 @@
-// runtime.hip — circuit-facing runtime glue (SURVEY.md §8b layer B2), host code.
+// runtime.hip — circuit-facing runtime glue (SURVEY.md §8b layer B2, direct GPU route), host code.
 //
-// Mirrors the memref wrappers the compiled circuit calls on the direct GPU route
-// (compiler include/concretelang/Runtime/wrappers.h:240-300; lib/Runtime/wrappers.cpp:88-363)
-// with the same memref-descriptor arguments and shape assertions, over an opaque keyset that
-// plays the part of RuntimeContext's key caches (include/concretelang/Runtime/context.h:86-145):
+// Mirrors the memref wrappers a compiled circuit calls on the direct GPU route
+// (compiler include/concretelang/Runtime/wrappers.h:240-300; lib/Runtime/wrappers.cpp:70-363)
+// with the same memref-descriptor arguments and shape assertions, over a keyset that plays the
+// part of RuntimeContext's key caches (include/concretelang/Runtime/context.h:86-145):
 //   * keys are registered once in standard form (host copies);
 //   * per device, the Fourier key is produced on first use under double-checked locking
 //     (context.h:90-115) — converted on the first device that needs it and peer-copied to the
 //     others — and stays resident for every later call;
-//   * a batched call is split into contiguous slices over the keyset's device list, one stream
-//     per slice, all slices in flight before the single synchronisation.
-#include <algorithm>
-#include <mutex>
-#include <vector>
+//   * a batched call is split into contiguous slices over the keyset's device list and every
+//     slice runs on its own host thread (as the reference's per-device scheduler threads,
+//     GPUDFG.cpp:852-895), on a stream and device buffers cached per slice slot across calls:
+//     slice r + 1's copies and kernel are issued while slice r's are in flight;
+//   * accumulators are built on the device from the LUT rows (lut.hip), so only N words per LUT
+//     cross PCIe instead of the (k+1)N-word trivial GLWE (wrappers.cpp:199-209).
+// Copies from / to the caller's (pageable) memory use the blocking hipMemcpyWithStream: HIP stages
+// pageable copies, and the staged tail of an asynchronous D2H was seen to land after
+// hipStreamSynchronize had returned (sdfg.hip); each slice's thread blocks on its own copies only.
+// Two name sets: memref_*_hip_u64 take the keyset handle itself; memref_*_cuda_u64 carry the
+// reference names and take the caller's runtime context pointer, resolved to a keyset through
+// concrete_hip_context_bind / concrete_hip_set_context_resolver.
+#include <stdarg.h>
 
-#include "../../include/concrete_hip.h"
+#include <algorithm>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+
 #include "common.hpp"
 #include "pbs.hpp"
+#include "runtime.hpp"
 
-using namespace chip;
+namespace chip {
 
-namespace {
-
-constexpr int MAX_DEV = 16;
-
-[[noreturn]] void die(const char* what) {
-  fprintf(stderr, "concrete-hip runtime: %s\n", what);
+void rt_die(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  fprintf(stderr, "concrete-hip runtime: ");
+  vfprintf(stderr, fmt, ap);
+  fprintf(stderr, "\n");
+  va_end(ap);
   abort();
 }
-#define RT_ASSERT(cond)                                     \
-  do {                                                      \
-    if (!(cond)) die("assertion failed: " #cond);           \
-  } while (0)
-
-struct BskEntry {
-  std::vector<uint64_t> host;
-  uint32_t n = 0, k = 0, level = 0, base_log = 0, N = 0;
-  void* dev[MAX_DEV] = {};
-  std::mutex m;
-};
-struct KskEntry {
-  std::vector<uint64_t> host;
-  uint32_t level = 0, base_log = 0, n_in = 0, n_out = 0;
-  void* dev[MAX_DEV] = {};
-  std::mutex m;
-};
-
-}  // namespace
-
-struct concrete_hip_keyset {
-  std::mutex m;
-  std::vector<BskEntry*> bsk;  // indexed by bsk_index
-  std::vector<KskEntry*> ksk;
-  std::vector<uint32_t> devices{0};
-};
 
 namespace {
 
@@ -68,11 +56,22 @@ E* entry(std::vector<E*>& v, uint32_t idx, std::mutex& m, bool create) {
   return v[idx];
 }
 
-// device Fourier key of bsk_index on `gpu` (context.h:86-115 double-checked locking)
-void* bsk_on(concrete_hip_keyset* ks, uint32_t idx, uint32_t gpu, hipStream_t s) {
-  BskEntry* e = entry(ks->bsk, idx, ks->m, false);
-  if (!e) die("bootstrap key index not registered");
-  RT_ASSERT(gpu < MAX_DEV);
+// live keysets (a context pointer that is itself a keyset resolves to it) and bound contexts
+std::mutex g_ctx_mu;
+std::unordered_set<const concrete_hip_keyset*> g_live;
+std::unordered_map<const void*, concrete_hip_keyset*> g_bound;
+concrete_hip_context_resolver g_resolver = nullptr;
+void* g_resolver_user = nullptr;
+
+}  // namespace
+
+BskEntry* keyset_bsk_entry(concrete_hip_keyset* ks, uint32_t idx) { return entry(ks->bsk, idx, ks->m, false); }
+KskEntry* keyset_ksk_entry(concrete_hip_keyset* ks, uint32_t idx) { return entry(ks->ksk, idx, ks->m, false); }
+
+void* keyset_bsk_on(concrete_hip_keyset* ks, uint32_t idx, uint32_t gpu, hipStream_t s) {
+  BskEntry* e = keyset_bsk_entry(ks, idx);
+  if (!e) rt_die("bootstrap key index %u not registered", idx);
+  RT_ASSERT(gpu < RT_MAX_DEV);
   if (e->dev[gpu]) return e->dev[gpu];
   std::lock_guard<std::mutex> g(e->m);
   if (e->dev[gpu]) return e->dev[gpu];
@@ -81,13 +80,13 @@ void* bsk_on(concrete_hip_keyset* ks, uint32_t idx, uint32_t gpu, hipStream_t s)
   void* d = nullptr;
   CHIP_CHECK(hipMalloc(&d, bytes));
   int src = -1;
-  for (int o = 0; o < MAX_DEV; ++o)
+  for (int o = 0; o < RT_MAX_DEV; ++o)
     if (e->dev[o]) src = o;
   if (src >= 0) {
     // one conversion per keyset; the other devices get the converted bytes (xGMI peer copy)
     CHIP_CHECK(hipMemcpyPeerAsync(d, (int)gpu, e->dev[src], src, bytes, s));
   } else if (concrete_hip_convert_bsk(s, gpu, d, e->host.data(), 0, e->n, e->k, e->level, e->N) != 0) {
-    die(concrete_hip_last_error());
+    rt_die("%s", concrete_hip_last_error());
   }
   // publication only after the key is complete (context.h:110-113)
   CHIP_CHECK(hipStreamSynchronize(s));
@@ -95,10 +94,10 @@ void* bsk_on(concrete_hip_keyset* ks, uint32_t idx, uint32_t gpu, hipStream_t s)
   return d;
 }
 
-void* ksk_on(concrete_hip_keyset* ks, uint32_t idx, uint32_t gpu, hipStream_t s) {
-  KskEntry* e = entry(ks->ksk, idx, ks->m, false);
-  if (!e) die("keyswitch key index not registered");
-  RT_ASSERT(gpu < MAX_DEV);
+void* keyset_ksk_on(concrete_hip_keyset* ks, uint32_t idx, uint32_t gpu, hipStream_t s) {
+  KskEntry* e = keyset_ksk_entry(ks, idx);
+  if (!e) rt_die("keyswitch key index %u not registered", idx);
+  RT_ASSERT(gpu < RT_MAX_DEV);
   if (e->dev[gpu]) return e->dev[gpu];
   std::lock_guard<std::mutex> g(e->m);
   if (e->dev[gpu]) return e->dev[gpu];
@@ -108,129 +107,218 @@ void* ksk_on(concrete_hip_keyset* ks, uint32_t idx, uint32_t gpu, hipStream_t s)
   CHIP_CHECK(hipMalloc(&d, bytes));
   CHIP_CHECK(hipMemcpyAsync(d, e->host.data(), bytes, hipMemcpyHostToDevice, s));
   CHIP_CHECK(hipStreamSynchronize(s));
+  track_device_buffer(d);  // resident for the keyset's lifetime: its int8 key bytes may be cached
   e->dev[gpu] = d;
   return d;
 }
 
+concrete_hip_keyset* keyset_of_context(const void* ctx) {
+  if (!ctx) rt_die("null runtime context");
+  concrete_hip_context_resolver fn;
+  void* user;
+  {
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    auto it = g_bound.find(ctx);
+    if (it != g_bound.end()) return it->second;
+    if (g_live.count((const concrete_hip_keyset*)ctx)) return (concrete_hip_keyset*)ctx;
+    fn = g_resolver, user = g_resolver_user;
+  }
+  concrete_hip_keyset* ks = fn ? fn(ctx, user) : nullptr;
+  if (!ks) rt_die("no keyset bound to runtime context %p (concrete_hip_context_bind)", ctx);
+  std::lock_guard<std::mutex> g(g_ctx_mu);
+  g_bound[ctx] = ks;  // a context's keys do not change during its lifetime (context.h:42-57)
+  return ks;
+}
+
+namespace {
+
 // contiguous slice of `total` for part r of `parts` (the first total % parts get one more)
-void slice(uint64_t total, uint64_t parts, uint64_t r, uint64_t& start, uint64_t& count) {
+void slice_of(uint64_t total, uint64_t parts, uint64_t r, uint64_t& start, uint64_t& count) {
   const uint64_t base = total / parts, extra = total % parts;
   count = base + (r < extra ? 1 : 0);
   start = r * base + (r < extra ? r : extra);
 }
 
-struct Slice {
-  uint32_t gpu;
-  hipStream_t s;
-  uint64_t start, count;
-  std::vector<void*> bufs;
-};
-
-void* dmalloc(Slice& sl, uint64_t bytes) {
-  void* p = nullptr;
-  CHIP_CHECK(hipMallocAsync(&p, bytes ? bytes : 8, sl.s));
-  sl.bufs.push_back(p);
-  return p;
+void slot_release(SliceSlot& sl) {
+  if (!sl.s) return;
+  CHIP_CHECK(hipSetDevice((int)sl.gpu));
+  CHIP_CHECK(hipStreamSynchronize(sl.s));
+  for (int i = 0; i < 4; ++i)
+    if (sl.buf[i]) CHIP_CHECK(hipFree(sl.buf[i]));
+  for (int i = 0; i < 5; ++i)
+    if (sl.ev[i]) CHIP_CHECK(hipEventDestroy(sl.ev[i]));
+  CHIP_CHECK(hipStreamDestroy(sl.s));
+  sl = SliceSlot{};
 }
 
-void finish(std::vector<Slice>& slices) {
-  for (auto& sl : slices) {
-    CHIP_CHECK(hipSetDevice((int)sl.gpu));
-    for (void* p : sl.bufs) CHIP_CHECK(hipFreeAsync(p, sl.s));
-  }
-  for (auto& sl : slices) {
-    CHIP_CHECK(hipSetDevice((int)sl.gpu));
-    CHIP_CHECK(hipStreamSynchronize(sl.s));
-    CHIP_CHECK(hipStreamDestroy(sl.s));
-  }
-  // a PBS whose wave synchronisation gave up produced wrong outputs: abort, as the reference's
-  // wrappers do on any backend failure
-  for (auto& sl : slices)
-    if (take_device_status((int)sl.gpu) != 0) die(concrete_hip_last_error());
+void slot_init(SliceSlot& sl, uint32_t gpu) {
+  if (sl.s && sl.gpu == gpu) return;
+  slot_release(sl);
+  sl.gpu = gpu;
+  CHIP_CHECK(hipSetDevice((int)gpu));
+  CHIP_CHECK(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
+  for (int i = 0; i < 5; ++i) CHIP_CHECK(hipEventCreate(&sl.ev[i]));
 }
 
-std::vector<Slice> make_slices(concrete_hip_keyset* ks, uint64_t num_samples) {
+// grow-only device buffer i of the slot (the slot's stream is idle between calls)
+uint64_t* slot_buf(SliceSlot& sl, int i, uint64_t bytes) {
+  bytes = std::max<uint64_t>(bytes, 8);
+  if (sl.cap[i] < bytes) {
+    if (sl.buf[i]) CHIP_CHECK(hipFree(sl.buf[i]));
+    sl.buf[i] = nullptr;
+    CHIP_CHECK(hipMalloc(&sl.buf[i], bytes));
+    sl.cap[i] = bytes;
+  }
+  return (uint64_t*)sl.buf[i];
+}
+
+void mark(concrete_hip_keyset* ks, SliceSlot& sl, int i) {
+  if (ks->timing) CHIP_CHECK(hipEventRecord(sl.ev[i], sl.s));
+}
+
+// Run body(slot, start, count) for every contiguous slice of the batch, one host thread per slice
+// when there are several, then check every device's status word (a PBS whose wave
+// synchronisation gave up produced wrong outputs: abort, as the reference's wrappers do).
+template <class F>
+void run_sliced(concrete_hip_keyset* ks, uint64_t num_samples, F&& body) {
+  std::lock_guard<std::mutex> call(ks->call_m);
   std::vector<uint32_t> devs;
   {
     std::lock_guard<std::mutex> g(ks->m);
     devs = ks->devices;
   }
   const uint64_t parts = std::max<uint64_t>(1, std::min<uint64_t>(devs.size(), num_samples));
-  std::vector<Slice> out(parts);
+  if (ks->slots.size() < parts) ks->slots.resize(parts);
+  std::vector<uint64_t> start(parts), count(parts);
   for (uint64_t r = 0; r < parts; ++r) {
-    out[r].gpu = devs[r];
-    CHIP_CHECK(hipSetDevice((int)devs[r]));
-    CHIP_CHECK(hipStreamCreateWithFlags(&out[r].s, hipStreamNonBlocking));
-    slice(num_samples, parts, r, out[r].start, out[r].count);
+    slot_init(ks->slots[r], devs[r]);
+    slice_of(num_samples, parts, r, start[r], count[r]);
   }
-  return out;
+  // timing base: one event per device, recorded on the device's first (idle) slot stream
+  int base_of[RT_MAX_DEV];
+  std::fill(base_of, base_of + RT_MAX_DEV, -1);
+  if (ks->timing)
+    for (uint64_t r = 0; r < parts; ++r) {
+      SliceSlot& sl = ks->slots[r];
+      if (base_of[sl.gpu] >= 0) continue;
+      base_of[sl.gpu] = (int)r;
+      CHIP_CHECK(hipSetDevice((int)sl.gpu));
+      CHIP_CHECK(hipEventRecord(sl.ev[4], sl.s));
+    }
+  if (parts == 1) {
+    body(ks->slots[0], start[0], count[0]);
+  } else {
+    std::vector<std::thread> th;
+    th.reserve(parts);
+    for (uint64_t r = 0; r < parts; ++r)
+      th.emplace_back([&, r] { body(ks->slots[r], start[r], count[r]); });
+    for (auto& t : th) t.join();
+  }
+  bool seen[RT_MAX_DEV] = {};
+  for (uint64_t r = 0; r < parts; ++r) {
+    const uint32_t g = ks->slots[r].gpu;
+    if (seen[g]) continue;
+    seen[g] = true;
+    if (take_device_status((int)g) != 0) rt_die("%s", concrete_hip_last_error());
+  }
+  if (ks->timing) {
+    ks->timeline.assign(parts * 6, 0.0);
+    for (uint64_t r = 0; r < parts; ++r) {
+      SliceSlot& sl = ks->slots[r];
+      CHIP_CHECK(hipSetDevice((int)sl.gpu));
+      double* t = &ks->timeline[r * 6];
+      t[0] = sl.gpu;
+      for (int i = 0; i < 4; ++i) {
+        float ms = 0.f;
+        CHIP_CHECK(hipEventElapsedTime(&ms, ks->slots[base_of[sl.gpu]].ev[4], sl.ev[i]));
+        t[1 + i] = ms;
+      }
+      t[5] = (double)count[r];
+    }
+  }
 }
 
-// batched PBS shared by the plain and mapped wrappers: luts = num_luts trivial GLWEs on host
-void run_batched_pbs(uint64_t* out, const uint64_t* ct0, uint64_t num_samples, const std::vector<uint64_t>& acc,
-                     uint64_t num_luts, uint32_t n, uint32_t N, uint32_t level, uint32_t base_log, uint32_t k,
-                     uint32_t bsk_index, concrete_hip_keyset* ks) {
+struct PbsCall {
+  const uint64_t* ct0;
+  uint64_t* out;
+  const uint64_t* tlu;  // num_luts rows of N words, row stride tlu_stride0
+  uint64_t num_luts, tlu_stride0;
+  uint32_t n, N, level, base_log, k, bsk_index;
+};
+
+void run_batched_pbs(concrete_hip_keyset* ks, uint64_t num_samples, const PbsCall& c) {
   if (num_samples == 0) return;
   {
     // the registered key must have the call's parameters: its device format (and size) follows
     // them, so a mismatch would read past the key or reinterpret its layout
-    BskEntry* e = entry(ks->bsk, bsk_index, ks->m, false);
-    if (!e) die("bootstrap key index not registered");
-    RT_ASSERT(e->n == n && e->k == k && e->N == N && e->level == level && e->base_log == base_log);
+    BskEntry* e = keyset_bsk_entry(ks, c.bsk_index);
+    if (!e) rt_die("bootstrap key index %u not registered", c.bsk_index);
+    RT_ASSERT(e->n == c.n && e->k == c.k && e->N == c.N && e->level == c.level && e->base_log == c.base_log);
   }
-  const uint64_t in_w = n + 1, out_w = (uint64_t)k * N + 1, glwe = (uint64_t)(k + 1) * N;
-  auto slices = make_slices(ks, num_samples);
-  for (auto& sl : slices) {
+  const uint64_t in_w = c.n + 1, out_w = (uint64_t)c.k * c.N + 1, glwe = (uint64_t)(c.k + 1) * c.N;
+  run_sliced(ks, num_samples, [&](SliceSlot& sl, uint64_t start, uint64_t count) {
     CHIP_CHECK(hipSetDevice((int)sl.gpu));
-    void* fbsk = bsk_on(ks, bsk_index, sl.gpu, sl.s);
-    uint64_t* d_in = (uint64_t*)dmalloc(sl, sl.count * in_w * 8);
-    uint64_t* d_out = (uint64_t*)dmalloc(sl, sl.count * out_w * 8);
-    CHIP_CHECK(hipMemcpyAsync(d_in, ct0 + sl.start * in_w, sl.count * in_w * 8, hipMemcpyHostToDevice, sl.s));
-    uint64_t* d_acc;
-    uint64_t* d_lidx = nullptr;
-    if (num_luts == 1) {
-      d_acc = (uint64_t*)dmalloc(sl, glwe * 8);
-      CHIP_CHECK(hipMemcpyAsync(d_acc, acc.data(), glwe * 8, hipMemcpyHostToDevice, sl.s));
+    void* fbsk = keyset_bsk_on(ks, c.bsk_index, sl.gpu, sl.s);
+    const bool mapped = c.num_luts > 1;
+    const uint64_t rows = mapped ? count : 1;
+    uint64_t* d_in = slot_buf(sl, 0, count * in_w * 8);
+    uint64_t* d_out = slot_buf(sl, 1, count * out_w * 8);
+    uint64_t* d_lut = slot_buf(sl, 2, rows * (c.N + glwe) * 8);  // LUT rows, then their accumulators
+    uint64_t* d_acc = d_lut + rows * c.N;
+    uint64_t* d_lidx = mapped ? slot_buf(sl, 3, count * 8) : nullptr;
+    mark(ks, sl, 0);
+    CHIP_CHECK(hipMemcpyWithStream(d_in, c.ct0 + start * in_w, count * in_w * 8, hipMemcpyHostToDevice, sl.s));
+    // one LUT per sample: this slice's rows, indexed 0..count-1 (wrappers.cpp:317-325)
+    const uint64_t* src = c.tlu + (mapped ? start * c.tlu_stride0 : 0);
+    if (c.tlu_stride0 == c.N || rows == 1) {
+      CHIP_CHECK(hipMemcpyWithStream(d_lut, src, rows * c.N * 8, hipMemcpyHostToDevice, sl.s));
     } else {
-      // one LUT per sample: this slice's LUTs, indexed 0..count-1 (wrappers.cpp:317-325)
-      d_acc = (uint64_t*)dmalloc(sl, sl.count * glwe * 8);
-      CHIP_CHECK(hipMemcpyAsync(d_acc, acc.data() + sl.start * glwe, sl.count * glwe * 8, hipMemcpyHostToDevice,
-                                sl.s));
-      std::vector<uint64_t> idx(sl.count);
-      for (uint64_t i = 0; i < sl.count; ++i) idx[i] = i;
-      d_lidx = (uint64_t*)dmalloc(sl, sl.count * 8);
-      CHIP_CHECK(hipMemcpyAsync(d_lidx, idx.data(), sl.count * 8, hipMemcpyHostToDevice, sl.s));
-      CHIP_CHECK(hipStreamSynchronize(sl.s));  // idx is a host temporary
+      std::vector<uint64_t> packed(rows * c.N);
+      for (uint64_t r = 0; r < rows; ++r) std::copy(src + r * c.tlu_stride0, src + r * c.tlu_stride0 + c.N, &packed[r * c.N]);
+      CHIP_CHECK(hipMemcpyWithStream(d_lut, packed.data(), rows * c.N * 8, hipMemcpyHostToDevice, sl.s));
     }
-    if (concrete_hip_pbs(sl.s, sl.gpu, d_out, nullptr, d_acc, d_lidx, d_in, nullptr, fbsk, n, k, N, base_log, level,
-                         (uint32_t)sl.count, nullptr) != 0)
-      die(concrete_hip_last_error());
-    CHIP_CHECK(hipMemcpyAsync(out + sl.start * out_w, d_out, sl.count * out_w * 8, hipMemcpyDeviceToHost, sl.s));
-  }
-  finish(slices);
+    launch_trivial_glwe(sl.s, d_acc, d_lut, rows, c.k, c.N);
+    if (mapped) launch_iota(sl.s, d_lidx, count);
+    mark(ks, sl, 1);
+    if (concrete_hip_pbs(sl.s, sl.gpu, d_out, nullptr, d_acc, d_lidx, d_in, nullptr, fbsk, c.n, c.k, c.N, c.base_log,
+                         c.level, (uint32_t)count, nullptr) != 0)
+      rt_die("%s", concrete_hip_last_error());
+    mark(ks, sl, 2);
+    CHIP_CHECK(hipMemcpyWithStream(c.out + start * out_w, d_out, count * out_w * 8, hipMemcpyDeviceToHost, sl.s));
+    mark(ks, sl, 3);
+    CHIP_CHECK(hipStreamSynchronize(sl.s));
+  });
 }
 
-std::vector<uint64_t> trivial_glwes(const uint64_t* tlu, uint64_t num_luts, uint64_t tlu_stride0, uint32_t N,
-                                    uint32_t k) {
-  // (wrappers.cpp:199-209, 296-305): k zero masks, body = LUT
-  const uint64_t glwe = (uint64_t)(k + 1) * N;
-  std::vector<uint64_t> acc(num_luts * glwe, 0);
-  for (uint64_t l = 0; l < num_luts; ++l)
-    for (uint32_t i = 0; i < N; ++i) acc[l * glwe + (uint64_t)k * N + i] = tlu[l * tlu_stride0 + i];
-  return acc;
+void run_batched_ks(concrete_hip_keyset* ks, uint64_t num_samples, const uint64_t* ct0, uint64_t* out, uint32_t level,
+                    uint32_t base_log, uint32_t n_in, uint32_t n_out, uint32_t ksk_index) {
+  if (num_samples == 0) return;
+  KskEntry* e = keyset_ksk_entry(ks, ksk_index);
+  if (!e) rt_die("keyswitch key index %u not registered", ksk_index);
+  RT_ASSERT(e->level == level && e->base_log == base_log && e->n_in == n_in && e->n_out == n_out);
+  const uint64_t in_w = n_in + 1, out_w = n_out + 1;
+  run_sliced(ks, num_samples, [&](SliceSlot& sl, uint64_t start, uint64_t count) {
+    CHIP_CHECK(hipSetDevice((int)sl.gpu));
+    void* dk = keyset_ksk_on(ks, ksk_index, sl.gpu, sl.s);
+    uint64_t* d_in = slot_buf(sl, 0, count * in_w * 8);
+    uint64_t* d_out = slot_buf(sl, 1, count * out_w * 8);
+    mark(ks, sl, 0);
+    CHIP_CHECK(hipMemcpyWithStream(d_in, ct0 + start * in_w, count * in_w * 8, hipMemcpyHostToDevice, sl.s));
+    mark(ks, sl, 1);
+    if (concrete_hip_keyswitch(sl.s, sl.gpu, d_out, nullptr, d_in, nullptr, (const uint64_t*)dk, n_in, n_out, base_log,
+                               level, (uint32_t)count) != 0)
+      rt_die("%s", concrete_hip_last_error());
+    mark(ks, sl, 2);
+    CHIP_CHECK(hipMemcpyWithStream(out + start * out_w, d_out, count * out_w * 8, hipMemcpyDeviceToHost, sl.s));
+    mark(ks, sl, 3);
+    CHIP_CHECK(hipStreamSynchronize(sl.s));
+  });
 }
 
-}  // namespace
-
-extern "C" {
-
-concrete_hip_keyset* concrete_hip_keyset_create(void) { return new concrete_hip_keyset(); }
-
-void concrete_hip_keyset_destroy(concrete_hip_keyset* ks) {
-  if (!ks) return;
+void free_keys(concrete_hip_keyset* ks) {
   for (BskEntry* e : ks->bsk) {
     if (!e) continue;
-    for (int d = 0; d < MAX_DEV; ++d)
+    for (int d = 0; d < RT_MAX_DEV; ++d)
       if (e->dev[d]) {
         CHIP_CHECK(hipSetDevice(d));
         CHIP_CHECK(hipFree(e->dev[d]));
@@ -239,13 +327,40 @@ void concrete_hip_keyset_destroy(concrete_hip_keyset* ks) {
   }
   for (KskEntry* e : ks->ksk) {
     if (!e) continue;
-    for (int d = 0; d < MAX_DEV; ++d)
+    for (int d = 0; d < RT_MAX_DEV; ++d)
       if (e->dev[d]) {
         CHIP_CHECK(hipSetDevice(d));
+        release_key_bytes(e->dev[d], nullptr, true);  // int8 key bytes cached for this KSK
         CHIP_CHECK(hipFree(e->dev[d]));
       }
     delete e;
   }
+}
+
+}  // namespace
+}  // namespace chip
+
+using namespace chip;
+
+extern "C" {
+
+concrete_hip_keyset* concrete_hip_keyset_create(void) {
+  concrete_hip_keyset* ks = new concrete_hip_keyset();
+  std::lock_guard<std::mutex> g(g_ctx_mu);
+  g_live.insert(ks);
+  return ks;
+}
+
+void concrete_hip_keyset_destroy(concrete_hip_keyset* ks) {
+  if (!ks) return;
+  {
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    g_live.erase(ks);
+    for (auto it = g_bound.begin(); it != g_bound.end();)
+      it = it->second == ks ? g_bound.erase(it) : std::next(it);
+  }
+  for (auto& sl : ks->slots) slot_release(sl);
+  free_keys(ks);
   delete ks;
 }
 
@@ -263,7 +378,7 @@ int concrete_hip_keyset_add_bsk(concrete_hip_keyset* ks, uint32_t bsk_index, con
   }
   BskEntry* e = entry(ks->bsk, bsk_index, ks->m, true);
   std::lock_guard<std::mutex> g(e->m);
-  for (int d = 0; d < MAX_DEV; ++d)
+  for (int d = 0; d < RT_MAX_DEV; ++d)
     if (e->dev[d]) {
       set_error("keyset_add_bsk: index %u already resident", bsk_index);
       return -3;
@@ -282,6 +397,11 @@ int concrete_hip_keyset_add_ksk(concrete_hip_keyset* ks, uint32_t ksk_index, con
   }
   KskEntry* e = entry(ks->ksk, ksk_index, ks->m, true);
   std::lock_guard<std::mutex> g(e->m);
+  for (int d = 0; d < RT_MAX_DEV; ++d)
+    if (e->dev[d]) {
+      set_error("keyset_add_ksk: index %u already resident", ksk_index);
+      return -3;
+    }
   const uint64_t len = (uint64_t)input_lwe_dim * level * (output_lwe_dim + 1);
   e->host.assign(ksk, ksk + len);
   e->level = level, e->base_log = base_log, e->n_in = input_lwe_dim, e->n_out = output_lwe_dim;
@@ -295,15 +415,57 @@ int concrete_hip_keyset_set_devices(concrete_hip_keyset* ks, const uint32_t* dev
   }
   const int nd = concrete_hip_device_count();
   for (uint32_t i = 0; i < count; ++i)
-    if ((int)devices[i] >= nd || devices[i] >= MAX_DEV) {
+    if ((int)devices[i] >= nd || devices[i] >= RT_MAX_DEV) {
       set_error("keyset_set_devices: device %u not visible", devices[i]);
       return -3;
     }
+  std::lock_guard<std::mutex> call(ks->call_m);
   std::lock_guard<std::mutex> g(ks->m);
   ks->devices.assign(devices, devices + count);
   return 0;
 }
 
+void concrete_hip_keyset_set_timing(concrete_hip_keyset* ks, int enable) {
+  if (!ks) return;
+  std::lock_guard<std::mutex> call(ks->call_m);
+  ks->timing = enable != 0;
+  ks->timeline.clear();
+}
+
+uint32_t concrete_hip_keyset_timeline(concrete_hip_keyset* ks, double* out, uint32_t max_slices) {
+  if (!ks) return 0;
+  std::lock_guard<std::mutex> call(ks->call_m);
+  const uint32_t n = (uint32_t)(ks->timeline.size() / 6);
+  if (out) std::copy(ks->timeline.begin(), ks->timeline.begin() + 6 * std::min(n, max_slices), out);
+  return n;
+}
+
+int concrete_hip_context_bind(const void* runtime_context, concrete_hip_keyset* ks) {
+  if (!runtime_context) {
+    set_error("context_bind: null context");
+    return -3;
+  }
+  std::lock_guard<std::mutex> g(g_ctx_mu);
+  if (ks) {
+    if (!g_live.count(ks)) {
+      set_error("context_bind: %p is not a live keyset", (void*)ks);
+      return -3;
+    }
+    g_bound[runtime_context] = ks;
+  } else {
+    g_bound.erase(runtime_context);
+  }
+  return 0;
+}
+
+void concrete_hip_set_context_resolver(concrete_hip_context_resolver fn, void* user) {
+  std::lock_guard<std::mutex> g(g_ctx_mu);
+  g_resolver = fn, g_resolver_user = user;
+}
+
+// ------------------------------------------------------------------------------------------
+// memref_*_hip_u64: the keyset handle is the context
+// ------------------------------------------------------------------------------------------
 void memref_batched_bootstrap_lwe_hip_u64(uint64_t* out_allocated, uint64_t* out_aligned, uint64_t out_offset,
                                           uint64_t out_size0, uint64_t out_size1, uint64_t out_stride0,
                                           uint64_t out_stride1, uint64_t* ct0_allocated, uint64_t* ct0_aligned,
@@ -321,9 +483,9 @@ void memref_batched_bootstrap_lwe_hip_u64(uint64_t* out_allocated, uint64_t* out
   RT_ASSERT(tlu_size == poly_size && tlu_stride == 1);
   RT_ASSERT(out_stride1 == 1 && out_stride0 == out_size1 && ct0_stride1 == 1 && ct0_stride0 == ct0_size1);
   RT_ASSERT(context);
-  auto acc = trivial_glwes(tlu_aligned + tlu_offset, 1, poly_size, poly_size, glwe_dim);
-  run_batched_pbs(out_aligned + out_offset, ct0_aligned + ct0_offset, out_size0, acc, 1, input_lwe_dim, poly_size,
-                  level, base_log, glwe_dim, bsk_index, context);
+  run_batched_pbs(context, out_size0,
+                  PbsCall{ct0_aligned + ct0_offset, out_aligned + out_offset, tlu_aligned + tlu_offset, 1, poly_size,
+                          input_lwe_dim, poly_size, level, base_log, glwe_dim, bsk_index});
 }
 
 void memref_batched_mapped_bootstrap_lwe_hip_u64(
@@ -339,12 +501,12 @@ void memref_batched_mapped_bootstrap_lwe_hip_u64(
   RT_ASSERT(out_size1 == (uint64_t)glwe_dim * poly_size + 1);
   RT_ASSERT(ct0_size1 == (uint64_t)input_lwe_dim + 1);
   RT_ASSERT((out_size0 == tlu_size0 || tlu_size0 == 1) && "Number of LUTs does not match batch size");
-  RT_ASSERT(tlu_size1 == poly_size && tlu_stride1 == 1);
+  RT_ASSERT(tlu_size1 == poly_size && tlu_stride1 == 1 && tlu_stride0 >= poly_size);
   RT_ASSERT(out_stride1 == 1 && out_stride0 == out_size1 && ct0_stride1 == 1 && ct0_stride0 == ct0_size1);
   RT_ASSERT(context);
-  auto acc = trivial_glwes(tlu_aligned + tlu_offset, tlu_size0, tlu_stride0, poly_size, glwe_dim);
-  run_batched_pbs(out_aligned + out_offset, ct0_aligned + ct0_offset, out_size0, acc, tlu_size0, input_lwe_dim,
-                  poly_size, level, base_log, glwe_dim, bsk_index, context);
+  run_batched_pbs(context, out_size0,
+                  PbsCall{ct0_aligned + ct0_offset, out_aligned + out_offset, tlu_aligned + tlu_offset, tlu_size0,
+                          tlu_stride0, input_lwe_dim, poly_size, level, base_log, glwe_dim, bsk_index});
 }
 
 void memref_bootstrap_lwe_hip_u64(uint64_t* out_allocated, uint64_t* out_aligned, uint64_t out_offset,
@@ -370,31 +532,13 @@ void memref_batched_keyswitch_lwe_hip_u64(uint64_t* out_allocated, uint64_t* out
                                           uint32_t base_log, uint32_t input_lwe_dim, uint32_t output_lwe_dim,
                                           uint32_t ksk_index, concrete_hip_keyset* context) {
   (void)out_allocated, (void)ct0_allocated;
+  // wrappers.cpp:118-120
   RT_ASSERT(out_size0 == ct0_size0);
   RT_ASSERT(out_size1 == (uint64_t)output_lwe_dim + 1 && ct0_size1 == (uint64_t)input_lwe_dim + 1);
   RT_ASSERT(out_stride1 == 1 && out_stride0 == out_size1 && ct0_stride1 == 1 && ct0_stride0 == ct0_size1);
   RT_ASSERT(context);
-  const uint64_t num_samples = out_size0;
-  if (num_samples == 0) return;
-  KskEntry* e = entry(context->ksk, ksk_index, context->m, false);
-  if (!e) die("keyswitch key index not registered");
-  RT_ASSERT(e->level == level && e->base_log == base_log && e->n_in == input_lwe_dim && e->n_out == output_lwe_dim);
-  const uint64_t in_w = input_lwe_dim + 1, out_w = output_lwe_dim + 1;
-  const uint64_t* ct0 = ct0_aligned + ct0_offset;
-  uint64_t* out = out_aligned + out_offset;
-  auto slices = make_slices(context, num_samples);
-  for (auto& sl : slices) {
-    CHIP_CHECK(hipSetDevice((int)sl.gpu));
-    void* dk = ksk_on(context, ksk_index, sl.gpu, sl.s);
-    uint64_t* d_in = (uint64_t*)dmalloc(sl, sl.count * in_w * 8);
-    uint64_t* d_out = (uint64_t*)dmalloc(sl, sl.count * out_w * 8);
-    CHIP_CHECK(hipMemcpyAsync(d_in, ct0 + sl.start * in_w, sl.count * in_w * 8, hipMemcpyHostToDevice, sl.s));
-    if (concrete_hip_keyswitch(sl.s, sl.gpu, d_out, nullptr, d_in, nullptr, (const uint64_t*)dk, input_lwe_dim,
-                               output_lwe_dim, base_log, level, (uint32_t)sl.count) != 0)
-      die(concrete_hip_last_error());
-    CHIP_CHECK(hipMemcpyAsync(out + sl.start * out_w, d_out, sl.count * out_w * 8, hipMemcpyDeviceToHost, sl.s));
-  }
-  finish(slices);
+  run_batched_ks(context, out_size0, ct0_aligned + ct0_offset, out_aligned + out_offset, level, base_log,
+                 input_lwe_dim, output_lwe_dim, ksk_index);
 }
 
 void memref_keyswitch_lwe_hip_u64(uint64_t* out_allocated, uint64_t* out_aligned, uint64_t out_offset,
@@ -402,10 +546,81 @@ void memref_keyswitch_lwe_hip_u64(uint64_t* out_allocated, uint64_t* out_aligned
                                   uint64_t* ct0_aligned, uint64_t ct0_offset, uint64_t ct0_size, uint64_t ct0_stride,
                                   uint32_t level, uint32_t base_log, uint32_t input_lwe_dim,
                                   uint32_t output_lwe_dim, uint32_t ksk_index, concrete_hip_keyset* context) {
+  // wrappers.cpp:70-86
   RT_ASSERT(out_stride == 1 && ct0_stride == 1);
   memref_batched_keyswitch_lwe_hip_u64(out_allocated, out_aligned, out_offset, 1, out_size, out_size, 1,
                                        ct0_allocated, ct0_aligned, ct0_offset, 1, ct0_size, ct0_size, 1, level,
                                        base_log, input_lwe_dim, output_lwe_dim, ksk_index, context);
+}
+
+// ------------------------------------------------------------------------------------------
+// memref_*_cuda_u64: the reference's names (wrappers.h:246-300); the last argument is the
+// caller's runtime context, resolved to its keyset
+// ------------------------------------------------------------------------------------------
+void memref_keyswitch_lwe_cuda_u64(uint64_t* out_allocated, uint64_t* out_aligned, uint64_t out_offset,
+                                   uint64_t out_size, uint64_t out_stride, uint64_t* ct0_allocated,
+                                   uint64_t* ct0_aligned, uint64_t ct0_offset, uint64_t ct0_size,
+                                   uint64_t ct0_stride, uint32_t level, uint32_t base_log, uint32_t input_lwe_dim,
+                                   uint32_t output_lwe_dim, uint32_t ksk_index, void* context) {
+  memref_keyswitch_lwe_hip_u64(out_allocated, out_aligned, out_offset, out_size, out_stride, ct0_allocated,
+                               ct0_aligned, ct0_offset, ct0_size, ct0_stride, level, base_log, input_lwe_dim,
+                               output_lwe_dim, ksk_index, keyset_of_context(context));
+}
+
+void memref_bootstrap_lwe_cuda_u64(uint64_t* out_allocated, uint64_t* out_aligned, uint64_t out_offset,
+                                   uint64_t out_size, uint64_t out_stride, uint64_t* ct0_allocated,
+                                   uint64_t* ct0_aligned, uint64_t ct0_offset, uint64_t ct0_size,
+                                   uint64_t ct0_stride, uint64_t* tlu_allocated, uint64_t* tlu_aligned,
+                                   uint64_t tlu_offset, uint64_t tlu_size, uint64_t tlu_stride,
+                                   uint32_t input_lwe_dim, uint32_t poly_size, uint32_t level, uint32_t base_log,
+                                   uint32_t glwe_dim, uint32_t bsk_index, void* context) {
+  memref_bootstrap_lwe_hip_u64(out_allocated, out_aligned, out_offset, out_size, out_stride, ct0_allocated,
+                               ct0_aligned, ct0_offset, ct0_size, ct0_stride, tlu_allocated, tlu_aligned, tlu_offset,
+                               tlu_size, tlu_stride, input_lwe_dim, poly_size, level, base_log, glwe_dim, bsk_index,
+                               keyset_of_context(context));
+}
+
+void memref_batched_keyswitch_lwe_cuda_u64(uint64_t* out_allocated, uint64_t* out_aligned, uint64_t out_offset,
+                                           uint64_t out_size0, uint64_t out_size1, uint64_t out_stride0,
+                                           uint64_t out_stride1, uint64_t* ct0_allocated, uint64_t* ct0_aligned,
+                                           uint64_t ct0_offset, uint64_t ct0_size0, uint64_t ct0_size1,
+                                           uint64_t ct0_stride0, uint64_t ct0_stride1, uint32_t level,
+                                           uint32_t base_log, uint32_t input_lwe_dim, uint32_t output_lwe_dim,
+                                           uint32_t ksk_index, void* context) {
+  memref_batched_keyswitch_lwe_hip_u64(out_allocated, out_aligned, out_offset, out_size0, out_size1, out_stride0,
+                                       out_stride1, ct0_allocated, ct0_aligned, ct0_offset, ct0_size0, ct0_size1,
+                                       ct0_stride0, ct0_stride1, level, base_log, input_lwe_dim, output_lwe_dim,
+                                       ksk_index, keyset_of_context(context));
+}
+
+void memref_batched_bootstrap_lwe_cuda_u64(uint64_t* out_allocated, uint64_t* out_aligned, uint64_t out_offset,
+                                           uint64_t out_size0, uint64_t out_size1, uint64_t out_stride0,
+                                           uint64_t out_stride1, uint64_t* ct0_allocated, uint64_t* ct0_aligned,
+                                           uint64_t ct0_offset, uint64_t ct0_size0, uint64_t ct0_size1,
+                                           uint64_t ct0_stride0, uint64_t ct0_stride1, uint64_t* tlu_allocated,
+                                           uint64_t* tlu_aligned, uint64_t tlu_offset, uint64_t tlu_size,
+                                           uint64_t tlu_stride, uint32_t input_lwe_dim, uint32_t poly_size,
+                                           uint32_t level, uint32_t base_log, uint32_t glwe_dim, uint32_t bsk_index,
+                                           void* context) {
+  memref_batched_bootstrap_lwe_hip_u64(out_allocated, out_aligned, out_offset, out_size0, out_size1, out_stride0,
+                                       out_stride1, ct0_allocated, ct0_aligned, ct0_offset, ct0_size0, ct0_size1,
+                                       ct0_stride0, ct0_stride1, tlu_allocated, tlu_aligned, tlu_offset, tlu_size,
+                                       tlu_stride, input_lwe_dim, poly_size, level, base_log, glwe_dim, bsk_index,
+                                       keyset_of_context(context));
+}
+
+void memref_batched_mapped_bootstrap_lwe_cuda_u64(
+    uint64_t* out_allocated, uint64_t* out_aligned, uint64_t out_offset, uint64_t out_size0, uint64_t out_size1,
+    uint64_t out_stride0, uint64_t out_stride1, uint64_t* ct0_allocated, uint64_t* ct0_aligned, uint64_t ct0_offset,
+    uint64_t ct0_size0, uint64_t ct0_size1, uint64_t ct0_stride0, uint64_t ct0_stride1, uint64_t* tlu_allocated,
+    uint64_t* tlu_aligned, uint64_t tlu_offset, uint64_t tlu_size0, uint64_t tlu_size1, uint64_t tlu_stride0,
+    uint64_t tlu_stride1, uint32_t input_lwe_dim, uint32_t poly_size, uint32_t level, uint32_t base_log,
+    uint32_t glwe_dim, uint32_t bsk_index, void* context) {
+  memref_batched_mapped_bootstrap_lwe_hip_u64(
+      out_allocated, out_aligned, out_offset, out_size0, out_size1, out_stride0, out_stride1, ct0_allocated,
+      ct0_aligned, ct0_offset, ct0_size0, ct0_size1, ct0_stride0, ct0_stride1, tlu_allocated, tlu_aligned, tlu_offset,
+      tlu_size0, tlu_size1, tlu_stride0, tlu_stride1, input_lwe_dim, poly_size, level, base_log, glwe_dim, bsk_index,
+      keyset_of_context(context));
 }
 
 }  // extern "C"

@@ -106,7 +106,7 @@ void cuda_negate_lwe_ciphertext_vector_64(void *stream, uint32_t gpu_index, void
  * Part 2: extensions (return 0 on success, < 0 on error; message via concrete_hip_last_error)
  * ------------------------------------------------------------------------------------------ */
 
-/* ABI version of this header. */
+/* ABI version of this header (2: round 3 — context-resolved memref_*_cuda_u64, stream emulator). */
 uint32_t concrete_hip_abi_version(void);
 /* thread-local message of the last failed concrete_hip_* call */
 const char *concrete_hip_last_error(void);
@@ -148,6 +148,22 @@ int concrete_hip_keyswitch(void *stream, uint32_t gpu_index, uint64_t *lwe_array
                            uint32_t num_samples);
 /* Fourier key registered for a `dest` of cuda_convert_lwe_programmable_bootstrap_key_64, or NULL */
 const void *concrete_hip_lookup_bsk(const void *bootstrapping_key);
+/* Release what the backend derived from device buffer `ptr` (a registered Fourier key whose `dest`
+ * is ptr, the int8 key bytes the matrix-core keyswitch cached for a KSK at ptr — cached only for
+ * buffers from cuda_malloc_async or a keyset) without freeing ptr itself; cuda_drop /
+ * cuda_drop_async do this for every pointer, and cuda_memcpy_async_to_gpu for its destination.
+ * Returns the number of cached key-byte entries released. */
+int concrete_hip_release_device_buffer(const void *ptr);
+/* LUT encoding on the device (compiler lib/Runtime/wrappers.cpp:388-450,
+ * memref_encode_expand_lut_for_bootstrap, for num_luts rows at once): out is num_luts x out_size,
+ * in is num_luts x in_size, device pointers; stream-ordered. */
+int concrete_hip_encode_expand_lut_device(void *stream, uint32_t gpu_index, uint64_t *out, uint64_t out_size,
+                                          const uint64_t *in, uint64_t in_size, uint64_t num_luts,
+                                          uint32_t out_message_bits, int is_signed);
+/* Trivial-GLWE accumulators on the device (wrappers.cpp:199-209): acc is num_luts x (k+1)N, row l =
+ * k zero polynomials then LUT row l of luts (num_luts x N); device pointers; stream-ordered. */
+int concrete_hip_build_accumulators(void *stream, uint32_t gpu_index, uint64_t *acc, const uint64_t *luts,
+                                    uint64_t num_luts, uint32_t glwe_dim, uint32_t polynomial_size);
 /* number of visible devices */
 int concrete_hip_device_count(void);
 /* Synchronise the device and return (and clear) its sticky status: 0 ok, -4 when a PBS kernel's
@@ -203,8 +219,24 @@ int concrete_hip_keyset_add_bsk(concrete_hip_keyset *ks, uint32_t bsk_index, con
                                 uint32_t glwe_dim, uint32_t level, uint32_t base_log, uint32_t poly_size);
 int concrete_hip_keyset_add_ksk(concrete_hip_keyset *ks, uint32_t ksk_index, const uint64_t *ksk, uint32_t level,
                                 uint32_t base_log, uint32_t input_lwe_dim, uint32_t output_lwe_dim);
-/* devices the batched calls shard across (default: device 0); entries may repeat */
+/* devices the batched calls shard across (default: device 0); entries may repeat.  Every slice of
+ * a call runs on its own host thread, stream and cached device buffers. */
 int concrete_hip_keyset_set_devices(concrete_hip_keyset *ks, const uint32_t *devices, uint32_t count);
+/* Diagnostics: record HIP events around every slice of the following calls ... */
+void concrete_hip_keyset_set_timing(concrete_hip_keyset *ks, int enable);
+/* ... and read them for the last call: 6 doubles per slice (device, then ms since the call's start
+ * on that device: slice start, inputs copied (kernel issue), kernel done, outputs copied, then the
+ * slice's sample count); returns the number of slices (copies at most max_slices). */
+uint32_t concrete_hip_keyset_timeline(concrete_hip_keyset *ks, double *out, uint32_t max_slices);
+
+/* The runtime's context pointer (mlir::concretelang::RuntimeContext *, context.h:42-154) is what
+ * the circuit passes to memref_*_cuda_u64 and to the stream emulator's KS / PBS processes.  The
+ * backend resolves it to a keyset: a pointer bound with concrete_hip_context_bind (NULL keyset
+ * unbinds), else the resolver's answer (cached per context), else the pointer itself when it is a
+ * live keyset handle.  An unresolvable context aborts (reference failure behaviour). */
+int concrete_hip_context_bind(const void *runtime_context, concrete_hip_keyset *ks);
+typedef concrete_hip_keyset *(*concrete_hip_context_resolver)(const void *runtime_context, void *user);
+void concrete_hip_set_context_resolver(concrete_hip_context_resolver fn, void *user);
 
 void memref_keyswitch_lwe_hip_u64(uint64_t *out_allocated, uint64_t *out_aligned, uint64_t out_offset,
                                   uint64_t out_size, uint64_t out_stride, uint64_t *ct0_allocated,
@@ -241,6 +273,123 @@ void memref_batched_mapped_bootstrap_lwe_hip_u64(
     uint64_t *tlu_aligned, uint64_t tlu_offset, uint64_t tlu_size0, uint64_t tlu_size1, uint64_t tlu_stride0,
     uint64_t tlu_stride1, uint32_t input_lwe_dim, uint32_t poly_size, uint32_t level, uint32_t base_log,
     uint32_t glwe_dim, uint32_t bsk_index, concrete_hip_keyset *context);
+
+/* The direct GPU route under the reference's own names and argument lists
+ * (compiler include/concretelang/Runtime/wrappers.h:246-300, lib/Runtime/wrappers.cpp:70-363):
+ * `context` is the caller's runtime context, resolved as described above.  Same semantics as the
+ * memref_*_hip_u64 forms (every batched call sharded over the keyset's devices). */
+void memref_keyswitch_lwe_cuda_u64(uint64_t *out_allocated, uint64_t *out_aligned, uint64_t out_offset,
+                                   uint64_t out_size, uint64_t out_stride, uint64_t *ct0_allocated,
+                                   uint64_t *ct0_aligned, uint64_t ct0_offset, uint64_t ct0_size,
+                                   uint64_t ct0_stride, uint32_t level, uint32_t base_log, uint32_t input_lwe_dim,
+                                   uint32_t output_lwe_dim, uint32_t ksk_index, void *context);
+void memref_bootstrap_lwe_cuda_u64(uint64_t *out_allocated, uint64_t *out_aligned, uint64_t out_offset,
+                                   uint64_t out_size, uint64_t out_stride, uint64_t *ct0_allocated,
+                                   uint64_t *ct0_aligned, uint64_t ct0_offset, uint64_t ct0_size,
+                                   uint64_t ct0_stride, uint64_t *tlu_allocated, uint64_t *tlu_aligned,
+                                   uint64_t tlu_offset, uint64_t tlu_size, uint64_t tlu_stride,
+                                   uint32_t input_lwe_dim, uint32_t poly_size, uint32_t level, uint32_t base_log,
+                                   uint32_t glwe_dim, uint32_t bsk_index, void *context);
+void memref_batched_keyswitch_lwe_cuda_u64(uint64_t *out_allocated, uint64_t *out_aligned, uint64_t out_offset,
+                                           uint64_t out_size0, uint64_t out_size1, uint64_t out_stride0,
+                                           uint64_t out_stride1, uint64_t *ct0_allocated, uint64_t *ct0_aligned,
+                                           uint64_t ct0_offset, uint64_t ct0_size0, uint64_t ct0_size1,
+                                           uint64_t ct0_stride0, uint64_t ct0_stride1, uint32_t level,
+                                           uint32_t base_log, uint32_t input_lwe_dim, uint32_t output_lwe_dim,
+                                           uint32_t ksk_index, void *context);
+void memref_batched_bootstrap_lwe_cuda_u64(uint64_t *out_allocated, uint64_t *out_aligned, uint64_t out_offset,
+                                           uint64_t out_size0, uint64_t out_size1, uint64_t out_stride0,
+                                           uint64_t out_stride1, uint64_t *ct0_allocated, uint64_t *ct0_aligned,
+                                           uint64_t ct0_offset, uint64_t ct0_size0, uint64_t ct0_size1,
+                                           uint64_t ct0_stride0, uint64_t ct0_stride1, uint64_t *tlu_allocated,
+                                           uint64_t *tlu_aligned, uint64_t tlu_offset, uint64_t tlu_size,
+                                           uint64_t tlu_stride, uint32_t input_lwe_dim, uint32_t poly_size,
+                                           uint32_t level, uint32_t base_log, uint32_t glwe_dim, uint32_t bsk_index,
+                                           void *context);
+void memref_batched_mapped_bootstrap_lwe_cuda_u64(
+    uint64_t *out_allocated, uint64_t *out_aligned, uint64_t out_offset, uint64_t out_size0, uint64_t out_size1,
+    uint64_t out_stride0, uint64_t out_stride1, uint64_t *ct0_allocated, uint64_t *ct0_aligned, uint64_t ct0_offset,
+    uint64_t ct0_size0, uint64_t ct0_size1, uint64_t ct0_stride0, uint64_t ct0_stride1, uint64_t *tlu_allocated,
+    uint64_t *tlu_aligned, uint64_t tlu_offset, uint64_t tlu_size0, uint64_t tlu_size1, uint64_t tlu_stride0,
+    uint64_t tlu_stride1, uint32_t input_lwe_dim, uint32_t poly_size, uint32_t level, uint32_t base_log,
+    uint32_t glwe_dim, uint32_t bsk_index, void *context);
+
+/* ------------------------------------------------------------------------------------------
+ * Part 5: the SDFG stream emulator — the default GPU route of a circuit compiled with SDFG
+ * extraction (compiler include/concretelang/Runtime/stream_emulator_api.h:30-106; reference
+ * implementation lib/Runtime/GPUDFG.cpp:1467-1799; call sequence emitted by
+ * lib/Conversion/SDFGToStreamEmulator/SDFGToStreamEmulator.cpp:25-73: init, make streams, make
+ * processes, run, put inputs, get outputs, delete).  Same names and argument lists; `stype` is the
+ * reference's `stream_type` enum (passed as int; values below).  A get evaluates the processes its
+ * stream depends on whose inputs changed since their last evaluation, the whole subgraph resident
+ * on the devices (sdfg.hip).  Devices: CONCRETE_HIP_SDFG_DEVICES ("0,0,1", repeats allowed), else
+ * SDFG_NUM_GPUS, else all visible devices.  `context` of KS / PBS processes: as in Part 4.
+ * ------------------------------------------------------------------------------------------ */
+enum {
+  CONCRETE_HIP_TS_STREAM_TYPE_X86_TO_TOPO_LSAP = 0,
+  CONCRETE_HIP_TS_STREAM_TYPE_TOPO_TO_TOPO_LSAP = 1,
+  CONCRETE_HIP_TS_STREAM_TYPE_TOPO_TO_X86_LSAP = 2,
+  CONCRETE_HIP_TS_STREAM_TYPE_TOPO_TO_BOTH = 3,
+  CONCRETE_HIP_TS_STREAM_TYPE_X86_TO_X86_LSAP = 4
+};
+void *stream_emulator_init(void);
+void stream_emulator_run(void *dfg);
+void stream_emulator_delete(void *dfg);
+void stream_emulator_make_memref_add_lwe_ciphertexts_u64_process(void *dfg, void *sin1, void *sin2, void *sout);
+void stream_emulator_make_memref_add_plaintext_lwe_ciphertext_u64_process(void *dfg, void *sin1, void *sin2,
+                                                                          void *sout);
+void stream_emulator_make_memref_mul_cleartext_lwe_ciphertext_u64_process(void *dfg, void *sin1, void *sin2,
+                                                                          void *sout);
+void stream_emulator_make_memref_negate_lwe_ciphertext_u64_process(void *dfg, void *sin1, void *sout);
+void stream_emulator_make_memref_keyswitch_lwe_u64_process(void *dfg, void *sin1, void *sout, uint32_t level,
+                                                           uint32_t base_log, uint32_t input_lwe_dim,
+                                                           uint32_t output_lwe_dim, uint32_t output_size,
+                                                           uint32_t ksk_index, void *context);
+void stream_emulator_make_memref_bootstrap_lwe_u64_process(void *dfg, void *sin1, void *sin2, void *sout,
+                                                           uint32_t input_lwe_dim, uint32_t poly_size,
+                                                           uint32_t level, uint32_t base_log, uint32_t glwe_dim,
+                                                           uint32_t output_size, uint32_t bsk_index, void *context);
+void stream_emulator_make_memref_batched_add_lwe_ciphertexts_u64_process(void *dfg, void *sin1, void *sin2,
+                                                                         void *sout);
+void stream_emulator_make_memref_batched_add_plaintext_lwe_ciphertext_u64_process(void *dfg, void *sin1, void *sin2,
+                                                                                  void *sout);
+void stream_emulator_make_memref_batched_add_plaintext_cst_lwe_ciphertext_u64_process(void *dfg, void *sin1,
+                                                                                      void *sin2, void *sout);
+void stream_emulator_make_memref_batched_mul_cleartext_lwe_ciphertext_u64_process(void *dfg, void *sin1, void *sin2,
+                                                                                  void *sout);
+void stream_emulator_make_memref_batched_mul_cleartext_cst_lwe_ciphertext_u64_process(void *dfg, void *sin1,
+                                                                                      void *sin2, void *sout);
+void stream_emulator_make_memref_batched_negate_lwe_ciphertext_u64_process(void *dfg, void *sin1, void *sout);
+void stream_emulator_make_memref_batched_keyswitch_lwe_u64_process(void *dfg, void *sin1, void *sout, uint32_t level,
+                                                                   uint32_t base_log, uint32_t input_lwe_dim,
+                                                                   uint32_t output_lwe_dim, uint32_t output_size,
+                                                                   uint32_t ksk_index, void *context);
+void stream_emulator_make_memref_batched_bootstrap_lwe_u64_process(void *dfg, void *sin1, void *sin2, void *sout,
+                                                                   uint32_t input_lwe_dim, uint32_t poly_size,
+                                                                   uint32_t level, uint32_t base_log,
+                                                                   uint32_t glwe_dim, uint32_t output_size,
+                                                                   uint32_t bsk_index, void *context);
+void stream_emulator_make_memref_batched_mapped_bootstrap_lwe_u64_process(void *dfg, void *sin1, void *sin2,
+                                                                          void *sout, uint32_t input_lwe_dim,
+                                                                          uint32_t poly_size, uint32_t level,
+                                                                          uint32_t base_log, uint32_t glwe_dim,
+                                                                          uint32_t output_size, uint32_t bsk_index,
+                                                                          void *context);
+void *stream_emulator_make_uint64_stream(const char *name, int stype);
+void stream_emulator_put_uint64(void *stream, uint64_t e);
+uint64_t stream_emulator_get_uint64(void *stream);
+void *stream_emulator_make_memref_stream(const char *name, int stype);
+void stream_emulator_put_memref(void *stream, uint64_t *allocated, uint64_t *aligned, uint64_t offset, uint64_t size,
+                                uint64_t stride, uint64_t data_ownership);
+void stream_emulator_get_memref(void *stream, uint64_t *out_allocated, uint64_t *out_aligned, uint64_t out_offset,
+                                uint64_t out_size, uint64_t out_stride);
+void *stream_emulator_make_memref_batch_stream(const char *name, int stype);
+void stream_emulator_put_memref_batch(void *stream, uint64_t *allocated, uint64_t *aligned, uint64_t offset,
+                                      uint64_t size0, uint64_t size1, uint64_t stride0, uint64_t stride1,
+                                      uint64_t data_ownership);
+void stream_emulator_get_memref_batch(void *stream, uint64_t *out_allocated, uint64_t *out_aligned,
+                                      uint64_t out_offset, uint64_t out_size0, uint64_t out_size1,
+                                      uint64_t out_stride0, uint64_t out_stride1);
 
 #ifdef __cplusplus
 }

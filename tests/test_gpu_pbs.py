@@ -455,3 +455,49 @@ def test_sync_timeout_is_reported(B, oracle, cfg2, torch_cuda):
     got = run_gpu(B, cfg2, cts[:16], acc, torch_cuda)
     assert B.device_status("cuda:0") == 0
     assert np.array_equal(got, run_oracle(oracle, cfg2, cts[:16], acc))
+
+
+def test_keyswitch_key_byte_cache_and_fallback(B, oracle, torch_cuda, monkeypatch):
+    """the matrix-core keyswitch caches the int8 key bytes of a KSK whose lifetime the
+    backend sees (allocated by cuda_malloc_async, as the runtime allocates it), releases them on
+    cuda_drop or a rewrite of the buffer, never caches torch-owned memory (its caching allocator
+    reuses addresses), and falls back to the scratch-free VALU kernel when operand scratch is
+    unavailable (CONCRETE_HIP_KS_SCRATCH_LIMIT forces that).  All bit-exact vs the oracle."""
+    from concrete_amd import _native
+    L = _native.lib()
+    p = B.CFG2
+    glwe_sk = B.binary_key(p.big_n, 8801)
+    lwe_sk = B.binary_key(p.n, 8802)
+    ksk = B.ksk_generate(p, glwe_sk, lwe_sk, 8803)
+    ksk2 = B.ksk_generate(p, glwe_sk, lwe_sk, 8804)
+    rng = np.random.RandomState(8805)
+    nb = 200
+    cts = rng.randint(0, 2 ** 63, size=(nb, p.big_n + 1), dtype=np.int64).astype(np.uint64) * np.uint64(2) + \
+        np.uint64(1)
+    op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, ks_l=p.ks_level, ks_logB=p.ks_base_log)
+    ref = oracle.keyswitch_batch(op, cts, ksk)
+    ref2 = oracle.keyswitch_batch(op, cts, ksk2)
+    d_in = B.to_device(cts, "cuda:0")
+    kb = B.RuntimeBuffer(ksk)
+    try:
+        for _ in range(2):  # built once, then reused
+            out = B.keyswitch(p, kb, d_in)
+            torch_cuda.cuda.synchronize()
+            assert np.array_equal(B.to_host(out), ref)
+        kb.write(ksk2)  # cuda_memcpy_async_to_gpu onto the key drops its cached bytes
+        out = B.keyswitch(p, kb, d_in)
+        torch_cuda.cuda.synchronize()
+        assert np.array_equal(B.to_host(out), ref2)
+        assert L.concrete_hip_release_device_buffer(kb.data_ptr()) == 1
+        assert L.concrete_hip_release_device_buffer(kb.data_ptr()) == 0
+    finally:
+        kb.free()
+    d_ksk = B.to_device(ksk, "cuda:0")
+    out = B.keyswitch(p, d_ksk, d_in)
+    torch_cuda.cuda.synchronize()
+    assert np.array_equal(B.to_host(out), ref)
+    assert L.concrete_hip_release_device_buffer(d_ksk.data_ptr()) == 0  # torch memory: not cached
+    monkeypatch.setenv("CONCRETE_HIP_KS_SCRATCH_LIMIT", "1")
+    out = B.keyswitch(p, d_ksk, d_in)
+    torch_cuda.cuda.synchronize()
+    assert np.array_equal(B.to_host(out), ref)

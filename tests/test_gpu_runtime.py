@@ -145,3 +145,120 @@ def test_batched_bootstrap_general_path(env):
     assert np.array_equal(got, ref)
     dec = B.lwe_decrypt(glwe_sk, got, p.big_n)
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+
+
+def test_slices_overlap_and_bit_exact(env):
+    """Slices of one call run concurrently (one host thread, stream and buffer set per slice):
+    slice r + 1's kernel is issued before slice r's outputs are back (the
+    round-2 loop issued slice r + 1 only after slice r's pageable D2H had returned)."""
+    B, R, O = env["B"], env["R"], env["O"]
+    p = B.CFG2  # full n: each slice's kernel runs for milliseconds
+    lwe_sk = B.binary_key(p.n, 61)
+    glwe_sk = B.binary_key(p.big_n, 62)
+    bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 63)
+    width = 3
+    table = np.array([6, 1, 7, 0, 3, 2, 5, 4], dtype=np.uint64)
+    tlu = B.expand_lut(table, p.N, width)
+    nb = 1024
+    rng = np.random.RandomState(64)
+    msgs = rng.randint(0, 1 << width, size=nb)
+    cts = B.lwe_encrypt(lwe_sk, [B.encode(m, width) for m in msgs], p.n, B.secure_std(1, p.n), 65)
+    ks = R.Keyset([0, 0, 0, 0])
+    ks.add_bsk(0, bsk, p)
+    R.batched_bootstrap(ks, p, cts[:8], tlu)  # key conversion outside the timed call
+    ks.set_timing(True)
+    got = R.batched_bootstrap(ks, p, cts, tlu)
+    tl = ks.timeline()
+    ks.close()
+    assert tl.shape == (4, 6) and list(tl[:, 5]) == [256] * 4
+    for r in range(3):
+        # columns: device, start, inputs copied (kernel issue), kernel done, outputs copied, count
+        assert tl[r + 1, 2] < tl[r, 4], tl
+    dec = B.lwe_decrypt(glwe_sk, got, p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+    op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
+    rows = np.array([0, 255, 256, 511, 767, 1023])
+    ref, _ = O.pbs_batch(op, cts[rows], B.trivial_glwe(p, tlu)[None, :], fbsk=O.bsk_to_fourier(op, bsk))
+    assert np.array_equal(got[rows], ref)
+
+
+def test_cuda_names_resolve_the_runtime_context(env):
+    """memref_*_cuda_u64 under the reference's names take the circuit's RuntimeContext pointer:
+    bound with concrete_hip_context_bind, or answered by a registered resolver."""
+    import ctypes as C
+    B, R, O, p = env["B"], env["R"], env["O"], env["p"]
+    width = 3
+    table = np.array([2, 7, 1, 0, 5, 5, 3, 6], dtype=np.uint64)
+    tlu = B.expand_lut(table, p.N, width)
+    msgs, cts = inputs(env, 6, width, 400)
+    ks = keyset(env, [0, 0])
+    fake_ctx = C.create_string_buffer(64)  # stands for a RuntimeContext object
+    ctx = C.addressof(fake_ctx)
+    ks.bind(ctx)
+    big = R.batched_bootstrap_cuda(ctx, p, cts, tlu)
+    ref, _ = O.pbs_batch(env["op"], cts, B.trivial_glwe(p, tlu)[None, :], fbsk=env["fcpu"])
+    assert np.array_equal(big, ref)
+    assert np.array_equal(R.bootstrap_cuda(ctx, p, cts[3], tlu), ref[3])
+    small = R.batched_keyswitch_cuda(ctx, p, big)
+    assert np.array_equal(small, O.keyswitch_batch(env["op"], big, env["ksk"]))
+    assert np.array_equal(R.keyswitch_cuda(ctx, p, big[1]), small[1])
+    tlus = np.stack([tlu, tlu[::-1].copy()] * 3)
+    mapped = R.batched_mapped_bootstrap_cuda(ctx, p, cts, tlus)
+    accs = np.stack([B.trivial_glwe(p, t) for t in tlus])
+    refm, _ = O.pbs_batch(env["op"], cts, accs, fbsk=env["fcpu"], lut_idx=np.arange(6, dtype=np.uint64))
+    assert np.array_equal(mapped, refm)
+    # a resolver answers for contexts nobody bound (e.g. one RuntimeContext per invocation)
+    L = ks.lib
+    seen = []
+    RESOLVER = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_void_p)
+
+    @RESOLVER
+    def resolve(c, user):
+        seen.append(c)
+        return ks.h
+
+    L.concrete_hip_set_context_resolver(C.cast(resolve, C.c_void_p), None)
+    other = C.create_string_buffer(64)
+    try:
+        again = R.batched_bootstrap_cuda(C.addressof(other), p, cts, tlu)
+        again2 = R.batched_bootstrap_cuda(C.addressof(other), p, cts, tlu)  # cached: resolver asked once
+    finally:
+        L.concrete_hip_set_context_resolver(None, None)
+    assert seen == [C.addressof(other)]
+    assert np.array_equal(again, ref) and np.array_equal(again2, ref)
+    ks.close()
+
+
+def test_device_lut_encoding_and_accumulators(env):
+    """LUT encoding and trivial-GLWE accumulators on the device (lut.hip) equal the runtime's host
+    forms (wrappers.cpp:388-450, 199-209) for every width, signedness and mega-case size."""
+    import torch
+    B, p = env["B"], env["p"]
+    L = env["R"]._native.lib()
+    rng = np.random.RandomState(9)
+    s = torch.cuda.current_stream().cuda_stream
+    for bits in (1, 2, 3, 4, 6, 8):
+        for signed in (False, True):
+            for N in (256, 1024, 4096):
+                if (N >> bits) < 2:
+                    continue
+                rows = 3
+                tabs = rng.randint(0, 1 << bits, size=(rows, 1 << bits)).astype(np.uint64)
+                d_in = B.to_device(tabs, "cuda:0")
+                d_out = torch.empty((rows, N), dtype=torch.int64, device="cuda:0")
+                assert L.concrete_hip_encode_expand_lut_device(s, 0, d_out.data_ptr(), N, d_in.data_ptr(), 1 << bits,
+                                                               rows, bits, int(signed)) == 0
+                got = B.to_host(d_out)
+                for r in range(rows):
+                    assert np.array_equal(got[r], B.expand_lut(tabs[r], N, bits, signed)), (bits, signed, N, r)
+    tl = np.stack([B.expand_lut(rng.randint(0, 8, size=8).astype(np.uint64), p.N, 3) for _ in range(4)])
+    for k in (1, 2):
+        d_l = B.to_device(tl, "cuda:0")
+        d_acc = torch.empty((4, (k + 1) * p.N), dtype=torch.int64, device="cuda:0")
+        assert L.concrete_hip_build_accumulators(s, 0, d_acc.data_ptr(), d_l.data_ptr(), 4, k, p.N) == 0
+        acc = B.to_host(d_acc)
+        for r in range(4):
+            want = np.zeros((k + 1) * p.N, dtype=np.uint64)
+            want[k * p.N:] = tl[r]
+            assert np.array_equal(acc[r], want)
+    assert L.concrete_hip_encode_expand_lut_device(s, 0, 1, 1000, 1, 8, 1, 3, 0) == -3  # 1000 / 8 is odd

@@ -1,0 +1,52 @@
+"""Turn tools/pmc.sh passes into the per-launch PMC record bench.py reports (roofline.traffic,
+roofline.valu, roofline.dram).
+
+  traffic = 2 * FETCH_SIZE + WRITE_SIZE (KB -> bytes): gfx950 tallies 128-B fabric read requests at
+            64 B, so FETCH_SIZE is doubled for 16-B/lane streaming reads (MI355X_MICROARCH.md
+            §HBM); WRITE_SIZE is exact for 16-B/lane stores.
+  f64_flop = 64 lanes * (2 * SQ_INSTS_VALU_FMA_F64 + SQ_INSTS_VALU_ADD_F64 + SQ_INSTS_VALU_MUL_F64)
+            (the SQ_INSTS_* counters count wave-instructions, summed over the device).
+The record carries the hash of the kernel sources it was measured on; bench.py uses it only while
+the sources are unchanged.
+Usage: python tools/pmc_record.py gpurun_out/<tag> profiles/<round>_<config>_pmc.json CONFIG BATCH
+       (<tag> holds the pass directories of tools/pmc.sh: d/e for traffic, b for the f64 mix)
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import kernel_source_hash  # noqa: E402
+
+KERNEL = {"cfg2": "pbs1024", "cfg4": "pbs2048"}
+
+
+def collect(src, kname):
+    vals = {}
+    for f in glob.glob(f"{src}/**/run_counter_collection.csv", recursive=True):
+        for row in csv.DictReader(open(f)):
+            if kname in row.get("Kernel_Name", ""):
+                vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}
+
+
+def main():
+    src, dst, config, batch = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+    kname = KERNEL.get(config, config)
+    v = collect(src, kname)
+    rec = {"kernel": kname, "config": config, "batch": batch, "source_hash": kernel_source_hash(), "pmc_dir": src,
+           "counters": v}
+    if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+        rec["traffic_bytes"] = int(round((2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024))
+    if "SQ_INSTS_VALU_FMA_F64" in v:
+        rec["f64_flop"] = 64.0 * (2 * v["SQ_INSTS_VALU_FMA_F64"] + v.get("SQ_INSTS_VALU_ADD_F64", 0.0)
+                                  + v.get("SQ_INSTS_VALU_MUL_F64", 0.0))
+    json.dump(rec, open(dst, "w"), indent=1)
+    print(json.dumps({k: rec[k] for k in rec if k != "counters"}))
+
+
+if __name__ == "__main__":
+    main()

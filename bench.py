@@ -119,6 +119,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", type=int, default=8, help="rows checked bit-exactly against the oracle (rank 0)")
     ap.add_argument("--no-ks", action="store_true", help="skip the secondary keyswitch measurement")
+    ap.add_argument("--check-gather", action="store_true",
+                    help="rank 0 checks the whole gathered batch: every row decrypts to its rank's LUT[m], and "
+                         "two rows per rank are bit-exact vs the oracle (inputs regenerated from the seeds)")
     return ap.parse_args()
 
 
@@ -182,11 +185,15 @@ def main():
         torch.cuda.synchronize()
         t_bcast = time.perf_counter() - t0
 
-    # ---- this rank's shard: 4096 fresh encryptions of random 3-bit messages, one shared LUT
-    rng = np.random.RandomState(1000 + rank)
-    table = rng.randint(0, 1 << width, size=1 << width).astype(np.uint64)
-    msgs = rng.randint(0, 1 << width, size=args.batch)
-    cts = B.lwe_encrypt(lwe_sk, [B.encode(m, width) for m in msgs], p.n, B.secure_std(1, p.n), 5000 + rank)
+    # ---- this rank's shard: fresh encryptions of random `width`-bit messages, one LUT per rank
+    def shard_inputs(r, count):
+        rng = np.random.RandomState(1000 + r)
+        table = rng.randint(0, 1 << width, size=1 << width).astype(np.uint64)
+        msgs = rng.randint(0, 1 << width, size=count)
+        cts = B.lwe_encrypt(lwe_sk, [B.encode(m, width) for m in msgs], p.n, B.secure_std(1, p.n), 5000 + r)
+        return table, msgs, cts
+
+    table, msgs, cts = shard_inputs(rank, args.batch)
     acc = B.trivial_glwe(p, B.expand_lut(table, p.N, width))
     d_in = B.to_device(cts, dev)
     d_lut = B.to_device(acc[None, :], dev)
@@ -282,12 +289,36 @@ def main():
 
     # ---- final gather of the output rows onto rank 0 (outside the timed PBS region)
     t_gather = 0.0
+    gather_check = None
+
+    def check_gather(rows, world_, total):
+        """Every gathered row decrypts to its rank's LUT[m]; two rows per rank bit-exact (oracle)."""
+        from concrete_amd.dist import shard_range
+        from oracle import pyoracle as O  # checker only, after the timed region
+        op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, limbs=O.limbs_for(p.N))
+        key = B.bsk_generate(p, lwe_sk, glwe_sk, 3) if bsk is None else bsk
+        fcpu = O.bsk_to_fourier(op, key)
+        dec_ok, exact = 0, True
+        for r in range(world_):
+            start, count = shard_range(total, world_, r)
+            tab_r, msgs_r, cts_r = shard_inputs(r, count)
+            mine = rows[start:start + count]
+            dec = B.lwe_decrypt(glwe_sk, mine, p.big_n)
+            dec_ok += sum(int(B.decode(d, width) == tab_r[m]) for d, m in zip(dec, msgs_r))
+            pick = np.array([0, count - 1])
+            acc_r = B.trivial_glwe(p, B.expand_lut(tab_r, p.N, width))
+            ref, _ = O.pbs_batch(op, cts_r[pick], acc_r[None, :], fbsk=fcpu)
+            exact &= bool(np.array_equal(ref, mine[pick]))
+        return {"rows": int(rows.shape[0]), "decrypt_ok": f"{dec_ok}/{total}", "bitexact_rows": 2 * world_,
+                "bitexact": exact}
     if world > 1:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         full = D.gather_rows(d_out, global_batch, dst=0)
         torch.cuda.synchronize()
         t_gather = time.perf_counter() - t0
+        if rank == 0 and args.check_gather:
+            gather_check = check_gather(B.to_host(full), world, global_batch)
         del full
 
     # ---- correctness of what was timed: decrypt-level on every row, bit-exact sample (rank 0)
@@ -380,7 +411,7 @@ def main():
             "cpu_baseline": cpu,
             "secondary": {"keyswitch": ks_res,
                           "pcie_inclusive_pbs_per_s": round(e2e * world, 1)},
-            "checks": {"decrypt_ok": f"{ok_all}/{global_batch}", "bitexact_rows": args.verify,
+            "checks": {"decrypt_ok": f"{ok_all}/{global_batch}", "bitexact_rows": args.verify, "gather": gather_check,
                        "bitexact": bitexact},
         }
         print(json.dumps(result), flush=True)

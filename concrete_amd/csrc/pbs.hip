@@ -12,7 +12,8 @@
 // error is certified < 1/2, so rounding recovers the exact integers; the
 // limbs are recombined modulo 2^64.  Results are bit-identical to the schoolbook definition.
 //
-// Mapping (N = 1024, k = 1): two waves per ciphertext, PBS_PAIRS ciphertexts per workgroup.
+// Mapping (N = 1024, k = 1): two waves per ciphertext, P ciphertexts per workgroup (P = 4; 2 or 1
+// for batches too small to give every CU a workgroup of 4: launch_pair).
 // Wave h of a pair
 //   * owns GLWE polynomial h of the accumulator (16 u64 per lane: lane t holds t + 64 m),
 //   * computes the l forward transforms of its own polynomial's digits,
@@ -23,7 +24,7 @@
 //     of its own output polynomial.
 // Each wave stays < 256 VGPRs (two waves per SIMD).  The Fourier key is streamed through a
 // 3-group LDS ring (24 KB groups = three spectra of one (column, limb) slice) filled by
-// LDS-DMA (global_load_lds_dwordx4) and read by all PBS_PAIRS pairs, so it crosses the L2->CU
+// LDS-DMA (global_load_lds_dwordx4) and read by all P pairs, so it crosses the L2->CU
 // port once per workgroup instead of once per ciphertext.  The whole CMUX loop runs in one
 // launch with the workgroup in lockstep (one raw s_barrier per key group and per half-spectrum
 // exchange).
@@ -96,8 +97,8 @@ __device__ __forceinline__ void xchg_barrier(uint32_t* flags, int w, uint32_t& c
 #endif
 }
 
-template <int L, bool RESID, bool STAMPS>
-__global__ void __launch_bounds__(PBS_PAIRS * 128, 2)
+template <int P, int L, bool RESID, bool STAMPS>
+__global__ void __launch_bounds__(P * 128, 2)
 pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx,
                     const uint64_t* __restrict__ luts, const uint64_t* __restrict__ lut_idx,
                     const uint64_t* __restrict__ in, const uint64_t* __restrict__ in_idx,
@@ -107,7 +108,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   constexpr int PER_I = K1 * LIMBS * RQ * 512;  // complex values per Fourier GGSW
   static_assert(XCH_SLOTS <= (int)PBS1024_XCH_SLOTS, "transpose scratch");
   static_assert(FFT512_TABLE_ENTRIES * sizeof(cplx) == PBS1024_TABLE_BYTES, "table bytes");
-  constexpr int NW = 2 * PBS_PAIRS;           // waves per workgroup
+  constexpr int NW = 2 * P;                   // waves per workgroup
   constexpr int GROUP = L * 512;              // complex values per ring group (one row of a slice)
   constexpr int NGRP = K1 * K1 * LIMBS;       // ring groups per CMUX step
   constexpr int GLDS = GROUP / 64 / NW;       // 1 KB LDS-DMA pieces per wave per group
@@ -123,7 +124,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   const int h = w & 1;  // polynomial = frequency half
   const uint64_t hsign = (uint64_t)h << 63;  // sign mask of the k2 ^ 4 relabeling (h = 1)
   const int lane = threadIdx.x & 63;
-  const uint32_t s = blockIdx.x * PBS_PAIRS + (w >> 1);
+  const uint32_t s = blockIdx.x * P + (w >> 1);
   const bool active = s < num_samples;
   cplx* xch = xch_all + w * PBS1024_XCH_SLOTS;
   uint64_t* xch64 = reinterpret_cast<uint64_t*>(xch);
@@ -167,7 +168,7 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     issue_group(key_w, 1);
   }
 
-  build_fft512_tables(tbl, threadIdx.x, PBS_PAIRS * 128);
+  build_fft512_tables(tbl, threadIdx.x, P * 128);
   if (lane == 0) pflags[w] = 0u;
   uint32_t pcnt = 0;
   __syncthreads();
@@ -518,18 +519,18 @@ pbs1024_pair_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 // ------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------
-template <int L, bool RESID, bool STAMPS>
+template <int P, int L, bool RESID, bool STAMPS>
 static int launch_pair_t(const PbsArgs& a) {
-  const size_t lds = pbs1024_pair_lds_bytes(L);
+  const size_t lds = pbs1024_pair_lds_bytes(L, P);
   // the exactness gate (pbs1024_exact) keeps l * logB <= 27: the decomposer state fits 32 bits
   if (!pbs1024_exact(1, L, a.base_log)) {
     set_error("pbs: N=1024 l=%d logB=%u is outside the exact range", L, a.base_log);
     return -2;
   }
-  auto kern = pbs1024_pair_kernel<L, RESID, STAMPS>;
+  auto kern = pbs1024_pair_kernel<P, L, RESID, STAMPS>;
   CHIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  const uint32_t blocks = (a.num_samples + PBS_PAIRS - 1) / PBS_PAIRS;
-  hipLaunchKernelGGL(kern, dim3(blocks), dim3(PBS_PAIRS * 128), lds, a.stream, a.out, a.out_idx, a.luts, a.lut_idx,
+  const uint32_t blocks = (a.num_samples + P - 1) / P;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(P * 128), lds, a.stream, a.out, a.out_idx, a.luts, a.lut_idx,
                      a.in, a.in_idx, reinterpret_cast<const cplx*>(a.fbsk), a.n, a.base_log, a.num_samples, a.resid,
                      a.guard);
   hipError_t e = hipGetLastError();
@@ -540,14 +541,44 @@ static int launch_pair_t(const PbsArgs& a) {
   return 0;
 }
 
+// compute units of the current device (cached per device)
+static uint32_t device_cus() {
+  static uint32_t cus[64] = {};
+  int dev = 0;
+  CHIP_CHECK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    int n = 0;
+    CHIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    cus[dev] = n > 0 ? (uint32_t)n : 256u;
+  }
+  return cus[dev];
+}
+
+template <int P, int L>
+static int launch_pair_p(const PbsArgs& a) {
+  // diagnostic: CONCRETE_HIP_PBS_STAMPS=1 runs the s_memtime-instrumented build; `resid` must then
+  // point at 2 * P * ceil(num_samples / P) * NSTAMP u64 (per-wave cycle sums)
+  static const bool stamps = getenv("CONCRETE_HIP_PBS_STAMPS") && atoi(getenv("CONCRETE_HIP_PBS_STAMPS"));
+  if (stamps) return launch_pair_t<P, L, true, true>(a);
+  return a.resid ? launch_pair_t<P, L, true, false>(a) : launch_pair_t<P, L, false, false>(a);
+}
+
 template <int L>
 static int launch_pair(const PbsArgs& a) {
   if (a.num_samples == 0) return 0;
-  // diagnostic: CONCRETE_HIP_PBS_STAMPS=1 runs the s_memtime-instrumented build; `resid` must then
-  // point at 2 * PBS_PAIRS * ceil(num_samples / PBS_PAIRS) * NSTAMP u64 (per-wave cycle sums)
-  static const bool stamps = getenv("CONCRETE_HIP_PBS_STAMPS") && atoi(getenv("CONCRETE_HIP_PBS_STAMPS"));
-  if (stamps) return launch_pair_t<L, true, true>(a);
-  return a.resid ? launch_pair_t<L, true, false>(a) : launch_pair_t<L, false, false>(a);
+  // Ciphertexts per workgroup: a workgroup runs alone on its CU (LDS), so 4 per workgroup leaves
+  // CUs idle below 4 x CUs ciphertexts.  The round time of a workgroup falls with fewer waves per
+  // SIMD, but not in proportion: 2 per workgroup pays off while their workgroups fit one round
+  // (<= 2 x CUs ciphertexts), 1 per workgroup at <= CUs.  CONCRETE_HIP_PBS_PAIRS=1/2/4 forces it.
+  const char* fe = getenv("CONCRETE_HIP_PBS_PAIRS");  // read per call (tests switch it)
+  const int forced = fe ? atoi(fe) : 0;
+  const uint32_t cus = device_cus();
+  const int P = forced == 1 || forced == 2 || forced == 4 ? forced
+                : a.num_samples <= cus ? 1 : a.num_samples <= 2 * cus ? 2 : 4;
+  if (P == 1) return launch_pair_p<1, L>(a);
+  if (P == 2) return launch_pair_p<2, L>(a);
+  return launch_pair_p<4, L>(a);
 }
 
 int pbs_launch(const PbsArgs& a) {

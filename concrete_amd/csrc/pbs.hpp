@@ -10,11 +10,14 @@ namespace chip {
 // one half of the frequency slots per wave).  LDS: the two pass-1/pass-2 twiddle tables and one
 // 9.2 KB transpose scratch per wave (which doubles as the half-spectrum mailbox).
 constexpr size_t PBS1024_TABLE_BYTES = (8 * 72 + 4 * (8 + 64 + 8)) * 16;  // FFT512_TABLE_ENTRIES (fft512.hpp)
-constexpr int PBS_PAIRS = 4;                // ciphertexts (wave pairs) per workgroup
+// Ciphertexts (wave pairs) per workgroup: PBS_PAIRS = 4 (8 waves, 2 per SIMD, one workgroup per CU
+// by LDS) for batches that fill the chip; 2 or 1 for batches of <= 2 or <= 1 ciphertexts per CU, where
+// 4 per workgroup would leave CUs idle (pbs.hip launch_pair: strong scaling, 512 per GPU on 8 GPUs).
+constexpr int PBS_PAIRS = 4;
 constexpr size_t PBS1024_XCH_SLOTS = 576;  // >= XCH_SLOTS (fft512.hpp), 16-B slots per wave
-constexpr size_t pbs1024_pair_lds_bytes(int level) {
-  return PBS1024_TABLE_BYTES + 2 * PBS_PAIRS * PBS1024_XCH_SLOTS * 16 + 3 * (size_t)level * 512 * 16 +
-         2 * PBS_PAIRS * 4;  // + pair-sync counters
+constexpr size_t pbs1024_pair_lds_bytes(int level, int pairs = PBS_PAIRS) {
+  return PBS1024_TABLE_BYTES + 2 * (size_t)pairs * PBS1024_XCH_SLOTS * 16 + 3 * (size_t)level * 512 * 16 +
+         2 * (size_t)pairs * 4;  // + pair-sync counters
 }
 
 // N = 2048 kernel geometry (pbs2048.hip): four waves per ciphertext (one per even/odd half of

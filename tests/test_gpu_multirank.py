@@ -34,3 +34,24 @@ def test_bench_two_ranks():
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 512
     assert d["checks"]["decrypt_ok"] == "512/512"
     assert d["checks"]["bitexact"] is True
+
+
+def test_bench_eight_ranks_configs2_shape():
+    """BASELINE configs[2] rehearsed on one GPU: 8 gloo ranks (sharing cuda:0) bootstrap 8,192
+    ciphertexts each (global batch 65,536); the key is built on rank 0 and broadcast; rank 0
+    gathers the whole batch and checks it: every row decrypts to its rank's LUT[m] and two rows
+    per rank are bit-exact vs the oracle."""
+    env = dict(os.environ, CONCRETE_HIP_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "8", "--steps", "1", "--warmup", "0", "--batch", "8192", "--no-cpu-baseline", "--no-ks",
+           "--verify", "2", "--check-gather"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["config"]["global_batch"] == 65536
+    assert d["checks"]["decrypt_ok"] == "65536/65536"
+    g = d["checks"]["gather"]
+    assert g["rows"] == 65536 and g["decrypt_ok"] == "65536/65536" and g["bitexact"] is True

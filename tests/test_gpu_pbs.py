@@ -501,3 +501,37 @@ def test_keyswitch_key_byte_cache_and_fallback(B, oracle, torch_cuda, monkeypatc
     out = B.keyswitch(p, d_ksk, d_in)
     torch_cuda.cuda.synchronize()
     assert np.array_equal(B.to_host(out), ref)
+
+
+@pytest.mark.parametrize("pairs", [1, 2, 4])
+@pytest.mark.parametrize("level,base_log", [(1, 11), (2, 6), (3, 7)])
+def test_pbs_pairs_per_workgroup(B, oracle, torch_cuda, monkeypatch, pairs, level, base_log):
+    """The N = 1024 kernel at 1, 2 and 4 ciphertexts per workgroup (the small-batch forms that keep
+    every CU busy at <= 2 x CUs ciphertexts, pbs.hip launch_pair; CONCRETE_HIP_PBS_PAIRS forces
+    one): ragged batches, permuted index arrays, per-sample LUTs — bit-exact vs the oracle with the
+    measured rounding residual below the certified bound."""
+    monkeypatch.setenv("CONCRETE_HIP_PBS_PAIRS", str(pairs))
+    p = replace(B.CFG2, n=12, level=level, base_log=base_log)
+    S = Setup(B, oracle, torch_cuda, p, 5100 + 10 * level + pairs)
+    width = 2
+    rng = np.random.RandomState(pairs * 100 + level)
+    nb = 7
+    tables = [rng.randint(0, 4, size=4) for _ in range(nb)]
+    msgs = rng.randint(0, 4, size=nb)
+    cts = encrypt(B, S, msgs, width, 51 + pairs, std=2.0 ** -25)
+    accs = np.stack([lut_acc(B, S, t, width) for t in tables])
+    in_idx = rng.permutation(nb).astype(np.uint64)
+    out_idx = rng.permutation(nb).astype(np.uint64)
+    lut_idx = rng.permutation(nb).astype(np.uint64)
+    dev = "cuda:0"
+    resid = torch_cuda.zeros(1, dtype=torch_cuda.int64, device=dev)
+    out = B.pbs(p, S.fbsk, B.to_device(cts, dev), B.to_device(accs, dev), lut_idx=B.to_device(lut_idx, dev),
+                in_idx=B.to_device(in_idx, dev), out_idx=B.to_device(out_idx, dev), resid=resid)
+    torch_cuda.cuda.synchronize()
+    got = B.to_host(out)
+    ref, _ = oracle.pbs_batch(S.op, cts[in_idx.astype(np.int64)], accs, fbsk=S.fbsk_cpu, lut_idx=lut_idx)
+    exp = np.zeros_like(ref)
+    exp[out_idx.astype(np.int64)] = ref
+    assert np.array_equal(got, exp)
+    r = float(np.array([int(resid.cpu()[0])], dtype=np.int64).view(np.float64)[0])
+    assert r < oracle.fft_error_bound(S.op, S.fbsk_cpu) < 0.5

@@ -208,3 +208,64 @@ def test_reference_fixtures_at_optimizer_rows(B, torch_cuda, bits):
     torch_cuda.cuda.synchronize()
     dec = B.lwe_decrypt(glwe_sk, B.to_host(out), p.big_n)
     assert [B.decode(d, bits, s) for d, (_, s) in zip(dec, expect)] == [e for e, _ in expect]
+
+
+def test_configs4_atomic_pattern_8bit(B, oracle, torch_cuda):
+    """BASELINE configs[4] (an 8-bit fhe.LookupTable) as the compiler lowers it
+    (FHEToTFHEScalar.cpp:373-437: encode/expand the LUT, keyswitch, bootstrap) at the optimizer's
+    8-bit row (v0_last_128: k = 1, N = 16384, n = 1006, br 2/15, ks 5/4), full sizes and secure
+    noise, on the reference's 8-bit fixtures (every signedness variant): the LUTs are encoded on
+    the device (concrete_hip_encode_expand_lut_device), the keyswitch kN = 16384 -> n = 1006 is
+    bit-exact vs the oracle, and every bootstrapped output decodes to the reference's expected
+    value."""
+    import json
+    import os
+    from concrete_amd import _native
+    L = _native.lib()
+    golden = os.path.join(os.path.dirname(__file__), "golden", "reference_lut_fixtures.json")
+    fx = json.load(open(golden))
+    cases = [c for c in fx["apply_lookup_table"] + fx["linalg_apply_lookup_table"]
+             if len(c["lut"]) == 256 and not c["description"].endswith("_2layer")]
+    p = B.OPTIMIZER_SETS[8]
+    bits = 8
+    lwe_sk = B.binary_key(p.n, 7800)
+    glwe_sk = B.binary_key(p.big_n, 7801)
+    fbsk = B.convert_bsk(p, B.bsk_generate(p, lwe_sk, glwe_sk, 7802), "cuda:0")
+    ksk = B.ksk_generate(p, glwe_sk, lwe_sk, 7803)
+    pts, lut_idx, expect, tables, signs = [], [], [], [], []
+    for ci, c in enumerate(cases):
+        tables.append(np.array(c["lut"], dtype=np.int64).view(np.uint64))
+        signs.append(bool(c["input_signed"]))
+        for x, e in zip(c["input"], c["expected"]):
+            pt = int(B.encode(int(x) & ((1 << 64) - 1), bits))
+            if c["input_signed"]:  # FHEToTFHEScalar.cpp:373-413: offset 2^(p-1) on the body
+                pt = (pt + int(B.encode(1 << (bits - 1), bits))) & ((1 << 64) - 1)
+            pts.append(pt)
+            lut_idx.append(ci)
+            expect.append((e, c["output_signed"]))
+    # the client encrypts under the big (GLWE-derived) LWE key: the TLU starts with the keyswitch
+    cts = B.lwe_encrypt(glwe_sk, pts, p.big_n, B.secure_std(p.k, p.N), 7804)
+    dev = "cuda:0"
+    s = torch_cuda.cuda.current_stream().cuda_stream
+    # LUT encoding on the device, signed and unsigned tables as two batched calls
+    d_tab = B.to_device(np.stack(tables), dev)
+    d_lut = torch_cuda.empty((len(cases), p.N), dtype=torch_cuda.int64, device=dev)
+    for signed in (False, True):
+        for ci in [i for i, sg in enumerate(signs) if sg == signed]:
+            assert L.concrete_hip_encode_expand_lut_device(s, 0, d_lut[ci].data_ptr(), p.N, d_tab[ci].data_ptr(),
+                                                           256, 1, bits, int(signed)) == 0
+    d_acc = torch_cuda.empty((len(cases), p.glwe_size), dtype=torch_cuda.int64, device=dev)
+    assert L.concrete_hip_build_accumulators(s, 0, d_acc.data_ptr(), d_lut.data_ptr(), len(cases), p.k, p.N) == 0
+    kb = B.RuntimeBuffer(ksk)
+    try:
+        d_small = B.keyswitch(p, kb, B.to_device(cts, dev))
+        out = B.pbs(p, fbsk, d_small, d_acc, lut_idx=B.to_device(np.array(lut_idx, dtype=np.uint64), dev))
+        torch_cuda.cuda.synchronize()
+    finally:
+        kb.free()
+    op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, ks_l=p.ks_level, ks_logB=p.ks_base_log)
+    assert np.array_equal(B.to_host(d_small), oracle.keyswitch_batch(op, cts, ksk))
+    host_luts = np.stack([B.expand_lut(t, p.N, bits, sg) for t, sg in zip(tables, signs)])
+    assert np.array_equal(B.to_host(d_lut), host_luts)
+    dec = B.lwe_decrypt(glwe_sk, B.to_host(out), p.big_n)
+    assert [B.decode(d, bits, sg) for d, (_, sg) in zip(dec, expect)] == [e for e, _ in expect]

@@ -377,7 +377,8 @@ struct StepArgs {
   uint32_t base;   // first sample of the chunk
   uint32_t count;  // samples in the chunk
   uint32_t n, k, level, base_log, bits, limbs, subs;
-  uint32_t step;  // FRONT: the mask position whose rotation is prepared
+  uint32_t step;     // FRONT: the mask position whose rotation is prepared
+  const cplx* Tau;   // four-step column twiddles [R][512] (gen_big_step_kernel)
 };
 
 enum { MODE_INIT = 1, MODE_BACK = 2, MODE_FRONT = 4 };
@@ -597,6 +598,294 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
     if (a.resid) {
       for (int off = 32; off > 0; off >>= 1) max_resid = fmax(max_resid, __shfl_xor(max_resid, off));
       if ((threadIdx.x & 63) == 0) atomicMax(a.resid, (unsigned long long)__double_as_longlong(max_resid));
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// N >= 2048: four-step step kernel.  The M-point transform (M = R x 512) splits into R rows of
+// 512 points (row j1 = the coefficients n = j1 + R J, J < 1024, folded as J and J + 512) done by
+// the one-wave fft512 transforms (fft512.hpp) in registers, and 512 R-point column DFTs across
+// the rows, one LDS exchange apart: with j = j1 + R j2 and f = k2 + 512 k1,
+//   Z_f = sum_j1 w_R^{j1 k1} tau(j1, k2) FFT512_j1[k2],  tau(j1, k2) = zeta_N^{j1} w_M^{j1 k2},
+// where FFT512_j1 is the row's 512-point transform with its own twist zeta_N^R = exp(i pi / 1024)
+// (exactly the twist fft512 folds into its first pass), and the inverse runs the same steps
+// backwards with conjugate twiddles.  Each path through the transform still takes log2 M
+// butterfly stages and at most log2 M inexact twiddle products (fft512's stages, tau, and at
+// most two inexact constants inside an R-point DFT of log2 R stages), each within the mu = 5u of
+// the certified bound (tau: one correctly rounded table entry), so generic_error_bound holds
+// unchanged; the tests check the measured residual against it.
+// Against gen_step_kernel<M> (one polynomial per workgroup through log M / 3 radix-8 LDS passes
+// of the whole polynomial, ~10 barriers per transform, digit spectra staged through HBM at
+// M = 8192): one LDS round trip of the polynomial and two barriers per transform.
+// Data layout: spectra in the order f' = k1 512 + pos (pos = slot 64 + lane of fft512's
+// output, frequency k2 = fft512_freq(lane, slot)); the Fourier key is stored in the same order
+// (gen_convert_kernel, perm), the product kernels are elementwise and unchanged.  Accumulators
+// in row order, acc[j1 1024 + J] (gen_extract_kernel, rlog).
+// LDS: R rows of 576 complex (512 + the pad that makes room for a wave's transpose scratch in
+// its own first row), the fft512 tables: 158 KB at M = 8192, one workgroup of 8 waves per CU.
+// ------------------------------------------------------------------------------------------
+template <int M>
+struct Big {
+  static constexpr int R = M / 512;
+  static constexpr int LOGR = R == 2 ? 1 : R == 4 ? 2 : R == 8 ? 3 : 4;
+  static constexpr int NW = R < 8 ? R : 8;  // waves
+  static constexpr int SPW = R / NW;        // rows per wave
+  static constexpr int NT = 64 * NW;
+  static constexpr int CPT = 512 / NT;      // column positions per thread
+  static constexpr int RS = 576;            // row stride (complex)
+  static constexpr int BIG = R * RS;
+  static constexpr int LDS = (BIG + FFT512_TABLE_ENTRIES) * 16;
+  static_assert((1 << LOGR) == R && R <= 16 && RS >= XCH_SLOTS, "rows");
+  static_assert(BIG >= M && LDS <= 160 * 1024, "LDS");
+};
+constexpr int ROWLEN = 1024;  // coefficients per row (N / R)
+
+// frequency held at spectrum position p of the four-step order
+__host__ __device__ constexpr uint32_t big_freq(uint32_t p) {
+  return (uint32_t)fft512_freq((int)(p & 63), (int)((p >> 6) & 7)) + 512u * (p >> 9);
+}
+
+// R-point DFT across the rows, natural order in and out (forward exp(-2 pi i jk/R), inverse +)
+constexpr double C16_1 = 0.92387953251128675613, S16_1 = 0.38268343236508977173;  // cos, sin pi/8
+constexpr double R2H = 0.70710678118654752440;
+template <int R, bool INV>
+__device__ __forceinline__ void dft_col(cplx (&u)[R]) {
+  if constexpr (R == 2) {
+    const cplx x0 = u[0], x1 = u[1];
+    u[0] = cadd(x0, x1);
+    u[1] = csub(x0, x1);
+  } else if constexpr (R == 4) {
+    const cplx t0 = cadd(u[0], u[2]), t1 = csub(u[0], u[2]);
+    const cplx t2 = cadd(u[1], u[3]), t3 = mul_mi<INV>(csub(u[1], u[3]));
+    u[0] = cadd(t0, t2);
+    u[2] = csub(t0, t2);
+    u[1] = cadd(t1, t3);
+    u[3] = csub(t1, t3);
+  } else if constexpr (R == 8) {
+    dft8<INV>(u);
+  } else {
+    static_assert(R == 16, "column radix");
+    // even / odd halves, then X[k] = E[k] + w16^k O[k], X[k + 8] = E[k] - w16^k O[k]
+    cplx e[8], o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e[i] = u[2 * i], o[i] = u[2 * i + 1];
+    dft8<INV>(e);
+    dft8<INV>(o);
+    const cplx w16[8] = {{1.0, 0.0},     {C16_1, -S16_1}, {R2H, -R2H},     {S16_1, -C16_1},
+                         {0.0, -1.0},    {-S16_1, -C16_1}, {-R2H, -R2H},   {-C16_1, -S16_1}};
+#pragma unroll
+    for (int k = 1; k < 8; ++k) o[k] = k == 4 ? mul_mi<INV>(o[4]) : INV ? cmulc(o[k], w16[k]) : cmul(o[k], w16[k]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      u[k] = cadd(e[k], o[k]);
+      u[k + 8] = csub(e[k], o[k]);
+    }
+  }
+}
+
+// W32: decomposition state and digits in 32 bits (level * base_log <= 31), else 64
+template <int M, int MODE, bool W32>
+__global__ void __launch_bounds__(Big<M>::NT) gen_big_step_kernel(StepArgs a) {
+  using G = Big<M>;
+  constexpr int N = 2 * M, R = G::R, LOGR = G::LOGR, SPW = G::SPW, NT = G::NT, CPT = G::CPT, RS = G::RS;
+  constexpr int LOG2_2N = Geo<M>::LOG + 2;
+  using St = typename std::conditional<W32, uint32_t, uint64_t>::type;
+  using Dg = typename std::conditional<W32, int32_t, int64_t>::type;
+  __shared__ cplx lds[G::BIG + FFT512_TABLE_ENTRIES];
+  cplx* E = lds;  // rows j1 at E + j1 RS
+  build_fft512_tables(lds + G::BIG, threadIdx.x, NT);
+  const Fft512Tables T = fft512_tables_at(lds + G::BIG);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  cplx* xch = E + w * SPW * RS;  // transpose scratch: the wave's first row and its pad
+  const uint32_t K1 = a.k + 1, poly = blockIdx.x, ct = poly / K1, c = poly % K1;
+  const uint32_t s = a.base + ct;
+  const uint64_t row = a.in_idx ? a.in_idx[s] : s;
+  const uint64_t* lwe = a.in + row * (uint64_t)(a.n + 1);
+  uint64_t* acc = a.acc + (uint64_t)poly * N;
+  // this thread's column positions and rows / coefficients: row jrow(sr), J = jcol(e) (e < 8:
+  // the real parts J = lane + 64 e, e >= 8: the imaginary parts J + 512)
+  auto pos_of = [&](int p) { return (int)threadIdx.x + p * NT; };
+  auto jrow = [&](int sr) { return w * SPW + sr; };
+  auto jcol = [&](int e) { return lane + 64 * (e & 7) + 512 * (e >> 3); };
+  // column twiddles tau(j1, pos), applied by the row waves (row j1 = jrow(sr), positions
+  // e 64 + lane): in registers for SPW = 1; at R = 16 (16 per thread next to the accumulator's 32
+  // words) they are read (L2) as each row is transformed
+  constexpr bool TAUREG = SPW == 1;
+  cplx tau_r[TAUREG ? 8 : 1];
+  if constexpr (TAUREG)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tau_r[e] = a.Tau[jrow(0) * 512 + e * 64 + lane];
+  auto tau = [&](int sr, int e) -> cplx {
+    if constexpr (TAUREG) {
+      return tau_r[e];
+    } else {
+      const cplx* tp = a.Tau;
+      asm volatile("" : "+s"(tp));  // not loop-invariant: read where it is used
+      return tp[jrow(sr) * 512 + e * 64 + lane];
+    }
+  };
+  uint64_t A[SPW][16];
+  double max_resid = 0.0;
+
+  if constexpr ((MODE & MODE_INIT) != 0) {
+    // acc_c = LUT_c * X^{-ms(b)} (blind_rotate_assign: polynomial_wrapping_monic_monomial_div)
+    const uint64_t* lut = a.luts + (a.lut_idx ? a.lut_idx[s] : 0ull) * (uint64_t)(K1 * N) + (uint64_t)c * N;
+    const uint32_t bt = modswitch(lwe[a.n], LOG2_2N);
+#pragma unroll
+    for (int sr = 0; sr < SPW; ++sr)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const uint32_t src = ((uint32_t)(jrow(sr) + R * jcol(e)) + bt) & (2 * N - 1);
+        const uint64_t v = lut[src & (N - 1)];
+        A[sr][e] = src < (uint32_t)N ? v : 0ull - v;
+      }
+  } else {
+#pragma unroll
+    for (int sr = 0; sr < SPW; ++sr)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) A[sr][e] = acc[jrow(sr) * ROWLEN + jcol(e)];
+  }
+  pair_barrier();  // fft512 tables
+
+  if constexpr ((MODE & MODE_BACK) != 0) {
+    // acc += sum_m 2^{m b} round(iFFT(Y_m) conj(zeta^j)); the key spectra carry the 1/M
+    const cplx* Yc = a.Y + (uint64_t)poly * a.limbs * M;
+#pragma unroll 1
+    for (uint32_t m = 0; m < a.limbs; ++m) {
+      const cplx* Ym = Yc + (uint64_t)m * M;
+#pragma unroll
+      for (int p = 0; p < CPT; ++p) {
+        cplx u[R];
+#pragma unroll
+        for (int k1 = 0; k1 < R; ++k1) u[k1] = Ym[k1 * 512 + pos_of(p)];
+        dft_col<R, true>(u);
+#pragma unroll
+        for (int j1 = 0; j1 < R; ++j1) E[j1 * RS + pos_of(p)] = u[j1];
+      }
+      pair_barrier();
+      const uint32_t sh = m * a.bits;
+#pragma unroll
+      for (int sr = 0; sr < SPW; ++sr) {
+        // row 0 of the wave is read whole before its transform writes the scratch over it
+        cplx v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = E[jrow(sr) * RS + e * 64 + lane];
+        wave_lds_fence();
+        if (jrow(sr) != 0)  // tau(0, .) = 1
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = cmulc(v[e], tau(sr, e));
+        fft512_inv(v, xch, T, lane);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const double tr = v[e].re + RND_MAGIC, ti = v[e].im + RND_MAGIC;
+          max_resid = fmax(max_resid, fmax(fabs(v[e].re - (tr - RND_MAGIC)), fabs(v[e].im - (ti - RND_MAGIC))));
+          if (sh < 64) {
+            A[sr][e] += ((uint64_t)__double_as_longlong(tr) - RND_MAGIC_BITS) << sh;
+            A[sr][e + 8] += ((uint64_t)__double_as_longlong(ti) - RND_MAGIC_BITS) << sh;
+          }
+        }
+      }
+      pair_barrier();
+    }
+  }
+
+  if constexpr ((MODE & (MODE_BACK | MODE_INIT)) != 0) {
+#pragma unroll
+    for (int sr = 0; sr < SPW; ++sr)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[jrow(sr) * ROWLEN + jcol(e)] = A[sr][e];
+  }
+
+  if constexpr ((MODE & MODE_FRONT) != 0) {
+    // ct1 = X^{ms(a_i)} acc - acc through the LDS copy of the accumulator (row order)
+    const uint32_t at = modswitch(lwe[a.step], LOG2_2N);
+    uint64_t* accl = reinterpret_cast<uint64_t*>(E);
+#pragma unroll
+    for (int sr = 0; sr < SPW; ++sr)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) accl[jrow(sr) * ROWLEN + jcol(e)] = A[sr][e];
+    pair_barrier();
+    const int nrep = 64 - (int)(a.level * a.base_log);
+    St S[SPW][16];
+#pragma unroll
+    for (int sr = 0; sr < SPW; ++sr)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const uint32_t src = ((uint32_t)(jrow(sr) + R * jcol(e)) - at) & (2 * N - 1);
+        const uint32_t idx = src & (N - 1);
+        const uint64_t rv = accl[(idx & (R - 1)) * ROWLEN + (idx >> LOGR)];
+        const uint64_t x = (src < (uint32_t)N ? rv : 0ull - rv) - A[sr][e];
+        S[sr][e] = (St)(nrep > 0 ? decomp_init(x, nrep) : x);
+      }
+    pair_barrier();
+    cplx* Xc = a.X + (uint64_t)poly * a.level * a.subs * M;
+    const int logB = (int)a.base_log, sb = (int)a.bits;
+    const St half = (St)1 << (sb - 1), bmask = ((St)1 << sb) - (St)1;
+#pragma unroll 1
+    for (uint32_t q = 0; q < a.level; ++q) {
+      Dg D[SPW][16];
+#pragma unroll
+      for (int sr = 0; sr < SPW; ++sr)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          if constexpr (W32) D[sr][e] = decomp_next_t<uint32_t>(S[sr][e], logB);
+          else D[sr][e] = decomp_next64(S[sr][e], logB);
+        }
+#pragma unroll 1
+      for (uint32_t t = 0; t < a.subs; ++t) {
+        cplx hold[8];  // SPW = 2: the first row's spectrum, until the second row's transform is done
+#pragma unroll
+        for (int sr = 0; sr < SPW; ++sr) {
+          cplx v[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            Dg s0 = D[sr][e], s1 = D[sr][e + 8];
+            if (a.subs > 1) {  // balanced b-bit sub-digit, exact: D - s is a multiple of 2^b
+              s0 = (Dg)(((St)D[sr][e] + half) & bmask) - (Dg)half;
+              s1 = (Dg)(((St)D[sr][e + 8] + half) & bmask) - (Dg)half;
+              D[sr][e] = (D[sr][e] - s0) >> sb;
+              D[sr][e + 8] = (D[sr][e + 8] - s1) >> sb;
+            }
+            v[e] = {(double)s0, (double)s1};
+          }
+          fft512_fwd(v, xch, T, lane);
+          if (jrow(sr) != 0)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = cmul(v[e], tau(sr, e));
+          if (SPW == 2 && sr == 0) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) hold[e] = v[e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) E[jrow(sr) * RS + e * 64 + lane] = v[e];
+          }
+        }
+        if constexpr (SPW == 2) {
+          wave_lds_fence();
+#pragma unroll
+          for (int e = 0; e < 8; ++e) E[jrow(0) * RS + e * 64 + lane] = hold[e];
+        }
+        pair_barrier();
+        cplx* dst = Xc + ((uint64_t)q * a.subs + t) * M;
+#pragma unroll
+        for (int p = 0; p < CPT; ++p) {
+          cplx u[R];
+#pragma unroll
+          for (int j1 = 0; j1 < R; ++j1) u[j1] = E[j1 * RS + pos_of(p)];
+          dft_col<R, false>(u);
+#pragma unroll
+          for (int k1 = 0; k1 < R; ++k1) dst[k1 * 512 + pos_of(p)] = u[k1];
+        }
+        pair_barrier();
+      }
+    }
+  }
+
+  if constexpr ((MODE & MODE_BACK) != 0) {
+    if (a.resid) {
+      for (int off = 32; off > 0; off >>= 1) max_resid = fmax(max_resid, __shfl_xor(max_resid, off));
+      if (lane == 0) atomicMax(a.resid, (unsigned long long)__double_as_longlong(max_resid));
     }
   }
 }
@@ -1102,11 +1391,14 @@ __global__ void __launch_bounds__((TileGeo<M, K1, KL, T, L, C>::NT)) gen_tile_ke
   }
 }
 
-// sample extract (nth = 0): out[r N + 0] = A_r[0], out[r N + j] = -A_r[N - j], out[k N] = B[0]
+// sample extract (nth = 0): out[r N + 0] = A_r[0], out[r N + j] = -A_r[N - j], out[k N] = B[0].
+// rlog > 0: accumulators in the four-step row order (coefficient n at (n mod R) N/R + n / R).
 __global__ void gen_extract_kernel(uint64_t* out, const uint64_t* out_idx, const uint64_t* acc, uint32_t base,
-                                   uint32_t count, uint32_t k, uint32_t N) {
+                                   uint32_t count, uint32_t k, uint32_t N, uint32_t rlog) {
   const uint64_t width = (uint64_t)k * N + 1;
   const uint64_t total = width * count;
+  const uint32_t rmask = (1u << rlog) - 1u, rowlen = N >> rlog;
+  auto at = [&](uint32_t j) { return (j & rmask) * rowlen + (j >> rlog); };
   for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < total; g += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t ct = (uint32_t)(g / width), e = (uint32_t)(g % width);
     const uint32_t s = base + ct;
@@ -1114,22 +1406,25 @@ __global__ void gen_extract_kernel(uint64_t* out, const uint64_t* out_idx, const
     const uint64_t* A = acc + (uint64_t)ct * (k + 1) * N;
     uint64_t v;
     if (e == k * N) {
-      v = A[(uint64_t)k * N];
+      v = A[(uint64_t)k * N];  // coefficient 0 sits at 0 in either order
     } else {
       const uint32_t r = e / N, j = e % N;
-      const uint64_t x = A[(uint64_t)r * N + ((N - j) & (N - 1))];
+      const uint64_t x = A[(uint64_t)r * N + at((N - j) & (N - 1))];
       v = j == 0 ? x : 0ull - x;
     }
     out[orow * width + e] = v;
   }
 }
 
-// Fourier key: G[i][c][lim][r][q][f] = FFT(twist(limb_lim(std[i][l-1-q][r][c])))[f] / M
+// Fourier key: G[i][c][lim][r][q][f] = FFT(twist(limb_lim(std[i][l-1-q][r][c])))[f] / M, frequencies
+// in natural order, or (perm) in the four-step order of gen_big_step_kernel: position p holds
+// frequency big_freq(p)
 template <int M>
 __global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, const uint64_t* src, const cplx* Wfull,
                                                                         const cplx* Wlo,
                                                                         const cplx* Whi, const cplx* Z, uint32_t k,
-                                                                        uint32_t level, uint32_t bits, uint32_t limbs) {
+                                                                        uint32_t level, uint32_t bits, uint32_t limbs,
+                                                                        uint32_t perm) {
   constexpr int N = 2 * M, TH = Geo<M>::THREADS, VPT = Geo<M>::VPT;
   constexpr bool PP = M <= 4096;  // as gen_step_kernel
   __shared__ cplx buf[M + (PP ? tile_tw_entries<M, TH>() : tw_entries<M>())];
@@ -1179,8 +1474,9 @@ __global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, c
     cplx* dst = G + ((((i * K1 + c) * limbs + lim) * K1 + r) * level + q) * (uint64_t)M;
 #pragma unroll
     for (int e = 0; e < VPT; ++e) {
-      const cplx x = buf[sw(tid + e * TH)];
-      dst[tid + e * TH] = {x.re * scale, x.im * scale};
+      const uint32_t p = tid + e * TH;
+      const cplx x = buf[sw(perm ? (int)big_freq(p) : (int)p)];
+      dst[p] = {x.re * scale, x.im * scale};
     }
     __syncthreads();
   }
@@ -1194,7 +1490,16 @@ struct Tables {
   cplx* Wlo = nullptr;  // e^{-2 pi i j/M}, j < TW_LO
   cplx* Whi = nullptr;  // e^{-2 pi i j TW_LO/M}, j < max(1, M/TW_LO)
   cplx* Z = nullptr;    // zeta^j, j < M
+  cplx* Tau = nullptr;  // four-step column twiddles tau(j1, k2(pos)) [R][512] (M >= 1024)
 };
+
+// Whether N runs on the four-step step kernel (and its keys are converted to the four-step
+// frequency order).  CONCRETE_HIP_GEN_FOURSTEP=0 selects gen_step_kernel for A/B runs; the choice
+// is made once per process, so conversion and PBS always agree.
+static bool four_step(uint32_t N) {
+  static const bool on = !getenv("CONCRETE_HIP_GEN_FOURSTEP") || atoi(getenv("CONCRETE_HIP_GEN_FOURSTEP")) != 0;
+  return on && N >= 2048 && N <= 16384;
+}
 
 // Twiddle and twist tables for polynomial size N on the current device, built once in long
 // double (correctly rounded to f64) and kept for the life of the process.
@@ -1223,6 +1528,18 @@ static Tables tables_for(uint32_t N) {
   CHIP_CHECK(hipMemcpy(t.Wlo, lo.data(), TW_LO * sizeof(cplx), hipMemcpyHostToDevice));
   CHIP_CHECK(hipMemcpy(t.Whi, hi.data(), NHI * sizeof(cplx), hipMemcpyHostToDevice));
   CHIP_CHECK(hipMemcpy(t.Z, z.data(), M * sizeof(cplx), hipMemcpyHostToDevice));
+  if (M >= 1024) {
+    // tau(j1, k2) = zeta^{j1} w_M^{j1 k2} = exp(i pi j1 (1 - 4 k2) / N), correctly rounded
+    const uint32_t R = M / 512;
+    std::vector<cplx> tau((size_t)R * 512);
+    for (uint32_t j1 = 0; j1 < R; ++j1)
+      for (uint32_t p = 0; p < 512; ++p) {
+        const int64_t e = ((int64_t)j1 * (1 - 4 * (int64_t)big_freq(p))) % (2 * (int64_t)N);
+        tau[(size_t)j1 * 512 + p] = ex(PI * (long double)(e < 0 ? e + 2 * (int64_t)N : e) / (long double)N);
+      }
+    CHIP_CHECK(hipMalloc((void**)&t.Tau, tau.size() * sizeof(cplx)));
+    CHIP_CHECK(hipMemcpy(t.Tau, tau.data(), tau.size() * sizeof(cplx), hipMemcpyHostToDevice));
+  }
   cache[{dev, N}] = t;
   return t;
 }
@@ -1234,8 +1551,26 @@ static void launch_step(const StepArgs& s, uint32_t K1, hipStream_t st) {
   hipLaunchKernelGGL((gen_step_kernel<M, MODE>), dim3(blocks), dim3(Geo<M>::BLOCK), 0, st, s);
 }
 
+template <int M, int MODE>
+static void launch_big_step(const StepArgs& s, uint32_t K1, hipStream_t st) {
+  const uint32_t blocks = s.count * K1;  // one workgroup per polynomial
+  if (s.level * s.base_log <= 31)
+    hipLaunchKernelGGL((gen_big_step_kernel<M, MODE, true>), dim3(blocks), dim3(Big<M>::NT), 0, st, s);
+  else
+    hipLaunchKernelGGL((gen_big_step_kernel<M, MODE, false>), dim3(blocks), dim3(Big<M>::NT), 0, st, s);
+}
+
 template <int MODE>
 static int step_dispatch(uint32_t N, const StepArgs& s, uint32_t K1, hipStream_t st) {
+  if (four_step(N)) {
+    switch (N) {
+      case 2048: launch_big_step<1024, MODE>(s, K1, st); return 0;
+      case 4096: launch_big_step<2048, MODE>(s, K1, st); return 0;
+      case 8192: launch_big_step<4096, MODE>(s, K1, st); return 0;
+      case 16384: launch_big_step<8192, MODE>(s, K1, st); return 0;
+      default: return -2;
+    }
+  }
   switch (N) {
     case 256: launch_step<128, MODE>(s, K1, st); break;
     case 512: launch_step<256, MODE>(s, K1, st); break;
@@ -1330,7 +1665,7 @@ int pbs_generic_launch(const PbsArgs& a) {
   for (uint32_t base = 0; base < a.num_samples && rc == 0; base += chunk) {
     const uint32_t cnt = std::min(chunk, a.num_samples - base);
     StepArgs s{acc,  X,    Y,   tb.Wfull, tb.Wlo, tb.Whi,  tb.Z,       a.in, a.in_idx, a.luts, a.lut_idx,
-               a.resid, base, cnt, a.n,    a.k,     a.level, a.base_log, b,    L,        T,      0};
+               a.resid, base, cnt, a.n,    a.k,     a.level, a.base_log, b,    L,        T,      0, tb.Tau};
     rc = step_dispatch<MODE_INIT | MODE_FRONT>(a.N, s, K1, a.stream);
     MacArgs m{X, Y, reinterpret_cast<const cplx*>(a.fbsk), cnt, a.k, a.level, L, T, M, 0};
     const dim3 mg((M + 255) / 256, K1 * L, (cnt + MAC_CTS - 1) / MAC_CTS);
@@ -1343,8 +1678,9 @@ int pbs_generic_launch(const PbsArgs& a) {
     }
     const uint64_t total = ((uint64_t)a.k * a.N + 1) * cnt;
     const uint32_t eb = (uint32_t)std::min<uint64_t>((total + 255) / 256, 65535);
+    const uint32_t rlog = four_step(a.N) ? (uint32_t)__builtin_ctz(M / 512) : 0u;
     hipLaunchKernelGGL(gen_extract_kernel, dim3(eb), dim3(256), 0, a.stream, a.out, a.out_idx, acc, base, cnt, a.k,
-                       a.N);
+                       a.N, rlog);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       set_error("generic pbs launch failed: %s", hipGetErrorString(e));
@@ -1368,7 +1704,8 @@ int convert_bsk_generic_launch(const ConvertArgs& a) {
   cplx* G = reinterpret_cast<cplx*>(a.dest);
 #define GEN_CONV(MM)                                                                                        \
   hipLaunchKernelGGL(gen_convert_kernel<MM>, dim3((uint32_t)blocks), dim3(Geo<MM>::THREADS), 0, a.stream, G, \
-                     a.src_dev, tb.Wfull, tb.Wlo, tb.Whi, tb.Z, a.k, a.level, fmt.bits, fmt.limbs)
+                     a.src_dev, tb.Wfull, tb.Wlo, tb.Whi, tb.Z, a.k, a.level, fmt.bits, fmt.limbs,        \
+                     four_step(a.N) ? 1u : 0u)
   switch (a.N) {
     case 256: GEN_CONV(128); break;
     case 512: GEN_CONV(256); break;

@@ -43,6 +43,10 @@ CASES = [
     # shapes off the tile kernels' instances (T = 1): the two-launch path at N = 512 and 1024
     ("k3_N512_T1_two_launch", 3, 512, 12, 1, 12, 3),
     ("k2_N1024_l2_two_launch", 2, 1024, 10, 2, 10, 3),
+    # four-step kernel with a 64-bit decomposition state (level * logB > 31): R = 4, 8, 16 rows
+    ("k1_N4096_l3_wide_state", 1, 4096, 4, 3, 12, 3),
+    ("k1_N8192_l2_wide_state", 1, 8192, 3, 2, 17, 4),
+    ("k1_N16384_l3_wide_state", 1, 16384, 2, 3, 11, 3),
 ]
 
 
@@ -144,6 +148,26 @@ def test_generic_index_arrays(B, oracle, torch_cuda, ci):
     ref, _ = oracle.pbs_batch(op, cts, luts, bsk=bsk, mode=oracle.MODE_KARATSUBA, lut_idx=lut_idx, in_idx=in_idx,
                               out_idx=out_idx)
     assert np.array_equal(B.to_host(out), ref)
+
+
+def test_generic_legacy_step_kernel(B, oracle, torch_cuda):
+    """CONCRETE_HIP_GEN_FOURSTEP=0 (natural-order keys, gen_step_kernel) stays bit-exact: the
+    N = 4096 and 16384 rows in a child process, since the choice is made once per process."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path.insert(0, %r); import tests.test_gpu_pbs_generic as T; "
+        "from concrete_amd import backend as B; import oracle.pyoracle as O; import torch, numpy as np\n"
+        "for ci in (5, 7):\n"
+        "    p, glwe_sk, bsk, fbsk, cts, acc, table, msgs, got, resid = T.run_case(B, O, torch, T.CASES[ci], 7600)\n"
+        "    op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)\n"
+        "    ref, _ = O.pbs_batch(op, cts, acc[None, :], bsk=bsk, mode=O.MODE_KARATSUBA)\n"
+        "    assert np.array_equal(got, ref), T.CASES[ci][0]\n"
+        "print('legacy ok')\n" % os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = dict(os.environ, CONCRETE_HIP_GEN_FOURSTEP="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "legacy ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
 def test_generic_outside_exact_range_refused(B):

@@ -378,7 +378,7 @@ struct StepArgs {
   uint32_t count;  // samples in the chunk
   uint32_t n, k, level, base_log, bits, limbs, subs;
   uint32_t step;     // FRONT: the mask position whose rotation is prepared
-  const cplx* Tau;   // four-step column twiddles [R][512] (gen_big_step_kernel)
+  const cplx* Tau;   // four-step column twiddles [R][512] + row/slot factors [R][8] (gen_big_step_kernel)
 };
 
 enum { MODE_INIT = 1, MODE_BACK = 2, MODE_FRONT = 4 };
@@ -623,7 +623,8 @@ __global__ void __launch_bounds__(Geo<M>::BLOCK) gen_step_kernel(StepArgs a) {
 // (gen_convert_kernel, perm), the product kernels are elementwise and unchanged.  Accumulators
 // in row order, acc[j1 1024 + J] (gen_extract_kernel, rlog).
 // LDS: R rows of 576 complex (512 + the pad that makes room for a wave's transpose scratch in
-// its own first row), the fft512 tables: 158 KB at M = 8192, one workgroup of 8 waves per CU.
+// its own first row), the fft512 tables, at R = 16 the column-twiddle slot factors beta: 160 KB
+// at M = 8192, one workgroup of 8 waves per CU.
 // ------------------------------------------------------------------------------------------
 template <int M>
 struct Big {
@@ -635,7 +636,8 @@ struct Big {
   static constexpr int CPT = 512 / NT;      // column positions per thread
   static constexpr int RS = 576;            // row stride (complex)
   static constexpr int BIG = R * RS;
-  static constexpr int LDS = (BIG + FFT512_TABLE_ENTRIES) * 16;
+  static constexpr int BETA = SPW == 1 ? 0 : R * 8;  // tau slot factors in LDS (rows per wave > 1)
+  static constexpr int LDS = (BIG + FFT512_TABLE_ENTRIES + BETA) * 16;
   static_assert((1 << LOGR) == R && R <= 16 && RS >= XCH_SLOTS, "rows");
   static_assert(BIG >= M && LDS <= 160 * 1024, "LDS");
 };
@@ -692,9 +694,11 @@ __global__ void __launch_bounds__(Big<M>::NT) gen_big_step_kernel(StepArgs a) {
   constexpr int LOG2_2N = Geo<M>::LOG + 2;
   using St = typename std::conditional<W32, uint32_t, uint64_t>::type;
   using Dg = typename std::conditional<W32, int32_t, int64_t>::type;
-  __shared__ cplx lds[G::BIG + FFT512_TABLE_ENTRIES];
+  __shared__ cplx lds[G::BIG + FFT512_TABLE_ENTRIES + G::BETA];
   cplx* E = lds;  // rows j1 at E + j1 RS
   build_fft512_tables(lds + G::BIG, threadIdx.x, NT);
+  cplx* beta = lds + G::BIG + FFT512_TABLE_ENTRIES;
+  for (int x = threadIdx.x; x < G::BETA; x += NT) beta[x] = a.Tau[R * 512 + x];
   const Fft512Tables T = fft512_tables_at(lds + G::BIG);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   cplx* xch = E + w * SPW * RS;  // transpose scratch: the wave's first row and its pad
@@ -709,20 +713,30 @@ __global__ void __launch_bounds__(Big<M>::NT) gen_big_step_kernel(StepArgs a) {
   auto jrow = [&](int sr) { return w * SPW + sr; };
   auto jcol = [&](int e) { return lane + 64 * (e & 7) + 512 * (e >> 3); };
   // column twiddles tau(j1, pos), applied by the row waves (row j1 = jrow(sr), positions
-  // e 64 + lane): in registers for SPW = 1; at R = 16 (16 per thread next to the accumulator's 32
-  // words) they are read (L2) as each row is transformed
+  // e 64 + lane): in registers for SPW = 1.  At R = 16 (16 per thread would not fit next to the
+  // accumulator's 32 words) tau(j1, e 64 + lane) = alpha(j1, lane) beta(j1, e), the lane factor
+  // alpha = tau(j1, lane) in registers and the slot factor beta(j1, e) = exp(-256 i pi j1 e / N)
+  // from LDS (a broadcast read): no global load inside the row phases, whose vmcnt(0) waits would
+  // also drain the next slot's prefetched columns.  Both factors are correctly rounded, so the
+  // computed twiddle is within 3u of tau (0.5u + 0.5u + 2u for the FMA complex product), inside
+  // the mu = 5u the certified bound allows each twiddle.
   constexpr bool TAUREG = SPW == 1;
-  cplx tau_r[TAUREG ? 8 : 1];
-  if constexpr (TAUREG)
+  cplx tau_r[TAUREG ? 8 : SPW];
+  if constexpr (TAUREG) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) tau_r[e] = a.Tau[jrow(0) * 512 + e * 64 + lane];
+  } else {
+#pragma unroll
+    for (int sr = 0; sr < SPW; ++sr) tau_r[sr] = a.Tau[jrow(sr) * 512 + lane];
+  }
   auto tau = [&](int sr, int e) -> cplx {
     if constexpr (TAUREG) {
       return tau_r[e];
     } else {
-      const cplx* tp = a.Tau;
-      asm volatile("" : "+s"(tp));  // not loop-invariant: read where it is used
-      return tp[jrow(sr) * 512 + e * 64 + lane];
+#ifdef DG_NOTAU  // timing diagnostic only (wrong results)
+      return cplx{1.0, 0.0};
+#endif
+      return e == 0 ? tau_r[sr] : cmul(tau_r[sr], beta[jrow(sr) * 8 + e]);
     }
   };
   uint64_t A[SPW][16];
@@ -751,20 +765,44 @@ __global__ void __launch_bounds__(Big<M>::NT) gen_big_step_kernel(StepArgs a) {
   if constexpr ((MODE & MODE_BACK) != 0) {
     // acc += sum_m 2^{m b} round(iFFT(Y_m) conj(zeta^j)); the key spectra carry the 1/M
     const cplx* Yc = a.Y + (uint64_t)poly * a.limbs * M;
+    // slot m + 1's columns are loaded while slot m's rows are transformed (the registers of the
+    // column DFT are free then): the HBM read of the next slot overlaps the row transforms
+    cplx pf[CPT][R];
+    auto load_cols = [&](uint32_t m) {
+      const cplx* Ym = Yc + (uint64_t)m * M;
+#pragma unroll
+      for (int p = 0; p < CPT; ++p)
+#pragma unroll
+        for (int k1 = 0; k1 < R; ++k1) {
+#ifdef DG_NOY  // timing diagnostic only (wrong results)
+          pf[p][k1] = cplx{(double)(k1 + m), (double)pos_of(p)};
+#else
+          pf[p][k1] = Ym[k1 * 512 + pos_of(p)];
+#endif
+        }
+    };
+    load_cols(0);
 #pragma unroll 1
     for (uint32_t m = 0; m < a.limbs; ++m) {
-      const cplx* Ym = Yc + (uint64_t)m * M;
 #pragma unroll
       for (int p = 0; p < CPT; ++p) {
         cplx u[R];
 #pragma unroll
-        for (int k1 = 0; k1 < R; ++k1) u[k1] = Ym[k1 * 512 + pos_of(p)];
+        for (int k1 = 0; k1 < R; ++k1) u[k1] = pf[p][k1];
+#ifndef DG_NOCOL
         dft_col<R, true>(u);
+#endif
 #pragma unroll
         for (int j1 = 0; j1 < R; ++j1) E[j1 * RS + pos_of(p)] = u[j1];
       }
+      // the next slot's loads stay behind the column DFT (hoisted above it, both arrays are live)
+      asm volatile("" ::: "memory");
+      if (m + 1 < a.limbs) load_cols(m + 1);
       pair_barrier();
-      const uint32_t sh = m * a.bits;
+      // slot shifts stay below 64: the top limb is 64 - (L - 1) b bits wide (key_format), so no
+      // guard (a per-element `sh < 64` test had become one branch per coefficient, with the
+      // accumulator spilled around each)
+      const uint32_t sh = (m * a.bits) & 63u;
 #pragma unroll
       for (int sr = 0; sr < SPW; ++sr) {
         // row 0 of the wave is read whole before its transform writes the scratch over it
@@ -775,15 +813,19 @@ __global__ void __launch_bounds__(Big<M>::NT) gen_big_step_kernel(StepArgs a) {
         if (jrow(sr) != 0)  // tau(0, .) = 1
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = cmulc(v[e], tau(sr, e));
-        fft512_inv(v, xch, T, lane);
+        // output twiddles read after the transpose (fft512_inv_tw): 32 fewer VGPRs live across
+        // it, which the next slot's prefetched columns need
+        cplx gi2[4];
+        inv_p2_stage_tw(gi2, T, lane & 7);
+#ifndef DG_NOROW
+        fft512_inv_tw(v, xch, T, lane, gi2, 0);
+#endif
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const double tr = v[e].re + RND_MAGIC, ti = v[e].im + RND_MAGIC;
           max_resid = fmax(max_resid, fmax(fabs(v[e].re - (tr - RND_MAGIC)), fabs(v[e].im - (ti - RND_MAGIC))));
-          if (sh < 64) {
-            A[sr][e] += ((uint64_t)__double_as_longlong(tr) - RND_MAGIC_BITS) << sh;
-            A[sr][e + 8] += ((uint64_t)__double_as_longlong(ti) - RND_MAGIC_BITS) << sh;
-          }
+          A[sr][e] += ((uint64_t)__double_as_longlong(tr) - RND_MAGIC_BITS) << sh;
+          A[sr][e + 8] += ((uint64_t)__double_as_longlong(ti) - RND_MAGIC_BITS) << sh;
         }
       }
       pair_barrier();
@@ -849,7 +891,9 @@ __global__ void __launch_bounds__(Big<M>::NT) gen_big_step_kernel(StepArgs a) {
             }
             v[e] = {(double)s0, (double)s1};
           }
+#ifndef DG_NOROW
           fft512_fwd(v, xch, T, lane);
+#endif
           if (jrow(sr) != 0)
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = cmul(v[e], tau(sr, e));
@@ -873,7 +917,9 @@ __global__ void __launch_bounds__(Big<M>::NT) gen_big_step_kernel(StepArgs a) {
           cplx u[R];
 #pragma unroll
           for (int j1 = 0; j1 < R; ++j1) u[j1] = E[j1 * RS + pos_of(p)];
+#ifndef DG_NOCOL
           dft_col<R, false>(u);
+#endif
 #pragma unroll
           for (int k1 = 0; k1 < R; ++k1) dst[k1 * 512 + pos_of(p)] = u[k1];
         }
@@ -1536,6 +1582,12 @@ static Tables tables_for(uint32_t N) {
       for (uint32_t p = 0; p < 512; ++p) {
         const int64_t e = ((int64_t)j1 * (1 - 4 * (int64_t)big_freq(p))) % (2 * (int64_t)N);
         tau[(size_t)j1 * 512 + p] = ex(PI * (long double)(e < 0 ? e + 2 * (int64_t)N : e) / (long double)N);
+      }
+    // slot factors beta(j1, e) = exp(-256 i pi j1 e / N) = tau(j1, e 64 + lane) / tau(j1, lane)
+    for (uint32_t j1 = 0; j1 < R; ++j1)
+      for (uint32_t e = 0; e < 8; ++e) {
+        const int64_t x = (-(int64_t)256 * j1 * e) % (2 * (int64_t)N);
+        tau.push_back(ex(PI * (long double)(x < 0 ? x + 2 * (int64_t)N : x) / (long double)N));
       }
     CHIP_CHECK(hipMalloc((void**)&t.Tau, tau.size() * sizeof(cplx)));
     CHIP_CHECK(hipMemcpy(t.Tau, tau.data(), tau.size() * sizeof(cplx), hipMemcpyHostToDevice));

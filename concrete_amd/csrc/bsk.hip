@@ -76,11 +76,9 @@ __device__ __forceinline__ double limb_value(uint64_t rem, uint32_t limb) {
   return (double)lv;
 }
 
-// In-LDS radix-2 DIT over buf (bit-reversed input, natural output, forward sign), then the
-// scatter into the PBS kernels' register layout: element e = (slot, lane) holds frequency
-// fft512_freq(lane, slot), scaled 1/M, stored at dst(e).
-template <int M, class Dst>
-__device__ __forceinline__ void dd_fft_scatter(ddc* buf, const ddc* __restrict__ tw_t, Dst dst) {
+// In-LDS radix-2 DIT over buf (bit-reversed input, natural output, forward sign)
+template <int M>
+__device__ __forceinline__ void dd_fft(ddc* buf, const ddc* __restrict__ tw_t) {
   for (int h = 1; h < M; h <<= 1) {
     for (int b = threadIdx.x; b < M / 2; b += blockDim.x) {
       const int grp = b / h, pos = b % h;
@@ -93,6 +91,13 @@ __device__ __forceinline__ void dd_fft_scatter(ddc* buf, const ddc* __restrict__
     }
     __syncthreads();
   }
+}
+
+// dd_fft, then the scatter into the PBS kernels' register layout: element e = (slot, lane) holds
+// frequency fft512_freq(lane, slot), scaled 1/M, stored at dst(e).
+template <int M, class Dst>
+__device__ __forceinline__ void dd_fft_scatter(ddc* buf, const ddc* __restrict__ tw_t, Dst dst) {
+  dd_fft<M>(buf, tw_t);
   const double scale = 1.0 / (double)M;
   for (int e = threadIdx.x; e < M; e += blockDim.x) {
     const int lane = e & 63, slot = e >> 6;
@@ -145,10 +150,50 @@ __global__ void __launch_bounds__(256) convert_bsk_kernel(cplx* __restrict__ des
 // the output layout [n][limb][col][row][parity][512]: the parity half p(u) = g[2u + par] of key
 // polynomial g (row, col), limb `limb`, as an N = 1024 negacyclic polynomial: folded, twisted,
 // transformed exactly like the N = 1024 key.
+#if P2_PM
+// P2_PM: block = (i, limb, col, row); both parity spectra G_e, G_o in double-double, then the key at
+// the square roots of each evaluation point, K+-[f] = (G_e[f] +- s_f G_o[f]) / 2 with
+// s_f = exp(i pi (1 - 4 f) / 2048) (s_f^2 = alpha_f), correctly rounded from double-double.  Layout
+// [n][limb][col][row][+-][slot][lane], scaled 1/512 like the even/odd key.
 template <int LIMBS>
 __global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__ dest, const uint64_t* __restrict__ src,
                                                              const ddc* __restrict__ zeta_t,
-                                                             const ddc* __restrict__ tw_t) {
+                                                             const ddc* __restrict__ tw_t,
+                                                             const ddc* __restrict__ sroot_t) {
+  constexpr int M = 512, LOGM = 9;
+  __shared__ ddc buf[2][M];
+  const uint64_t blk = blockIdx.x;
+  const uint32_t row = (uint32_t)(blk & 1), col = (uint32_t)((blk >> 1) & 1);
+  const uint32_t limb = (uint32_t)((blk >> 2) % LIMBS);
+  const uint64_t i = (blk >> 2) / LIMBS;
+  const uint64_t* g = src + (i * 4 + row * 2 + col) * 2048;  // [n][l = 1][row][col][N]
+  for (int e = threadIdx.x; e < 2 * M; e += blockDim.x) {
+    const int par = e / M, j = e % M;
+    ddc z{dd_from(limb_value<LIMBS>(g[2 * j + par], limb)), dd_from(limb_value<LIMBS>(g[2 * (j + M) + par], limb))};
+    z = ddc_mul(z, zeta_t[j]);
+    const int r = (int)(__builtin_bitreverse32((uint32_t)j) >> (32 - LOGM));
+    buf[par][r] = z;
+  }
+  __syncthreads();
+  dd_fft<M>(buf[0], tw_t);
+  dd_fft<M>(buf[1], tw_t);
+  const double scale = 0.5 / (double)M;
+  cplx* base = dest + blk * 2 * M;
+  for (int e = threadIdx.x; e < M; e += blockDim.x) {
+    const int f = fft512_freq(e & 63, e >> 6);
+    const ddc so = ddc_mul(buf[1][f], sroot_t[f]);
+    const ddc ge = buf[0][f];
+    const ddc kp{dd_add(ge.re, so.re), dd_add(ge.im, so.im)};
+    const ddc km{dd_add(ge.re, dd_neg(so.re)), dd_add(ge.im, dd_neg(so.im))};
+    base[e] = {(kp.re.hi + kp.re.lo) * scale, (kp.im.hi + kp.im.lo) * scale};
+    base[M + e] = {(km.re.hi + km.re.lo) * scale, (km.im.hi + km.im.lo) * scale};
+  }
+}
+#else
+template <int LIMBS>
+__global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__ dest, const uint64_t* __restrict__ src,
+                                                             const ddc* __restrict__ zeta_t,
+                                                             const ddc* __restrict__ tw_t, const ddc* __restrict__) {
   constexpr int M = 512, LOGM = 9;
   __shared__ ddc buf[M];
   const uint64_t blk = blockIdx.x;
@@ -166,6 +211,7 @@ __global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__
   __syncthreads();
   dd_fft_scatter<M>(buf, tw_t, [&](int e) { return dest + blk * M + e; });
 }
+#endif
 
 template <int N, int K, int L, int LIMBS>
 static int launch_convert(const ConvertArgs& a, const ddc* zeta, const ddc* tw) {
@@ -205,6 +251,17 @@ static void make_tables(uint32_t N, std::vector<ddc>& zeta, std::vector<ddc>& tw
     tw[t] = {{c.hi, c.lo}, {s.hi, s.lo}};
   }
 }
+// square roots s_f = exp(i pi (1 - 4 f) / 2048) of the N = 1024 evaluation points, f < 512 (P2_PM)
+static void make_sroots(std::vector<ddc>& sr) {
+  const long double PI = 3.14159265358979323846264338327950288L;
+  sr.resize(512);
+  for (uint32_t f = 0; f < 512; ++f) {
+    const long double ang = PI * (1.0L - 4.0L * (long double)f) / 2048.0L;
+    const long double c = cosl(ang), s = sinl(ang);
+    const double ch = (double)c, sh = (double)s;
+    sr[f] = {{ch, (double)(c - (long double)ch)}, {sh, (double)(s - (long double)sh)}};
+  }
+}
 
 int convert_bsk_launch(const ConvertArgs& a) {
   if (key_format(a.k, a.N, a.level).kind == KeyKind::GENERIC) return convert_bsk_generic_launch(a);
@@ -223,10 +280,15 @@ int convert_bsk_launch(const ConvertArgs& a) {
   CHIP_CHECK(hipMemcpyAsync(dz, zeta.data(), zeta.size() * sizeof(ddc), hipMemcpyHostToDevice, a.stream));
   CHIP_CHECK(hipMemcpyAsync(dt, tw.data(), tw.size() * sizeof(ddc), hipMemcpyHostToDevice, a.stream));
   int rc = 0;
+  std::vector<ddc> sr;
+  ddc* ds = nullptr;
   if (n2048) {
-    const uint64_t blocks = (uint64_t)a.n * PBS2_LIMBS * 4 * 2;
+    make_sroots(sr);
+    CHIP_CHECK(hipMallocAsync((void**)&ds, sr.size() * sizeof(ddc), a.stream));
+    CHIP_CHECK(hipMemcpyAsync(ds, sr.data(), sr.size() * sizeof(ddc), hipMemcpyHostToDevice, a.stream));
+    const uint64_t blocks = (uint64_t)a.n * PBS2_LIMBS * 4 * (P2_PM ? 1 : 2);
     hipLaunchKernelGGL((convert_bsk2048_kernel<PBS2_LIMBS>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
-                       reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt);
+                       reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, ds);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       set_error("convert launch failed: %s", hipGetErrorString(e));
@@ -241,6 +303,7 @@ int convert_bsk_launch(const ConvertArgs& a) {
   CHIP_CHECK(hipStreamSynchronize(a.stream));
   CHIP_CHECK(hipFreeAsync(dz, a.stream));
   CHIP_CHECK(hipFreeAsync(dt, a.stream));
+  if (ds) CHIP_CHECK(hipFreeAsync(ds, a.stream));
   return rc;
 }
 

@@ -29,6 +29,14 @@ constexpr int PBS2_LIMBS = 4;     // 16-bit key limbs
 constexpr int PBS2_SUBS = 2;      // sub-digits per decomposition digit: balanced 16-bit d_lo, d_hi
 constexpr int PBS2_SUB_BITS = 16; // on the key-limb grid (pbs2048.hip)
 constexpr int PBS2_MAX_LOGB = 24; // |d_hi| <= 2^(logB-17) + 1 keeps the certified bound < 1/2
+// P2_PM = 1: the key holds the spectra at the two square roots +-s_k of each evaluation point
+// alpha_k, K+- = (G_e +- s G_o) / 2 (the N = 2048 polynomial evaluated at +-s_k, i.e. its
+// 1024-point negacyclic spectrum), so a product costs 2 complex multiplies per frequency instead
+// of the 4 of the even/odd form (a_e b_e + Z a_o b_o, a_e b_o + a_o b_e); 0: the even/odd key
+// (pbs2048.hip, bsk.hip; A/B builds only, the key format follows it).
+#ifndef P2_PM
+#define P2_PM 1
+#endif
 constexpr size_t pbs2048_lds_bytes() {
   return PBS1024_TABLE_BYTES + 4 * PBS2_CTS * PBS1024_XCH_SLOTS * 16 + (size_t)PBS2_RING_SLOTS * 1024 * 16 +
          4 * PBS2_CTS * 4;  // + per-wave sync counters

@@ -24,6 +24,15 @@
 // goes to its three partners through LDS), does the key MAC for all four outputs on its quarter
 // of the frequencies, trades quarters back and runs the inverse transforms of its own output.
 // PBS2_CTS ciphertexts per workgroup share a ring of 16 KB key groups filled by LDS-DMA.
+//
+// Products at the square roots (P2_PM, pbs.hpp).  With s_k^2 = alpha_k, the N = 2048 polynomial
+// evaluated at +-s_k is A+-_k = A_e(alpha_k) +- s_k A_o(alpha_k) (its 1024-point negacyclic
+// spectrum: the even/odd 512-point transforms plus one radix-2 stage), so
+//     C+- = A+- B+-,   C_e = (C+ + C-) / 2,   C_o = (C+ - C-) / (2 s_k)
+// — two complex multiplies per frequency and key value instead of the four of the even/odd form.
+// The key holds K+- = B+- / 2 (bsk.hip); each wave forms A+- of its frequency quarter after the
+// spectrum exchange, accumulates U+- = sum A+- K+- in the key windows, and a completed slot is
+// unfolded to C_e = U+ + U-, C_o = (U+ - U-) conj(s_k) before it is mailed to its owners.
 #include "common.hpp"
 #include "fft512.hpp"
 #include "kernel_util.hpp"
@@ -169,6 +178,30 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     }
   }
 
+#if P2_PM
+  // square roots s_k = exp(i pi (1 - 4k) / 2048) of the evaluation points of my two frequency slots
+  cplx sroot[2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int k = fft512_freq(lane, 2 * v + jj);
+    const int num = (1 - 4 * k) & 4095;  // in units of pi / 2048
+    double sn, cs;
+    sincospi((double)num / 2048.0, &sn, &cs);
+    sroot[jj] = {cs, sn};
+  }
+  // X[2 row][sub] / X[2 row + 1][sub] (parity e / o spectra of one row) -> A+ / A- in place
+  auto to_pm = [&](cplx (&X)[4][PBS2_SUBS][2], int sub) __attribute__((always_inline)) {
+#pragma unroll
+    for (int row = 0; row < 2; ++row)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const cplx so = cmul(X[2 * row + 1][sub][jj], sroot[jj]);
+        const cplx xe = X[2 * row][sub][jj];
+        X[2 * row][sub][jj] = cadd(xe, so);
+        X[2 * row + 1][sub][jj] = csub(xe, so);
+      }
+  };
+#else
   // evaluation points of my two frequency slots (multiplication by Z = X^2)
   cplx alpha[2];
 #pragma unroll
@@ -179,6 +212,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     sincospi((double)num / 1024.0, &sn, &cs);
     alpha[jj] = {cs, sn};
   }
+#endif
 
   const int nrep = 64 - (int)base_log;
   const int logB = (int)base_log;
@@ -269,6 +303,9 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         for (int vv = 0; vv < 4; ++vv)
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) X[vv][sub][jj] = ctx[vv * XS + (2 * v + jj) * 64 + lane];
+#if P2_PM
+        to_pm(X, sub);
+#endif
 #pragma unroll
         for (int vv = 0; vv < 4; ++vv)
 #pragma unroll
@@ -301,6 +338,17 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
       for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) Yb[cc][0][jj] = Yb[cc][1][jj] = Pb[cc][jj] = {0.0, 0.0};
+#if P2_PM
+      // U+ += A+ K+, U- += A- K- of one row (Y[0] / Y[1] hold U+ / U-; P unused)
+      auto mac = [&](cplx (&Y)[2][2], cplx (&P)[2], const cplx& xp, const cplx& xm, const cplx& kp, const cplx& km,
+                     int jj) __attribute__((always_inline)) {
+        (void)P;
+        Y[0][jj].re = __builtin_fma(xp.re, kp.re, __builtin_fma(-xp.im, kp.im, Y[0][jj].re));
+        Y[0][jj].im = __builtin_fma(xp.re, kp.im, __builtin_fma(xp.im, kp.re, Y[0][jj].im));
+        Y[1][jj].re = __builtin_fma(xm.re, km.re, __builtin_fma(-xm.im, km.im, Y[1][jj].re));
+        Y[1][jj].im = __builtin_fma(xm.re, km.im, __builtin_fma(xm.im, km.re, Y[1][jj].im));
+      };
+#else
       // (a_e b_e + Z a_o b_o) and (a_e b_o + a_o b_e) of one row into (Y, P)
       auto mac = [&](cplx (&Y)[2][2], cplx (&P)[2], const cplx& xe, const cplx& xo, const cplx& ge, const cplx& go,
                      int jj) __attribute__((always_inline)) {
@@ -313,6 +361,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         Y[1][jj].re = __builtin_fma(xo.re, ge.re, __builtin_fma(-xo.im, ge.im, Y[1][jj].re));
         Y[1][jj].im = __builtin_fma(xo.re, ge.im, __builtin_fma(xo.im, ge.re, Y[1][jj].im));
       };
+#endif
 #pragma unroll
       for (int cc = 0; cc < K1; ++cc) {
 #pragma unroll
@@ -334,6 +383,9 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
                 for (int jj = 0; jj < 2; ++jj)
                   X[vv][PBS2_SUBS - 1][jj] = ctx[vv * XS + (2 * v + jj) * 64 + lane];
+#if P2_PM
+              to_pm(X, PBS2_SUBS - 1);
+#endif
             }
           }
           {
@@ -365,9 +417,17 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         // before the second), and nobody writes it again before the next limb's windows.
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
+#if P2_PM
+          // C_e = U+ + U-, C_o = (U+ - U-) conj(s)
+          const cplx ce = cadd(Ya[cc][0][jj], Ya[cc][1][jj]);
+          const cplx co = cmulc(csub(Ya[cc][0][jj], Ya[cc][1][jj]), sroot[jj]);
+          ctxw[(2 * cc) * XS + (v * 2 + jj) * 64 + lane] = ce;
+          ctxw[(2 * cc + 1) * XS + (v * 2 + jj) * 64 + lane] = co;
+#else
           Ya[cc][0][jj] = cadd(Ya[cc][0][jj], cmul(Pa[cc][jj], alpha[jj]));
           ctxw[(2 * cc) * XS + (v * 2 + jj) * 64 + lane] = Ya[cc][0][jj];
           ctxw[(2 * cc + 1) * XS + (v * 2 + jj) * 64 + lane] = Ya[cc][1][jj];
+#endif
         }
       }
       // slot li + 1 so far (d_hi * g_li): fold its odd products now, so that only the Y values are
@@ -377,7 +437,11 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) {
+#if P2_PM
+            Ya[cc][0][jj] = Yb[cc][0][jj];
+#else
             Ya[cc][0][jj] = cadd(Yb[cc][0][jj], cmul(Pb[cc][jj], alpha[jj]));
+#endif
             Ya[cc][1][jj] = Yb[cc][1][jj];
             Pa[cc][jj] = {0.0, 0.0};
             pin(Ya[cc][0][jj]), pin(Ya[cc][1][jj]);

@@ -864,6 +864,9 @@ __global__ void __launch_bounds__(Big<M>::NT) gen_big_step_kernel(StepArgs a) {
     cplx* Xc = a.X + (uint64_t)poly * a.level * a.subs * M;
     const int logB = (int)a.base_log, sb = (int)a.bits;
     const St half = (St)1 << (sb - 1), bmask = ((St)1 << sb) - (St)1;
+#ifdef DG_NOFRONT  // timing diagnostic only (wrong results): no forward transforms / X stores
+    if (S[0][0] != (St)0x12345) return;
+#endif
 #pragma unroll 1
     for (uint32_t q = 0; q < a.level; ++q) {
       Dg D[SPW][16];

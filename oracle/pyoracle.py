@@ -105,30 +105,30 @@ def limbs_for(N: int) -> int:
 
 def gpu2048_error_bound(fbsk_gpu: np.ndarray, logB: int = 23) -> float:
     """Certified bound on |x - round(x)| for the GPU's N = 2048 scheme (concrete_amd/csrc/
-    pbs2048.hip): even/odd halves as N = 1024 negacyclic products; the digit split
-    on the 16-bit key-limb grid, d = d_lo + 2^16 d_hi (|d_lo| <= 2^15, |d_hi| <= 2^(logB-17) + 1),
-    so output slot m sums d_lo g_m + d_hi g_{m-1} over both rows: per output parity half 4
-    products with d_lo and 4 with d_hi; plus the rounding of the pointwise multiplication by
-    alpha_k (folded twice into a slot: once for its d_hi part, once for d_lo) and of those two
-    additions.  fbsk_gpu: the device key (f64 view, scaled by 1/512)."""
-    M = 512
+    pbs2048.hip).  The products are taken at the square roots +-s_k of the
+    N = 1024 evaluation points (P2_PM): each digit polynomial's 1024-point negacyclic spectrum is
+    its two parity halves' 512-point transforms plus one radix-2 stage with twiddle s_k, and the
+    output is unfolded by the inverse stage (C_e = U+ + U-, C_o = (U+ - U-) conj s_k) before the
+    512-point inverse transforms: Higham's bound for a 1024-point transform (log M = 10) with
+    twiddle error mu = 2u (s_k from sincospi, <= 1 ulp per component; the tables are correctly
+    rounded).  The digit split on the 16-bit key-limb grid, d = d_lo + 2^16 d_hi (|d_lo| <= 2^15,
+    |d_hi| <= 2^(logB-17) + 1), makes output slot m the sum of d_lo g_m + d_hi g_{m-1} over both
+    rows: 4 full N = 2048 products.  fbsk_gpu: the device key (f64 view; K+- = G(+-s) / 1024)."""
     u = 2.0 ** -53
-    logM = 9.0
-    eta = u + 4.0 * u / (1.0 - 4.0 * u) * (np.sqrt(2.0) + u)
+    logM = 10.0
+    mu = 2.0 * u
+    eta = mu + 4.0 * u / (1.0 - 4.0 * u) * (np.sqrt(2.0) + mu)
     gamma = logM * eta / (1.0 - logM * eta)
     f = np.asarray(fbsk_gpu, dtype=np.float64).reshape(-1, 2)
-    maxG = float(np.max(np.hypot(f[:, 0], f[:, 1]))) * M
+    maxG = float(np.max(np.hypot(f[:, 0], f[:, 1]))) * 1024.0
     dlo = 2.0 ** 15
     dhi = 2.0 ** max(logB - 17, 0) + 1.0
-    dsum = 4.0 * (dlo + dhi)                    # sum over the 8 products of max |digit|
-    # Higham's transform bound per product (forward, pointwise product, inverse), plus two more
-    # roundings (the alpha folds' additions) on the accumulated spectrum: (4 gamma + 5 u)
-    main = np.sqrt(1024.0) * dsum * maxG * (4.0 * gamma + 5.0 * u) * 1.0001
-    # alpha * P: |P_k| <= (2 (dlo + dhi) 512 sqrt2) * maxG / 512 over the two folds, complex
-    # multiply error <= 2 sqrt2 u |P_k|, summed over the 512 frequencies of the unnormalised inverse
-    alpha_term = M * 2.0 * np.sqrt(2.0) * u * 2.0 * np.sqrt(2.0) * (dlo + dhi) * maxG
-    max_out = 1024.0 * dsum * 2.0 ** 15
-    return float(main + alpha_term + 4.0 * u * max_out)
+    dsum = 2.0 * (dlo + dhi)                    # sum over the 4 products of max |digit|
+    # forward transform, key rounding, pointwise product and inverse of each product, plus the
+    # accumulation and unfold additions: (4 gamma + 5 u), as for the N = 1024 products
+    main = np.sqrt(2048.0) * dsum * maxG * (4.0 * gamma + 5.0 * u) * 1.0001
+    max_out = 2048.0 * dsum * 2.0 ** 15
+    return float(main + 4.0 * u * max_out)
 
 
 def generic_error_bound(k: int, N: int, l: int, logB: int, bits: int, fbsk_gpu=None) -> float:

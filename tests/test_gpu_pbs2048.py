@@ -103,9 +103,11 @@ def signed_limb(x, limb, limbs=4):
 
 
 def test_fourier_key_2048_layout(B, small4, torch_cuda):
-    """Device key [n][limb][col][row][parity][slot][lane] == numpy complex128 transform of the
-    parity halves of g's 16-bit limbs (folded, twisted by zeta^t, zeta = e^{i pi/1024}), frequency
-    order fft512_freq, scaled 1/512.  (numpy's FFT is not correctly rounded: tolerance 1e-13.)"""
+    """Device key [n][limb][col][row][+-][slot][lane] == the N = 2048 key polynomial's 16-bit limb
+    evaluated at +-s_k, s_k = exp(i pi (1 - 4k) / 2048), k = fft512_freq(lane, slot), divided by
+    1024: (G_e(alpha_k) +- s_k G_o(alpha_k)) / 1024 with G_e / G_o the numpy transforms of the parity
+    halves (folded, twisted by zeta^t, zeta = e^{i pi/1024}).  (numpy's FFT is not correctly
+    rounded: tolerance 1e-13.)"""
     p = small4.p
     got = B.to_host(small4.fbsk).view(np.float64).reshape(p.n, 4, 2, 2, 2, 8, 64, 2)
     bsk = small4.bsk.reshape(p.n, 1, 2, 2, 2048)
@@ -114,16 +116,20 @@ def test_fourier_key_2048_layout(B, small4, torch_cuda):
     K = (lane[None, :] >> 3) + 8 * (lane[None, :] & 7) + 64 * slot[:, None]
     t = np.arange(512)
     tw = np.exp(1j * np.pi * t / 1024.0)
+    sroot = np.exp(1j * np.pi * (1.0 - 4.0 * K) / 2048.0)
     worst = 0.0
     for i in (0, p.n - 1):
         for li in range(4):
             for col in range(2):
                 for row in range(2):
+                    spec = []
                     for par in range(2):
                         lv = signed_limb(bsk[i, 0, row, col, par::2], li)
                         z = (lv[:512] + 1j * lv[512:]) * tw
-                        ref = np.fft.fft(z)[K] / 512.0
-                        gg = got[i, li, col, row, par]
+                        spec.append(np.fft.fft(z)[K])
+                    for pm, sign in ((0, 1.0), (1, -1.0)):
+                        ref = (spec[0] + sign * sroot * spec[1]) / 1024.0
+                        gg = got[i, li, col, row, pm]
                         err = np.max(np.abs(gg[..., 0] + 1j * gg[..., 1] - ref))
                         worst = max(worst, err / np.max(np.abs(ref)))
     assert worst < 1e-13, worst

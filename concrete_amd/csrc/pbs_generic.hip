@@ -741,6 +741,25 @@ __global__ void __launch_bounds__(Big<M>::NT) gen_big_step_kernel(StepArgs a) {
   };
   uint64_t A[SPW][16];
   double max_resid = 0.0;
+  // BACK: slot m + 1's columns are loaded while slot m's columns and rows are transformed, the
+  // first slot's ahead of the accumulator: every HBM read of Y overlaps work
+  const cplx* Yc = a.Y + (uint64_t)poly * a.limbs * M;
+  cplx pf[CPT][R];
+  auto load_cols = [&](uint32_t m) {
+    const cplx* Ym = Yc + (uint64_t)m * M;
+#pragma unroll
+    for (int p = 0; p < CPT; ++p)
+#pragma unroll
+      for (int k1 = 0; k1 < R; ++k1) {
+#ifdef DG_NOY  // timing diagnostic only (wrong results)
+        pf[p][k1] = cplx{(double)(k1 + m), (double)pos_of(p)};
+#else
+        pf[p][k1] = Ym[k1 * 512 + pos_of(p)];
+#endif
+      }
+    __builtin_amdgcn_sched_barrier(0);  // issued here, not sunk to their first use
+  };
+  if constexpr ((MODE & MODE_BACK) != 0) load_cols(0);
 
   if constexpr ((MODE & MODE_INIT) != 0) {
     // acc_c = LUT_c * X^{-ms(b)} (blind_rotate_assign: polynomial_wrapping_monic_monomial_div)
@@ -764,40 +783,22 @@ __global__ void __launch_bounds__(Big<M>::NT) gen_big_step_kernel(StepArgs a) {
 
   if constexpr ((MODE & MODE_BACK) != 0) {
     // acc += sum_m 2^{m b} round(iFFT(Y_m) conj(zeta^j)); the key spectra carry the 1/M
-    const cplx* Yc = a.Y + (uint64_t)poly * a.limbs * M;
-    // slot m + 1's columns are loaded while slot m's rows are transformed (the registers of the
-    // column DFT are free then): the HBM read of the next slot overlaps the row transforms
-    cplx pf[CPT][R];
-    auto load_cols = [&](uint32_t m) {
-      const cplx* Ym = Yc + (uint64_t)m * M;
+#pragma unroll 1
+    for (uint32_t m = 0; m < a.limbs; ++m) {
+      cplx u[CPT][R];
 #pragma unroll
       for (int p = 0; p < CPT; ++p)
 #pragma unroll
-        for (int k1 = 0; k1 < R; ++k1) {
-#ifdef DG_NOY  // timing diagnostic only (wrong results)
-          pf[p][k1] = cplx{(double)(k1 + m), (double)pos_of(p)};
-#else
-          pf[p][k1] = Ym[k1 * 512 + pos_of(p)];
-#endif
-        }
-    };
-    load_cols(0);
-#pragma unroll 1
-    for (uint32_t m = 0; m < a.limbs; ++m) {
+        for (int k1 = 0; k1 < R; ++k1) u[p][k1] = pf[p][k1];
+      if (m + 1 < a.limbs) load_cols(m + 1);
 #pragma unroll
       for (int p = 0; p < CPT; ++p) {
-        cplx u[R];
-#pragma unroll
-        for (int k1 = 0; k1 < R; ++k1) u[k1] = pf[p][k1];
 #ifndef DG_NOCOL
-        dft_col<R, true>(u);
+        dft_col<R, true>(u[p]);
 #endif
 #pragma unroll
-        for (int j1 = 0; j1 < R; ++j1) E[j1 * RS + pos_of(p)] = u[j1];
+        for (int j1 = 0; j1 < R; ++j1) E[j1 * RS + pos_of(p)] = u[p][j1];
       }
-      // the next slot's loads stay behind the column DFT (hoisted above it, both arrays are live)
-      asm volatile("" ::: "memory");
-      if (m + 1 < a.limbs) load_cols(m + 1);
       pair_barrier();
       // slot shifts stay below 64: the top limb is 64 - (L - 1) b bits wide (key_format), so no
       // guard (a per-element `sh < 64` test had become one branch per coefficient, with the
@@ -863,7 +864,9 @@ __global__ void __launch_bounds__(Big<M>::NT) gen_big_step_kernel(StepArgs a) {
     pair_barrier();
     cplx* Xc = a.X + (uint64_t)poly * a.level * a.subs * M;
     const int logB = (int)a.base_log, sb = (int)a.bits;
-    const St half = (St)1 << (sb - 1), bmask = ((St)1 << sb) - (St)1;
+    // one sub-digit: half = 0 and an all-ones mask make s = D and leave D = 0 (no per-element branch)
+    const bool split = a.subs > 1;
+    const St half = split ? (St)1 << (sb - 1) : (St)0, bmask = split ? ((St)1 << sb) - (St)1 : ~(St)0;
 #ifdef DG_NOFRONT  // timing diagnostic only (wrong results): no forward transforms / X stores
     if (S[0][0] != (St)0x12345) return;
 #endif
@@ -885,13 +888,11 @@ __global__ void __launch_bounds__(Big<M>::NT) gen_big_step_kernel(StepArgs a) {
           cplx v[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            Dg s0 = D[sr][e], s1 = D[sr][e + 8];
-            if (a.subs > 1) {  // balanced b-bit sub-digit, exact: D - s is a multiple of 2^b
-              s0 = (Dg)(((St)D[sr][e] + half) & bmask) - (Dg)half;
-              s1 = (Dg)(((St)D[sr][e + 8] + half) & bmask) - (Dg)half;
-              D[sr][e] = (D[sr][e] - s0) >> sb;
-              D[sr][e + 8] = (D[sr][e + 8] - s1) >> sb;
-            }
+            // balanced b-bit sub-digit, exact: D - s is a multiple of 2^b
+            const Dg s0 = (Dg)(((St)D[sr][e] + half) & bmask) - (Dg)half;
+            const Dg s1 = (Dg)(((St)D[sr][e + 8] + half) & bmask) - (Dg)half;
+            D[sr][e] = (D[sr][e] - s0) >> sb;
+            D[sr][e + 8] = (D[sr][e + 8] - s1) >> sb;
             v[e] = {(double)s0, (double)s1};
           }
 #ifndef DG_NOROW
@@ -947,7 +948,9 @@ struct MacArgs {
   uint32_t count, k, level, limbs, subs, M;
   uint32_t i;  // GGSW index (LWE mask position)
 };
-constexpr int MAC_CTS = 16;  // ciphertexts per block (key values loaded once per tile)
+#ifndef MAC_CTS
+#define MAC_CTS 16  // ciphertexts per block (key values loaded once per tile)
+#endif
 
 __global__ void __launch_bounds__(256) gen_mac_kernel(MacArgs a) {
   const uint32_t f = blockIdx.x * 256 + threadIdx.x;
@@ -1024,7 +1027,8 @@ __global__ void __launch_bounds__(256) gen_mac2_kernel(MacArgs a) {
 
 // k = 1 (two output polynomials): one thread per frequency computing both outputs, so each
 // digit spectrum value is read once per tile instead of once per output polynomial (the
-// product is HBM-bound on the X/Y spectra at N >= 2048).
+// product is HBM-bound on the X/Y spectra at N >= 2048).  (Tried: the next ciphertext's spectra
+// double-buffered by LDS-DMA, twice the loads in flight per wave: opt8 823.0 vs 822.7 PBS/s.)
 template <int KL, int L, int T>
 __global__ void __launch_bounds__(256) gen_mac2k1_kernel(MacArgs a) {
   const uint32_t f = blockIdx.x * 256 + threadIdx.x;
@@ -1682,6 +1686,22 @@ uint64_t generic_scratch_bytes_per_sample(uint32_t k, uint32_t N, uint32_t level
   return K1 * level * T * M * 16 + K1 * f.limbs * M * 16 + K1 * N * 8;
 }
 
+// A second stream per device for the two-launch path's chunk pairs (created once, never destroyed:
+// it lives as long as the process, like the device tables).
+static hipStream_t side_stream(int idx) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, hipStream_t> streams;
+  int dev = 0;
+  CHIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(mu);
+  auto it = streams.find({dev, idx});
+  if (it != streams.end()) return it->second;
+  hipStream_t s = nullptr;
+  CHIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  streams[{dev, idx}] = s;
+  return s;
+}
+
 int pbs_generic_launch(const PbsArgs& a) {
   using namespace gen;
   if (a.num_samples == 0) return 0;
@@ -1706,41 +1726,97 @@ int pbs_generic_launch(const PbsArgs& a) {
       return 0;
     }
   }
+  // Two-launch path: chunks of <= 2 GB of X / Y / accumulator scratch.  With two or more chunks,
+  // groups of NS chunks run on NS streams (the caller's and library streams of the device), their
+  // launches interleaved: the step kernel (one LDS-filling workgroup per CU, its HBM traffic in
+  // phase-locked bursts) and the product kernel (HBM streaming) of different chunks then share
+  // the chip instead of alternating on it.  CONCRETE_HIP_GEN_STREAMS=n (1..4, default 2) sets NS.
   const uint64_t per_ct = generic_scratch_bytes_per_sample(a.k, a.N, a.level, a.base_log);
-  const uint64_t budget = 2ull << 30;
-  const uint32_t chunk = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(a.num_samples, 65536),
-                                                      std::max<uint64_t>(1, budget / per_ct));
+  const char* be = getenv("CONCRETE_HIP_GEN_BUDGET_MB");  // scratch per chunk (A/B runs)
+  const uint64_t budget = be && atoi(be) > 0 ? (uint64_t)atoi(be) << 20 : 2ull << 30;
+  // CONCRETE_HIP_GEN_CHUNK caps the ciphertexts per chunk (tests: several chunks at small batches);
+  // both knobs are read per call
+  const char* ce = getenv("CONCRETE_HIP_GEN_CHUNK");
+  const uint64_t cap = ce && atoi(ce) > 0 ? (uint64_t)atoi(ce) : 65536;
+  const uint32_t chunk_max = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(a.num_samples, cap),
+                                                          std::max<uint64_t>(1, budget / per_ct));
+  uint32_t nchunks = (a.num_samples + chunk_max - 1) / chunk_max;
+  constexpr int MAX_NS = 4;
+  const char* se = getenv("CONCRETE_HIP_GEN_STREAMS");
+  const int want = se && atoi(se) >= 1 ? std::min(atoi(se), MAX_NS) : 2;
+  const int NS = (int)std::min<uint32_t>((uint32_t)want, nchunks);
+  nchunks = (nchunks + NS - 1) / NS * NS;  // balanced groups of NS chunks
+  const uint32_t chunk = (a.num_samples + nchunks - 1) / nchunks;
+  hipStream_t st[MAX_NS];
+  for (int q = 0; q < MAX_NS; ++q) st[q] = q == 0 || q >= NS ? a.stream : side_stream(q);
+  hipEvent_t ev_in = nullptr, ev_out[MAX_NS] = {};
   void* scratch = nullptr;
   keep_pool_memory();
-  CHIP_CHECK(hipMallocAsync(&scratch, per_ct * chunk, a.stream));
-  cplx* X = reinterpret_cast<cplx*>(scratch);
-  cplx* Y = X + (uint64_t)chunk * K1 * a.level * T * M;
-  uint64_t* acc = reinterpret_cast<uint64_t*>(Y + (uint64_t)chunk * K1 * L * M);
+  CHIP_CHECK(hipMallocAsync(&scratch, per_ct * chunk * NS, a.stream));
+  if (NS > 1) {  // the library streams start after the caller's prior work and the allocation
+    CHIP_CHECK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+    CHIP_CHECK(hipEventRecord(ev_in, a.stream));
+    for (int q = 1; q < NS; ++q) CHIP_CHECK(hipStreamWaitEvent(st[q], ev_in, 0));
+  }
+  struct Lane {
+    StepArgs s;
+    MacArgs m;
+    uint64_t* acc;
+    uint32_t cnt;
+  };
   int rc = 0;
-  for (uint32_t base = 0; base < a.num_samples && rc == 0; base += chunk) {
-    const uint32_t cnt = std::min(chunk, a.num_samples - base);
-    StepArgs s{acc,  X,    Y,   tb.Wfull, tb.Wlo, tb.Whi,  tb.Z,       a.in, a.in_idx, a.luts, a.lut_idx,
-               a.resid, base, cnt, a.n,    a.k,     a.level, a.base_log, b,    L,        T,      0, tb.Tau};
-    rc = step_dispatch<MODE_INIT | MODE_FRONT>(a.N, s, K1, a.stream);
-    MacArgs m{X, Y, reinterpret_cast<const cplx*>(a.fbsk), cnt, a.k, a.level, L, T, M, 0};
-    const dim3 mg((M + 255) / 256, K1 * L, (cnt + MAC_CTS - 1) / MAC_CTS);
-    for (uint32_t i = 0; i < a.n && rc == 0; ++i) {
-      m.i = i;
-      if (!launch_mac2(m, cnt, a.stream)) hipLaunchKernelGGL(gen_mac_kernel, mg, dim3(256), 0, a.stream, m);
-      s.step = i + 1;
-      rc = i + 1 < a.n ? step_dispatch<MODE_BACK | MODE_FRONT>(a.N, s, K1, a.stream)
-                       : step_dispatch<MODE_BACK>(a.N, s, K1, a.stream);
+  for (uint32_t base0 = 0; base0 < a.num_samples && rc == 0; base0 += NS * chunk) {
+    Lane ln[MAX_NS];
+    int nl = 0;
+    for (int q = 0; q < NS; ++q) {
+      const uint32_t base = base0 + q * chunk;
+      if (base >= a.num_samples) break;
+      const uint32_t cnt = std::min(chunk, a.num_samples - base);
+      cplx* X = reinterpret_cast<cplx*>(static_cast<char*>(scratch) + (uint64_t)q * per_ct * chunk);
+      cplx* Y = X + (uint64_t)chunk * K1 * a.level * T * M;
+      uint64_t* acc = reinterpret_cast<uint64_t*>(Y + (uint64_t)chunk * K1 * L * M);
+      ln[q].s = StepArgs{acc,     X,    Y,   tb.Wfull, tb.Wlo,  tb.Whi,     tb.Z, a.in, a.in_idx, a.luts, a.lut_idx,
+                         a.resid, base, cnt, a.n,      a.k,     a.level,    a.base_log, b, L,      T,      0, tb.Tau};
+      ln[q].m = MacArgs{X, Y, reinterpret_cast<const cplx*>(a.fbsk), cnt, a.k, a.level, L, T, M, 0};
+      ln[q].acc = acc;
+      ln[q].cnt = cnt;
+      ++nl;
     }
-    const uint64_t total = ((uint64_t)a.k * a.N + 1) * cnt;
-    const uint32_t eb = (uint32_t)std::min<uint64_t>((total + 255) / 256, 65535);
-    const uint32_t rlog = four_step(a.N) ? (uint32_t)__builtin_ctz(M / 512) : 0u;
-    hipLaunchKernelGGL(gen_extract_kernel, dim3(eb), dim3(256), 0, a.stream, a.out, a.out_idx, acc, base, cnt, a.k,
-                       a.N, rlog);
+    for (int q = 0; q < nl && rc == 0; ++q) rc = step_dispatch<MODE_INIT | MODE_FRONT>(a.N, ln[q].s, K1, st[q]);
+    for (uint32_t i = 0; i < a.n && rc == 0; ++i) {
+      for (int q = 0; q < nl && rc == 0; ++q) {
+        Lane& l = ln[q];
+        l.m.i = i;
+        if (!launch_mac2(l.m, l.cnt, st[q])) {
+          const dim3 mg((M + 255) / 256, K1 * L, (l.cnt + MAC_CTS - 1) / MAC_CTS);
+          hipLaunchKernelGGL(gen_mac_kernel, mg, dim3(256), 0, st[q], l.m);
+        }
+        l.s.step = i + 1;
+        rc = i + 1 < a.n ? step_dispatch<MODE_BACK | MODE_FRONT>(a.N, l.s, K1, st[q])
+                         : step_dispatch<MODE_BACK>(a.N, l.s, K1, st[q]);
+      }
+    }
+    for (int q = 0; q < nl && rc == 0; ++q) {
+      const uint64_t total = ((uint64_t)a.k * a.N + 1) * ln[q].cnt;
+      const uint32_t eb = (uint32_t)std::min<uint64_t>((total + 255) / 256, 65535);
+      const uint32_t rlog = four_step(a.N) ? (uint32_t)__builtin_ctz(M / 512) : 0u;
+      hipLaunchKernelGGL(gen_extract_kernel, dim3(eb), dim3(256), 0, st[q], a.out, a.out_idx, ln[q].acc, ln[q].s.base,
+                         ln[q].cnt, a.k, a.N, rlog);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       set_error("generic pbs launch failed: %s", hipGetErrorString(e));
       rc = -1;
     }
+  }
+  if (NS > 1) {  // the caller's stream resumes after the library streams' chunks
+    for (int q = 1; q < NS; ++q) {
+      CHIP_CHECK(hipEventCreateWithFlags(&ev_out[q], hipEventDisableTiming));
+      CHIP_CHECK(hipEventRecord(ev_out[q], st[q]));
+      CHIP_CHECK(hipStreamWaitEvent(a.stream, ev_out[q], 0));
+      CHIP_CHECK(hipEventDestroy(ev_out[q]));
+    }
+    CHIP_CHECK(hipEventDestroy(ev_in));
   }
   CHIP_CHECK(hipFreeAsync(scratch, a.stream));
   return rc;

@@ -170,6 +170,36 @@ def test_generic_legacy_step_kernel(B, oracle, torch_cuda):
     assert r.returncode == 0 and "legacy ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
+@pytest.mark.parametrize("streams", [1, 2, 3])
+@pytest.mark.parametrize("ci", [5, 7], ids=[CASES[i][0] for i in (5, 7)])
+def test_generic_chunked_two_streams(B, oracle, torch_cuda, ci, streams, monkeypatch):
+    """The two-launch path over several chunks (CONCRETE_HIP_GEN_CHUNK=3 on 7 ciphertexts: 3
+    chunks of 3 + 3 + 1 on one or three streams, evened to 4 chunks of 2 + 2 + 2 + 1 for two
+    streams: groups of chunks on the caller's and library streams), with permuted input / output
+    rows and mapped LUTs: bit-exact vs the exact oracle."""
+    label, k, N, n, l, logB, width = CASES[ci]
+    p, lwe_sk, glwe_sk, bsk, fbsk = setup(B, torch_cuda, k, N, n, l, logB, 7700)
+    rng = np.random.RandomState(11)
+    tables = [rng.randint(0, 1 << width, size=1 << width).astype(np.uint64) for _ in range(2)]
+    luts = np.stack([B.trivial_glwe(p, B.expand_lut(t, p.N, width)) for t in tables])
+    msgs = rng.randint(0, 1 << width, size=7)
+    cts = B.lwe_encrypt(lwe_sk, [B.encode(m, width) for m in msgs], p.n, 2.0 ** -30, 7703)
+    in_idx = np.array([3, 6, 0, 5, 1, 4, 2], dtype=np.uint64)
+    out_idx = np.array([5, 2, 6, 0, 3, 1, 4], dtype=np.uint64)
+    lut_idx = np.array([1, 0, 1, 1, 0, 0, 1], dtype=np.uint64)
+    dev = "cuda:0"
+    d = {name: B.to_device(a, dev) for name, a in (("in_idx", in_idx), ("out_idx", out_idx), ("lut_idx", lut_idx))}
+    out = torch_cuda.zeros((7, p.lwe_out_size), dtype=torch_cuda.int64, device=dev)
+    monkeypatch.setenv("CONCRETE_HIP_GEN_CHUNK", "3")
+    monkeypatch.setenv("CONCRETE_HIP_GEN_STREAMS", str(streams))
+    B.pbs(p, fbsk, B.to_device(cts, dev), B.to_device(luts, dev), out=out, **d)
+    torch_cuda.cuda.synchronize()
+    op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
+    ref, _ = oracle.pbs_batch(op, cts, luts, bsk=bsk, mode=oracle.MODE_KARATSUBA, lut_idx=lut_idx, in_idx=in_idx,
+                              out_idx=out_idx)
+    assert np.array_equal(B.to_host(out), ref)
+
+
 def test_generic_outside_exact_range_refused(B):
     """Sets whose certified bound would exceed the gate are refused, not rounded wrongly."""
     assert not B.pbs_supported(B.PbsParams(n=8, k=1, N=32768, level=2, base_log=15))

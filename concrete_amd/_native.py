@@ -124,6 +124,18 @@ SIGNATURES = {
     "stream_emulator_make_memref_batch_stream": (vp, [C.c_char_p, i32]),
     "stream_emulator_put_memref_batch": (None, [vp, vp, vp, u64, u64, u64, u64, u64, u64]),
     "stream_emulator_get_memref_batch": (None, [vp, vp, vp, u64, u64, u64, u64, u64]),
+    # Part 5: key wire-format import (concrete-protocol.capnp)
+    "concrete_hip_server_keyset_deserialize": (i32, [vp, u64, u32, C.POINTER(vp)]),
+    "concrete_hip_server_keyset_load_file": (i32, [C.c_char_p, u32, C.POINTER(vp)]),
+    "concrete_hip_server_keyset_destroy": (None, [vp]),
+    "concrete_hip_server_keyset_bsk_count": (u32, [vp]),
+    "concrete_hip_server_keyset_ksk_count": (u32, [vp]),
+    "concrete_hip_server_keyset_bsk_info": (i32, [vp, u32, vp]),
+    "concrete_hip_server_keyset_ksk_info": (i32, [vp, u32, vp]),
+    "concrete_hip_server_keyset_read_bsk": (i32, [vp, u32, vp, u64]),
+    "concrete_hip_server_keyset_read_ksk": (i32, [vp, u32, vp, u64]),
+    "concrete_hip_keyset_add_server_keyset": (i32, [vp, vp]),
+    "concrete_hip_set_seeded_key_decompressors": (None, [vp, vp]),
 }
 
 _lib = None
@@ -153,7 +165,8 @@ def declared_symbols():
     """Function names declared in include/concrete_hip.h."""
     txt = open(HEADER_PATH).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b([a-z_][a-z0-9_]*)\s*\(", txt)) - {"defined"})
+    # a name followed by "(" that does not open a function-pointer declarator "(*"
+    return sorted(set(re.findall(r"\b([a-z_][a-z0-9_]*)\s*\((?!\s*\*)", txt)) - {"defined"})
 
 
 def check(rc, what):

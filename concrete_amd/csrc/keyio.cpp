@@ -1,0 +1,667 @@
+// keyio.cpp — key wire-format import (host code of libconcrete_hip).
+//
+// Reads the evaluation keys of a concrete keyset from its Cap'n Proto wire form, the messages
+// the reference writes with capnp::writeMessage (compiler include/concretelang/Common/
+// Protocol.h:158-175, unpacked stream framing) for the schema
+// tools/concrete-protocol/src/concrete-protocol.capnp:149-297 (ServerKeyset, Keyset,
+// LweBootstrapKey, LweKeyswitchKey and their Info / Params structs), and hands the standard-domain
+// keys to a runtime keyset (runtime.hip) in the order the runtime context indexes them
+// (context.cpp:36-94: position in the ServerKeyset's lists).
+//
+// No capnp library is in the image, so this is a self-contained reader of the published encoding:
+//   * stream framing: u32 (segment count - 1), u32 size (words) per segment, padding to 8 bytes,
+//     then the segments;
+//   * pointers: struct (kind 0: signed 30-bit word offset, data / pointer section sizes), list
+//     (kind 1: element size code, count; composite lists with a tag word), far (kind 2: landing
+//     pad in another segment, single or double), null = 0; out-of-range fields read as defaults;
+//   * field placement inside each struct follows capnp's layout rule (fields in ordinal order,
+//     each in the first free aligned hole of the data section), computed by hand for the structs
+//     read here (offsets below, one comment per struct).
+// Payloads are `List(Data)` blobs concatenated in order (Protocol.h:349-372), little-endian u64.
+// Seeded keys (Compression::SEED: 2 seed words + bodies, Keys.cpp:121-137,193-218) are expanded by
+// the caller-installed concrete-cpu decompressors (concrete_cpu_decompress_seeded_lwe_*_u64, the
+// functions Keys.cpp calls): their mask stream is concrete-csprng's, which is not restated here.
+//
+// Parity: unpinned — the reference holds no serialized keyset; tests/test_keyio.py round-trips the
+// writer in concrete_amd/keys.py (single-segment, single-far and double-far layouts) and checks
+// malformed messages are refused.
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/concrete_hip.h"
+
+namespace chip {
+void set_error(const char* fmt, ...);
+}
+using chip::set_error;
+
+struct concrete_hip_server_keyset {
+  struct Key {
+    concrete_hip_key_info info;
+    std::vector<uint64_t> payload;  // concatenated blobs (u64 words)
+  };
+  std::vector<Key> bsk, ksk;
+};
+
+namespace {
+
+constexpr uint64_t MAX_WORDS = 1ull << 37;  // 1 TiB: sanity bound on declared segment sizes
+
+class Reader {
+ public:
+  // words: the message body (segments back to back), seg_start / seg_size in words
+  Reader(const uint64_t* words, std::vector<uint64_t> start, std::vector<uint64_t> size)
+      : w_(words), start_(std::move(start)), size_(std::move(size)) {}
+
+  struct Struct {
+    bool present = false;
+    uint32_t seg = 0;
+    uint64_t data = 0;  // word index within the segment
+    uint32_t dw = 0, pw = 0;
+  };
+  struct List {
+    bool present = false;
+    uint32_t seg = 0;
+    uint64_t start = 0;   // first element (word index; byte lists: word index of the first byte)
+    uint32_t esize = 0;   // capnp element size code
+    uint64_t count = 0;   // elements
+    uint32_t dw = 0, pw = 0;  // composite element layout
+  };
+
+  bool ok() const { return err_.empty(); }
+  const std::string& err() const { return err_; }
+
+  uint64_t word(uint32_t seg, uint64_t i) const { return w_[start_[seg] + i]; }
+
+  Struct root() {
+    if (size_.empty() || size_[0] < 1) return fail_s("empty message");
+    return read_struct_ptr(0, 0);
+  }
+
+  // --- fields ---------------------------------------------------------------------------------
+  uint32_t u32(const Struct& s, uint32_t byte_off) const {
+    if ((byte_off + 4) > s.dw * 8ull) return 0;  // beyond the data section: default
+    uint64_t v = word(s.seg, s.data + byte_off / 8);
+    return (uint32_t)(v >> (8 * (byte_off % 8)));
+  }
+  uint16_t u16(const Struct& s, uint32_t byte_off) const {
+    if ((byte_off + 2) > s.dw * 8ull) return 0;
+    uint64_t v = word(s.seg, s.data + byte_off / 8);
+    return (uint16_t)(v >> (8 * (byte_off % 8)));
+  }
+  double f64(const Struct& s, uint32_t byte_off) const {
+    if ((byte_off + 8) > s.dw * 8ull) return 0.0;
+    uint64_t v = word(s.seg, s.data + byte_off / 8);
+    double d;
+    memcpy(&d, &v, 8);
+    return d;
+  }
+  Struct ptr_struct(const Struct& s, uint32_t idx) {
+    if (idx >= s.pw) return Struct{};
+    return read_struct_ptr(s.seg, s.data + s.dw + idx);
+  }
+  List ptr_list(const Struct& s, uint32_t idx) {
+    if (idx >= s.pw) return List{};
+    return read_list_ptr(s.seg, s.data + s.dw + idx);
+  }
+  Struct list_struct(const List& l, uint64_t i) {
+    Struct r;
+    if (!l.present || i >= l.count) return r;
+    if (l.esize != 7) {
+      fail("list of structs expected (element size %u)", l.esize);
+      return r;
+    }
+    r.present = true;
+    r.seg = l.seg;
+    r.data = l.start + i * (uint64_t)(l.dw + l.pw);
+    r.dw = l.dw;
+    r.pw = l.pw;
+    return r;
+  }
+  List list_ptr_list(const List& l, uint64_t i) {  // element i of a List(Data) / List(List(..))
+    if (!l.present || i >= l.count) return List{};
+    if (l.esize != 6) {
+      fail("list of pointers expected (element size %u)", l.esize);
+      return List{};
+    }
+    return read_list_ptr(l.seg, l.start + i);
+  }
+  const uint8_t* bytes(const List& l) const {
+    return reinterpret_cast<const uint8_t*>(w_ + start_[l.seg] + l.start);
+  }
+
+ private:
+  const uint64_t* w_;
+  std::vector<uint64_t> start_, size_;
+  std::string err_;
+
+  void fail(const char* fmt, ...) __attribute__((format(printf, 2, 3))) {
+    if (!err_.empty()) return;
+    char b[256];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(b, sizeof b, fmt, ap);
+    va_end(ap);
+    err_ = b;
+  }
+  Struct fail_s(const char* m) {
+    fail("%s", m);
+    return Struct{};
+  }
+
+  static int64_t off30(uint64_t w) { return (int64_t)((int32_t)(uint32_t)w >> 2); }
+
+  // Follows the pointer at (seg, at): the target's segment, first word and the tag describing it
+  // (the pointer itself, or the landing pad's tag for far pointers).  false: null or malformed.
+  bool deref(uint32_t seg, uint64_t at, uint32_t& tseg, uint64_t& tstart, uint64_t& tag) {
+    if (at >= size_[seg]) {
+      fail("pointer outside its segment");
+      return false;
+    }
+    const uint64_t p = word(seg, at);
+    if (p == 0) return false;
+    const uint32_t kind = p & 3;
+    if (kind == 3) {
+      fail("capability pointer in a key message");
+      return false;
+    }
+    if (kind != 2) {
+      tseg = seg;
+      tag = p;
+      const int64_t t = (int64_t)at + 1 + off30(p);
+      if (t < 0 || (uint64_t)t > size_[seg]) {
+        fail("pointer target outside its segment");
+        return false;
+      }
+      tstart = (uint64_t)t;
+      return true;
+    }
+    const bool dbl = (p >> 2) & 1;
+    const uint64_t pad = (p >> 3) & 0x1fffffffu;
+    const uint32_t sid = (uint32_t)(p >> 32);
+    if (sid >= size_.size() || pad + (dbl ? 2 : 1) > size_[sid]) {
+      fail("far pointer outside the message");
+      return false;
+    }
+    const uint64_t l0 = word(sid, pad);
+    if (!dbl) {
+      if ((l0 & 3) == 2 || (l0 & 3) == 3) {
+        fail("far pointer landing pad is not a struct or list pointer");
+        return false;
+      }
+      tseg = sid;
+      tag = l0;
+      const int64_t t = (int64_t)pad + 1 + off30(l0);
+      if (t < 0 || (uint64_t)t > size_[sid]) {
+        fail("landing pad target outside its segment");
+        return false;
+      }
+      tstart = (uint64_t)t;
+      return true;
+    }
+    // double far: pad[0] = single far pointer to the content's start, pad[1] = its tag
+    if ((l0 & 7) != 2) {
+      fail("double-far landing pad is not a single far pointer");
+      return false;
+    }
+    const uint32_t cseg = (uint32_t)(l0 >> 32);
+    const uint64_t cstart = (l0 >> 3) & 0x1fffffffu;
+    if (cseg >= size_.size() || cstart > size_[cseg]) {
+      fail("double-far content outside the message");
+      return false;
+    }
+    tseg = cseg;
+    tstart = cstart;
+    tag = word(sid, pad + 1);
+    return true;
+  }
+
+  Struct read_struct_ptr(uint32_t seg, uint64_t at) {
+    Struct s;
+    uint32_t tseg;
+    uint64_t tstart, tag;
+    if (!deref(seg, at, tseg, tstart, tag)) return s;
+    if ((tag & 3) != 0) return fail_s("struct pointer expected");
+    s.dw = (uint32_t)((tag >> 32) & 0xffff);
+    s.pw = (uint32_t)(tag >> 48);
+    if (tstart + s.dw + s.pw > size_[tseg]) return fail_s("struct outside its segment");
+    s.present = true;
+    s.seg = tseg;
+    s.data = tstart;
+    return s;
+  }
+
+  List read_list_ptr(uint32_t seg, uint64_t at) {
+    List l;
+    uint32_t tseg;
+    uint64_t tstart, tag;
+    if (!deref(seg, at, tseg, tstart, tag)) return l;
+    if ((tag & 3) != 1) {
+      fail("list pointer expected");
+      return l;
+    }
+    l.esize = (uint32_t)((tag >> 32) & 7);
+    const uint64_t n = tag >> 35;
+    l.seg = tseg;
+    if (l.esize == 7) {  // composite: n = words after the tag word
+      if (tstart + 1 + n > size_[tseg]) {
+        fail("composite list outside its segment");
+        return l;
+      }
+      const uint64_t t = word(tseg, tstart);
+      if ((t & 3) != 0) {
+        fail("composite list tag is not a struct tag");
+        return l;
+      }
+      l.count = (t >> 2) & 0x3fffffffu;
+      l.dw = (uint32_t)((t >> 32) & 0xffff);
+      l.pw = (uint32_t)(t >> 48);
+      if (l.count * (uint64_t)(l.dw + l.pw) > n) {
+        fail("composite list elements exceed its word count");
+        return l;
+      }
+      l.start = tstart + 1;
+    } else {
+      static const uint32_t bits[7] = {0, 1, 8, 16, 32, 64, 64};
+      const uint64_t words = (n * bits[l.esize] + 63) / 64;
+      if (tstart + words > size_[tseg]) {
+        fail("list outside its segment");
+        return l;
+      }
+      l.count = n;
+      l.start = tstart;
+    }
+    l.present = true;
+    return l;
+  }
+};
+
+// --- schema offsets (concrete-protocol.capnp; capnp layout rule, bytes in the data section) ------
+// LweBootstrapKey / LweKeyswitchKey: data 0 words; ptr 0 info, ptr 1 payload.
+// *KeyInfo: id u32 @0, inputId u32 @4, outputId u32 @8, compression u16 @12 (enum);
+//           ptr 0 params.
+// LweBootstrapKeyParams: levelCount @0, baseLog @4, glweDimension @8, polynomialSize @12,
+//           variance f64 @16, integerPrecision @24, keyType u16 @28, inputLweDimension @32;
+//           ptr 0 modulus.
+// LweKeyswitchKeyParams: levelCount @0, baseLog @4, variance f64 @8, integerPrecision @16,
+//           keyType u16 @20, inputLweDimension @24, outputLweDimension @28; ptr 0 modulus.
+// Modulus: union discriminant u16 @0 (0 native, 1 powerOfTwo, 2 integer); ptr 0 the member,
+//           PowerOfTwoModulus.power / IntegerModulus.modulus u32 @0.
+// Payload: ptr 0 data (List(Data)).
+// ServerKeyset: ptr 0 lweBootstrapKeys, ptr 1 lweKeyswitchKeys, ptr 2 packingKeyswitchKeys.
+// Keyset: ptr 0 server, ptr 1 client.
+
+bool read_modulus(Reader& r, const Reader::Struct& params, concrete_hip_key_info& k) {
+  Reader::Struct m = r.ptr_struct(params, 0);
+  k.modulus_kind = 0;
+  k.modulus_value = 0;
+  if (!m.present) return r.ok();  // default: native
+  k.modulus_kind = r.u16(m, 0);
+  if (k.modulus_kind == 1 || k.modulus_kind == 2) {
+    Reader::Struct v = r.ptr_struct(m, 0);
+    if (v.present) k.modulus_value = r.u32(v, 0);
+  }
+  return r.ok();
+}
+
+bool read_payload(Reader& r, const Reader::Struct& key, std::vector<uint64_t>& out, uint64_t& words) {
+  Reader::Struct payload = r.ptr_struct(key, 1);
+  out.clear();
+  words = 0;
+  if (!payload.present) return r.ok();
+  Reader::List blobs = r.ptr_list(payload, 0);
+  if (!blobs.present) return r.ok();
+  if (blobs.esize != 6) {
+    set_error("key payload: List(Data) expected");
+    return false;
+  }
+  uint64_t total = 0;
+  std::vector<Reader::List> parts(blobs.count);
+  for (uint64_t i = 0; i < blobs.count; ++i) {
+    parts[i] = r.list_ptr_list(blobs, i);
+    if (!r.ok()) return false;
+    if (parts[i].present && parts[i].esize != 2) {
+      set_error("key payload: blob %llu is not Data", (unsigned long long)i);
+      return false;
+    }
+    total += parts[i].present ? parts[i].count : 0;
+  }
+  if (total % 8) {
+    set_error("key payload: %llu bytes is not a whole number of u64 words", (unsigned long long)total);
+    return false;
+  }
+  out.resize(total / 8);
+  uint8_t* dst = reinterpret_cast<uint8_t*>(out.data());
+  for (const auto& p : parts)
+    if (p.present && p.count) {
+      memcpy(dst, r.bytes(p), p.count);
+      dst += p.count;
+    }
+  words = total / 8;
+  return true;
+}
+
+uint64_t bsk_words(const concrete_hip_key_info& k) {  // concrete_cpu_bootstrap_key_size_u64
+  const uint64_t g = (uint64_t)k.glwe_dim + 1;
+  return (uint64_t)k.input_lwe_dim * k.level_count * g * g * k.poly_size;
+}
+uint64_t seeded_bsk_words(const concrete_hip_key_info& k) {  // 2 seed words + seeded GGSW bodies
+  return 2 + (uint64_t)k.input_lwe_dim * k.level_count * ((uint64_t)k.glwe_dim + 1) * k.poly_size;
+}
+uint64_t ksk_words(const concrete_hip_key_info& k) {  // concrete_cpu_keyswitch_key_size_u64
+  return (uint64_t)k.input_lwe_dim * k.level_count * ((uint64_t)k.output_lwe_dim + 1);
+}
+uint64_t seeded_ksk_words(const concrete_hip_key_info& k) {
+  return 2 + (uint64_t)k.input_lwe_dim * k.level_count;
+}
+
+bool read_info(Reader& r, const Reader::Struct& key, bool is_bsk, concrete_hip_key_info& k) {
+  memset(&k, 0, sizeof k);
+  Reader::Struct info = r.ptr_struct(key, 0);
+  if (!info.present) {
+    set_error("key without info");
+    return false;
+  }
+  k.id = r.u32(info, 0);
+  k.input_id = r.u32(info, 4);
+  k.output_id = r.u32(info, 8);
+  k.compression = r.u16(info, 12);
+  Reader::Struct p = r.ptr_struct(info, 0);
+  if (!p.present) {
+    set_error("key info without params");
+    return false;
+  }
+  k.level_count = r.u32(p, 0);
+  k.base_log = r.u32(p, 4);
+  if (is_bsk) {
+    k.glwe_dim = r.u32(p, 8);
+    k.poly_size = r.u32(p, 12);
+    k.variance = r.f64(p, 16);
+    k.integer_precision = r.u32(p, 24);
+    k.key_type = r.u16(p, 28);
+    k.input_lwe_dim = r.u32(p, 32);
+    k.output_lwe_dim = k.glwe_dim * k.poly_size;
+  } else {
+    k.variance = r.f64(p, 8);
+    k.integer_precision = r.u32(p, 16);
+    k.key_type = r.u16(p, 20);
+    k.input_lwe_dim = r.u32(p, 24);
+    k.output_lwe_dim = r.u32(p, 28);
+  }
+  if (!read_modulus(r, p, k)) return false;
+  k.key_words = is_bsk ? bsk_words(k) : ksk_words(k);  // the standard-domain (decompressed) size
+  return r.ok();
+}
+
+bool read_keys(Reader& r, const Reader::List& list, bool is_bsk, std::vector<concrete_hip_server_keyset::Key>& out) {
+  if (!list.present) return r.ok();
+  for (uint64_t i = 0; i < list.count; ++i) {
+    Reader::Struct key = r.list_struct(list, i);
+    if (!r.ok()) return false;
+    concrete_hip_server_keyset::Key k;
+    if (!read_info(r, key, is_bsk, k.info)) return false;
+    if (!read_payload(r, key, k.payload, k.info.payload_words)) return false;
+    out.push_back(std::move(k));
+  }
+  return true;
+}
+
+int parse(const uint64_t* words, uint64_t n_words, uint32_t root, concrete_hip_server_keyset** out) {
+  if (n_words < 1) {
+    set_error("deserialize: empty input");
+    return -3;
+  }
+  const uint32_t* h = reinterpret_cast<const uint32_t*>(words);
+  const uint64_t nseg = (uint64_t)h[0] + 1;
+  const uint64_t header_words = (4 * (1 + nseg) + 7) / 8;
+  if (nseg > 512 || header_words > n_words) {
+    set_error("deserialize: bad segment table (%llu segments)", (unsigned long long)nseg);
+    return -3;
+  }
+  std::vector<uint64_t> start(nseg), size(nseg);
+  uint64_t at = header_words;
+  for (uint64_t s = 0; s < nseg; ++s) {
+    size[s] = h[1 + s];
+    start[s] = at;
+    at += size[s];
+    if (size[s] > MAX_WORDS || at > n_words) {
+      set_error("deserialize: segment %llu extends past the input (%llu of %llu words)", (unsigned long long)s,
+                (unsigned long long)at, (unsigned long long)n_words);
+      return -3;
+    }
+  }
+  Reader r(words, start, size);
+  Reader::Struct top = r.root();
+  if (!r.ok() || !top.present) {
+    set_error("deserialize: %s", r.ok() ? "null root" : r.err().c_str());
+    return -3;
+  }
+  auto* ks = new concrete_hip_server_keyset();
+  bool ok = true;
+  switch (root) {
+    case CONCRETE_HIP_ROOT_KEYSET:
+      top = r.ptr_struct(top, 0);  // Keyset.server
+      if (!top.present) break;
+      /* fallthrough */
+    case CONCRETE_HIP_ROOT_SERVER_KEYSET:
+      ok = read_keys(r, r.ptr_list(top, 0), true, ks->bsk) && read_keys(r, r.ptr_list(top, 1), false, ks->ksk);
+      break;
+    case CONCRETE_HIP_ROOT_LWE_BOOTSTRAP_KEY:
+    case CONCRETE_HIP_ROOT_LWE_KEYSWITCH_KEY: {
+      const bool is_bsk = root == CONCRETE_HIP_ROOT_LWE_BOOTSTRAP_KEY;
+      concrete_hip_server_keyset::Key k;
+      ok = read_info(r, top, is_bsk, k.info) && read_payload(r, top, k.payload, k.info.payload_words);
+      if (ok) (is_bsk ? ks->bsk : ks->ksk).push_back(std::move(k));
+      break;
+    }
+    default:
+      set_error("deserialize: unknown root type %u", root);
+      ok = false;
+  }
+  if (ok && !r.ok()) {
+    set_error("deserialize: %s", r.err().c_str());
+    ok = false;
+  }
+  if (!ok) {
+    delete ks;
+    return -3;
+  }
+  *out = ks;
+  return 0;
+}
+
+std::mutex g_dec_mu;
+concrete_hip_bsk_decompressor g_bsk_dec = nullptr;
+concrete_hip_ksk_decompressor g_ksk_dec = nullptr;
+
+// Checks a key's parameters and payload size and writes its standard-domain form to dst.
+int expand(const concrete_hip_server_keyset::Key& k, bool is_bsk, uint64_t* dst, uint64_t dst_words) {
+  const concrete_hip_key_info& i = k.info;
+  const char* what = is_bsk ? "bootstrap key" : "keyswitch key";
+  if (i.integer_precision != 64 || i.modulus_kind != 0) {
+    set_error("%s %u: only 64-bit keys over the native modulus are supported (precision %u, modulus kind %u)", what,
+              i.id, i.integer_precision, i.modulus_kind);
+    return -2;
+  }
+  if (dst_words < i.key_words) {
+    set_error("%s %u: destination holds %llu words, the key needs %llu", what, i.id, (unsigned long long)dst_words,
+              (unsigned long long)i.key_words);
+    return -3;
+  }
+  if (i.compression == 0) {
+    if (k.payload.size() != i.key_words) {
+      set_error("%s %u: payload has %llu words, its parameters need %llu", what, i.id,
+                (unsigned long long)k.payload.size(), (unsigned long long)i.key_words);
+      return -3;
+    }
+    memcpy(dst, k.payload.data(), i.key_words * 8);
+    return 0;
+  }
+  if (i.compression != 1) {
+    set_error("%s %u: unsupported compression %u", what, i.id, i.compression);
+    return -2;
+  }
+  const uint64_t need = is_bsk ? seeded_bsk_words(i) : seeded_ksk_words(i);
+  if (k.payload.size() != need) {
+    set_error("%s %u: seeded payload has %llu words, its parameters need %llu", what, i.id,
+              (unsigned long long)k.payload.size(), (unsigned long long)need);
+    return -3;
+  }
+  // Csprng.cpp:125-140 readSeed: word 0 = bytes 0-7, word 1 = bytes 8-15, little endian
+  concrete_hip_uint128 seed;
+  for (int b = 0; b < 16; ++b) seed.little_endian_bytes[b] = (uint8_t)(k.payload[b / 8] >> (8 * (b % 8)));
+  concrete_hip_bsk_decompressor bf;
+  concrete_hip_ksk_decompressor kf;
+  {
+    std::lock_guard<std::mutex> g(g_dec_mu);
+    bf = g_bsk_dec;
+    kf = g_ksk_dec;
+  }
+  if (is_bsk ? !bf : !kf) {
+    set_error("%s %u is seeded: install concrete-cpu's decompressor with concrete_hip_set_seeded_key_decompressors",
+              what, i.id);
+    return -2;
+  }
+  if (is_bsk)
+    bf(dst, k.payload.data() + 2, i.input_lwe_dim, i.poly_size, i.glwe_dim, i.level_count, i.base_log, seed, 1u);
+  else
+    kf(dst, k.payload.data() + 2, i.input_lwe_dim, i.output_lwe_dim, i.level_count, i.base_log, seed, 1u);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int concrete_hip_server_keyset_deserialize(const void* bytes, uint64_t size, uint32_t root,
+                                           concrete_hip_server_keyset** out) {
+  if (!out || (!bytes && size)) {
+    set_error("server_keyset_deserialize: bad argument");
+    return -3;
+  }
+  *out = nullptr;
+  if (size % 8) {
+    set_error("server_keyset_deserialize: %llu bytes is not a whole number of words", (unsigned long long)size);
+    return -3;
+  }
+  if ((uintptr_t)bytes % 8 == 0) return parse((const uint64_t*)bytes, size / 8, root, out);
+  std::vector<uint64_t> copy(size / 8);
+  memcpy(copy.data(), bytes, size);
+  return parse(copy.data(), copy.size(), root, out);
+}
+
+int concrete_hip_server_keyset_load_file(const char* path, uint32_t root, concrete_hip_server_keyset** out) {
+  if (!path || !out) {
+    set_error("server_keyset_load_file: bad argument");
+    return -3;
+  }
+  *out = nullptr;
+  FILE* f = fopen(path, "rb");
+  if (!f) {
+    set_error("server_keyset_load_file: cannot open %s", path);
+    return -3;
+  }
+  std::vector<uint64_t> buf;
+  uint64_t got = 0;
+  if (fseek(f, 0, SEEK_END) == 0) {
+    long len = ftell(f);
+    if (len > 0 && len % 8 == 0 && fseek(f, 0, SEEK_SET) == 0) {
+      buf.resize((uint64_t)len / 8);
+      got = fread(buf.data(), 1, (size_t)len, f);
+    }
+  }
+  fclose(f);
+  if (buf.empty() || got != buf.size() * 8) {
+    set_error("server_keyset_load_file: %s is empty, unreadable or not a whole number of words", path);
+    return -3;
+  }
+  return parse(buf.data(), buf.size(), root, out);
+}
+
+void concrete_hip_server_keyset_destroy(concrete_hip_server_keyset* sk) { delete sk; }
+
+uint32_t concrete_hip_server_keyset_bsk_count(const concrete_hip_server_keyset* sk) {
+  return sk ? (uint32_t)sk->bsk.size() : 0;
+}
+uint32_t concrete_hip_server_keyset_ksk_count(const concrete_hip_server_keyset* sk) {
+  return sk ? (uint32_t)sk->ksk.size() : 0;
+}
+
+int concrete_hip_server_keyset_bsk_info(const concrete_hip_server_keyset* sk, uint32_t index,
+                                        concrete_hip_key_info* out) {
+  if (!sk || !out || index >= sk->bsk.size()) {
+    set_error("server_keyset_bsk_info: bad argument or index %u", index);
+    return -3;
+  }
+  *out = sk->bsk[index].info;
+  return 0;
+}
+
+int concrete_hip_server_keyset_ksk_info(const concrete_hip_server_keyset* sk, uint32_t index,
+                                        concrete_hip_key_info* out) {
+  if (!sk || !out || index >= sk->ksk.size()) {
+    set_error("server_keyset_ksk_info: bad argument or index %u", index);
+    return -3;
+  }
+  *out = sk->ksk[index].info;
+  return 0;
+}
+
+int concrete_hip_server_keyset_read_bsk(const concrete_hip_server_keyset* sk, uint32_t index, uint64_t* dst,
+                                        uint64_t dst_words) {
+  if (!sk || !dst || index >= sk->bsk.size()) {
+    set_error("server_keyset_read_bsk: bad argument or index %u", index);
+    return -3;
+  }
+  return expand(sk->bsk[index], true, dst, dst_words);
+}
+
+int concrete_hip_server_keyset_read_ksk(const concrete_hip_server_keyset* sk, uint32_t index, uint64_t* dst,
+                                        uint64_t dst_words) {
+  if (!sk || !dst || index >= sk->ksk.size()) {
+    set_error("server_keyset_read_ksk: bad argument or index %u", index);
+    return -3;
+  }
+  return expand(sk->ksk[index], false, dst, dst_words);
+}
+
+void concrete_hip_set_seeded_key_decompressors(concrete_hip_bsk_decompressor bsk, concrete_hip_ksk_decompressor ksk) {
+  std::lock_guard<std::mutex> g(g_dec_mu);
+  g_bsk_dec = bsk;
+  g_ksk_dec = ksk;
+}
+
+int concrete_hip_keyset_add_server_keyset(concrete_hip_keyset* ks, const concrete_hip_server_keyset* sk) {
+  if (!ks || !sk) {
+    set_error("keyset_add_server_keyset: bad argument");
+    return -3;
+  }
+  std::vector<uint64_t> buf;
+  for (uint32_t i = 0; i < sk->bsk.size(); ++i) {
+    const concrete_hip_key_info& k = sk->bsk[i].info;
+    buf.assign(k.key_words, 0);
+    int rc = expand(sk->bsk[i], true, buf.data(), buf.size());
+    if (rc) return rc;
+    rc = concrete_hip_keyset_add_bsk(ks, i, buf.data(), k.input_lwe_dim, k.glwe_dim, k.level_count, k.base_log,
+                                     k.poly_size);
+    if (rc) return rc;
+  }
+  for (uint32_t i = 0; i < sk->ksk.size(); ++i) {
+    const concrete_hip_key_info& k = sk->ksk[i].info;
+    buf.assign(k.key_words, 0);
+    int rc = expand(sk->ksk[i], false, buf.data(), buf.size());
+    if (rc) return rc;
+    rc = concrete_hip_keyset_add_ksk(ks, i, buf.data(), k.level_count, k.base_log, k.input_lwe_dim,
+                                     k.output_lwe_dim);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+}  // extern "C"

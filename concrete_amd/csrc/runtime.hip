@@ -145,6 +145,7 @@ void slot_release(SliceSlot& sl) {
   CHIP_CHECK(hipStreamSynchronize(sl.s));
   for (int i = 0; i < 4; ++i)
     if (sl.buf[i]) CHIP_CHECK(hipFree(sl.buf[i]));
+  for (void* p : sl.retired) CHIP_CHECK(hipFree(p));
   for (int i = 0; i < 5; ++i)
     if (sl.ev[i]) CHIP_CHECK(hipEventDestroy(sl.ev[i]));
   CHIP_CHECK(hipStreamDestroy(sl.s));
@@ -160,11 +161,14 @@ void slot_init(SliceSlot& sl, uint32_t gpu) {
   for (int i = 0; i < 5; ++i) CHIP_CHECK(hipEventCreate(&sl.ev[i]));
 }
 
-// grow-only device buffer i of the slot (the slot's stream is idle between calls)
+// grow-only device buffer i of the slot (the slot's stream is idle between calls).  hipFree
+// synchronises the whole device, so an outgrown buffer is retired and freed after the slice
+// threads join: freeing it here stalled this slice until the other slices' kernels on the same
+// device had finished (seen in tests/test_gpu_runtime.py::test_slices_overlap_and_bit_exact).
 uint64_t* slot_buf(SliceSlot& sl, int i, uint64_t bytes) {
   bytes = std::max<uint64_t>(bytes, 8);
   if (sl.cap[i] < bytes) {
-    if (sl.buf[i]) CHIP_CHECK(hipFree(sl.buf[i]));
+    if (sl.buf[i]) sl.retired.push_back(sl.buf[i]);
     sl.buf[i] = nullptr;
     CHIP_CHECK(hipMalloc(&sl.buf[i], bytes));
     sl.cap[i] = bytes;
@@ -213,6 +217,13 @@ void run_sliced(concrete_hip_keyset* ks, uint64_t num_samples, F&& body) {
     for (uint64_t r = 0; r < parts; ++r)
       th.emplace_back([&, r] { body(ks->slots[r], start[r], count[r]); });
     for (auto& t : th) t.join();
+  }
+  for (uint64_t r = 0; r < parts; ++r) {
+    SliceSlot& sl = ks->slots[r];
+    if (sl.retired.empty()) continue;
+    CHIP_CHECK(hipSetDevice((int)sl.gpu));
+    for (void* p : sl.retired) CHIP_CHECK(hipFree(p));
+    sl.retired.clear();
   }
   bool seen[RT_MAX_DEV] = {};
   for (uint64_t r = 0; r < parts; ++r) {

@@ -42,6 +42,7 @@ struct SliceSlot {
   void* buf[4] = {};      // in, out, luts (+ accumulators), lut indexes
   uint64_t cap[4] = {};   // bytes
   hipEvent_t ev[5] = {};  // start, after H2D, after kernel, after D2H; ev[4] unused
+  std::vector<void*> retired;  // outgrown buffers, freed once every slice thread has joined
 };
 
 }  // namespace chip

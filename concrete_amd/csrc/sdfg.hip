@@ -78,7 +78,17 @@ struct Slot {
   hipStream_t s = nullptr;
   std::vector<void*> buf;
   std::vector<uint64_t> cap;
+  std::vector<void*> retired;  // outgrown buffers, freed once every shard thread has joined
 };
+
+// hipFree synchronises the whole device, so a buffer outgrown while other shards' kernels run on
+// the same device is retired and freed after the threads join
+void slot_free_retired(Slot& sl) {
+  if (sl.retired.empty()) return;
+  CHIP_CHECK(hipSetDevice((int)sl.gpu));
+  for (void* p : sl.retired) CHIP_CHECK(hipFree(p));
+  sl.retired.clear();
+}
 
 void slot_free(Slot& sl) {
   if (!sl.s) return;
@@ -86,6 +96,7 @@ void slot_free(Slot& sl) {
   CHIP_CHECK(hipStreamSynchronize(sl.s));
   for (void* p : sl.buf)
     if (p) CHIP_CHECK(hipFree(p));
+  for (void* p : sl.retired) CHIP_CHECK(hipFree(p));
   CHIP_CHECK(hipStreamDestroy(sl.s));
   sl = Slot{};
 }
@@ -327,7 +338,7 @@ void run_chunk(const Plan& P, Slot& sl, uint64_t start, uint64_t cnt) {
     bytes = std::max<uint64_t>(bytes, 8);
     if (nbuf == sl.buf.size()) sl.buf.push_back(nullptr), sl.cap.push_back(0);
     if (sl.cap[nbuf] < bytes) {
-      if (sl.buf[nbuf]) CHIP_CHECK(hipFree(sl.buf[nbuf]));
+      if (sl.buf[nbuf]) sl.retired.push_back(sl.buf[nbuf]);
       sl.buf[nbuf] = nullptr;
       CHIP_CHECK(hipMalloc(&sl.buf[nbuf], bytes));
       sl.cap[nbuf] = bytes;
@@ -467,6 +478,7 @@ void execute(Dfg* g, Stream* target) {
     for (uint64_t r = 0; r < parts; ++r) th.emplace_back(work, r);
     for (auto& t : th) t.join();
   }
+  for (uint64_t r = 0; r < parts; ++r) slot_free_retired(g->slots[r]);
   bool seen[RT_MAX_DEV] = {};
   for (uint64_t r = 0; r < parts; ++r) {
     const uint32_t d = g->slots[r].gpu;

@@ -18,6 +18,7 @@
 #define CONCRETE_HIP_H
 
 #include <stdbool.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -390,6 +391,75 @@ void stream_emulator_put_memref_batch(void *stream, uint64_t *allocated, uint64_
 void stream_emulator_get_memref_batch(void *stream, uint64_t *out_allocated, uint64_t *out_aligned,
                                       uint64_t out_offset, uint64_t out_size0, uint64_t out_size1,
                                       uint64_t out_stride0, uint64_t out_stride1);
+
+/* ------------------------------------------------------------------------------------------
+ * Part 5: key wire-format import (concrete_amd/csrc/keyio.cpp).
+ * Reads the evaluation keys of a serialized concrete keyset — the Cap'n Proto messages
+ * `ServerKeyset.serialize()` / `Keyset.serialize()` write (capnp::writeMessage, unpacked framing,
+ * include/concretelang/Common/Protocol.h:158-175; schema tools/concrete-protocol/src/
+ * concrete-protocol.capnp:149-297) — and registers them in a runtime keyset under the indexes the
+ * runtime context uses (list position, lib/Runtime/context.cpp:36-94), replacing the reference's
+ * ServerKeyset::fromProto + LweBootstrapKey/LweKeyswitchKey::fromProto (lib/Common/Keys.cpp:142-163,
+ * 262-283).  Payloads: List(Data) blobs concatenated (Protocol.h:349-372).  Seeded keys
+ * (Compression::SEED, Keys.cpp:193-218) are expanded by concrete-cpu's own decompressors, which the
+ * caller installs (the runtime already links concrete-cpu); without them a seeded key is refused.
+ * Only 64-bit keys over the native modulus are accepted (the PBS / KS kernels' torus).
+ * Returns 0, or < 0 with concrete_hip_last_error() set (malformed message, size mismatch, ...).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct concrete_hip_server_keyset concrete_hip_server_keyset;
+enum {
+  CONCRETE_HIP_ROOT_SERVER_KEYSET = 0,    /* ServerKeyset (ServerKeyset.serialize()) */
+  CONCRETE_HIP_ROOT_KEYSET = 1,           /* Keyset: its `server` part (Keyset.serialize()) */
+  CONCRETE_HIP_ROOT_LWE_BOOTSTRAP_KEY = 2, /* one LweBootstrapKey */
+  CONCRETE_HIP_ROOT_LWE_KEYSWITCH_KEY = 3  /* one LweKeyswitchKey */
+};
+typedef struct concrete_hip_key_info {
+  uint32_t id, input_id, output_id;          /* LweBootstrapKeyInfo / LweKeyswitchKeyInfo */
+  uint32_t level_count, base_log;
+  uint32_t glwe_dim, poly_size;              /* bootstrap keys only */
+  uint32_t input_lwe_dim, output_lwe_dim;    /* bootstrap keys: output = glwe_dim * poly_size */
+  uint32_t integer_precision;
+  uint32_t key_type;                         /* KeyType: 0 binary, 1 ternary */
+  uint32_t compression;                      /* Compression: 0 none, 1 seed, 2 paillier */
+  uint32_t modulus_kind, modulus_value;      /* Modulus union: 0 native, 1 power of two, 2 integer */
+  double variance;
+  uint64_t payload_words;                    /* u64 words on the wire */
+  uint64_t key_words;                        /* u64 words of the standard-domain key */
+} concrete_hip_key_info;
+int concrete_hip_server_keyset_deserialize(const void *bytes, uint64_t size, uint32_t root,
+                                           concrete_hip_server_keyset **out);
+int concrete_hip_server_keyset_load_file(const char *path, uint32_t root, concrete_hip_server_keyset **out);
+void concrete_hip_server_keyset_destroy(concrete_hip_server_keyset *sk);
+uint32_t concrete_hip_server_keyset_bsk_count(const concrete_hip_server_keyset *sk);
+uint32_t concrete_hip_server_keyset_ksk_count(const concrete_hip_server_keyset *sk);
+int concrete_hip_server_keyset_bsk_info(const concrete_hip_server_keyset *sk, uint32_t index,
+                                        concrete_hip_key_info *out);
+int concrete_hip_server_keyset_ksk_info(const concrete_hip_server_keyset *sk, uint32_t index,
+                                        concrete_hip_key_info *out);
+/* the standard-domain key (BSK [n][l][k+1][k+1][N], KSK [n_in][l][n_out+1]); dst holds >= key_words */
+int concrete_hip_server_keyset_read_bsk(const concrete_hip_server_keyset *sk, uint32_t index, uint64_t *dst,
+                                        uint64_t dst_words);
+int concrete_hip_server_keyset_read_ksk(const concrete_hip_server_keyset *sk, uint32_t index, uint64_t *dst,
+                                        uint64_t dst_words);
+/* every bootstrap key i -> bsk_index i, every keyswitch key i -> ksk_index i */
+int concrete_hip_keyset_add_server_keyset(concrete_hip_keyset *ks, const concrete_hip_server_keyset *sk);
+/* Same layout and calling convention as concrete-cpu's Uint128 and its decompressors
+ * (backends/concrete-cpu/implementation/include/concrete-cpu.h:49-51,185-207), so
+ * concrete_cpu_decompress_seeded_lwe_{bootstrap,keyswitch}_key_u64 install directly.  The last
+ * argument is concrete-cpu's Parallelism (1 = Rayon, what Keys.cpp:209-211 passes). */
+typedef struct concrete_hip_uint128 {
+  uint8_t little_endian_bytes[16];
+} concrete_hip_uint128;
+typedef void (*concrete_hip_bsk_decompressor)(uint64_t *lwe_bsk, const uint64_t *seeded_lwe_bsk,
+                                              size_t input_lwe_dimension, size_t output_polynomial_size,
+                                              size_t output_glwe_dimension, size_t decomposition_level_count,
+                                              size_t decomposition_base_log, concrete_hip_uint128 compression_seed,
+                                              uint32_t parallelism);
+typedef void (*concrete_hip_ksk_decompressor)(uint64_t *lwe_ksk, const uint64_t *seeded_lwe_ksk,
+                                              size_t input_lwe_dimension, size_t output_lwe_dimension,
+                                              size_t decomposition_level_count, size_t decomposition_base_log,
+                                              concrete_hip_uint128 compression_seed, uint32_t parallelism);
+void concrete_hip_set_seeded_key_decompressors(concrete_hip_bsk_decompressor bsk, concrete_hip_ksk_decompressor ksk);
 
 #ifdef __cplusplus
 }

@@ -262,3 +262,30 @@ def test_device_lut_encoding_and_accumulators(env):
             want[k * p.N:] = tl[r]
             assert np.array_equal(acc[r], want)
     assert L.concrete_hip_encode_expand_lut_device(s, 0, 1, 1000, 1, 8, 1, 3, 0) == -3  # 1000 / 8 is odd
+
+
+@pytest.mark.parametrize("layout", ["flat", "mixed"])
+def test_keyset_from_wire_format(env, layout):
+    """A server keyset serialized in the concrete-protocol wire form (include/concrete_hip.h Part 5)
+    loads into a runtime keyset and runs the PBS -> KS -> PBS chain bit-exactly (oracle)."""
+    from concrete_amd import keys as K
+    B, R, O, p = env["B"], env["R"], env["O"], env["p"]
+    width = 2
+    table = np.array([2, 0, 3, 1], dtype=np.uint64)
+    tlu = B.expand_lut(table, p.N, width)
+    msgs, cts = inputs(env, 6, width, 500)
+    data = K.serialize_server_keyset([(K.bsk_info(p), env["bsk"])], [(K.ksk_info(p), env["ksk"])],
+                                     layout=layout, blob_words=4096)
+    sk = K.ServerKeyset.deserialize(data)
+    ks = R.Keyset([0, 0])
+    sk.add_to(ks)
+    sk.close()
+    big = R.batched_bootstrap(ks, p, cts, tlu)
+    small = R.batched_keyswitch(ks, p, big)
+    out = R.batched_bootstrap(ks, p, small, tlu)
+    ks.close()
+    ref, _ = O.pbs_batch(env["op"], cts, B.trivial_glwe(p, tlu)[None, :], fbsk=env["fcpu"])
+    assert np.array_equal(big, ref)
+    assert np.array_equal(small, O.keyswitch_batch(env["op"], big, env["ksk"]))
+    dec = B.lwe_decrypt(env["glwe_sk"], out, p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[table[m]]) for m in msgs]

@@ -1,0 +1,274 @@
+"""Key wire-format import (include/concrete_hip.h Part 5, concrete_amd/csrc/keyio.cpp): CPU tests.
+
+Parity unpinned: the reference holds no serialized keyset (no capnp library or fixture in the
+image), so these tests pin the reader against (a) capnp's struct-layout rule recomputed here from
+the schema's field lists (concrete-protocol.capnp:149-207), (b) round trips through the writer in
+concrete_amd/keys.py in every pointer form capnp produces (near, single far, double far; one or
+many segments and blobs), (c) refusal of malformed or unsupported messages, and (d) the seeded-key
+hand-off to an installed concrete-cpu-signature decompressor.
+"""
+import ctypes as C
+import struct
+
+import numpy as np
+import pytest
+
+from concrete_amd import _native
+from concrete_amd import keys as K
+
+
+# ---- (a) capnp layout rule ------------------------------------------------------------------
+def _capnp_layout(fields):
+    """Byte offsets of data fields under capnp's allocation rule (fields in ordinal order, each in
+    the first free hole of its size, splitting larger holes, else a new word).  fields: list of
+    (name, bits) in ordinal order, bits = 0 for pointer fields.  Returns ({name: byte offset},
+    data words)."""
+    holes = {}  # lg size -> offset in units of that size
+    words = 0
+    out = {}
+
+    def try_alloc(lg):
+        if lg >= 6:
+            return None
+        if holes.get(lg):
+            v = holes.pop(lg)
+            return v
+        nxt = try_alloc(lg + 1)
+        if nxt is None:
+            return None
+        holes[lg] = nxt * 2 + 1
+        return nxt * 2
+
+    for name, bits in fields:
+        if bits == 0:
+            continue
+        lg = {8: 3, 16: 4, 32: 5, 64: 6}[bits]
+        off = try_alloc(lg)
+        if off is None:
+            off = words << (6 - lg)
+            words += 1
+            # the rest of the new word becomes holes of sizes lg .. 32 bits
+            o, s = off + 1, lg
+            while s < 6:
+                holes[s] = o
+                s += 1
+                o = (o + 1) // 2
+        out[name] = off * bits // 8
+    return out, words
+
+
+def test_schema_offsets_follow_capnp_layout():
+    info, w = _capnp_layout([("id", 32), ("input_id", 32), ("output_id", 32), ("params", 0), ("compression", 16)])
+    assert info == K.INFO_OFF and w == K.INFO_WORDS
+    bsk, w = _capnp_layout([("level_count", 32), ("base_log", 32), ("glwe_dim", 32), ("poly_size", 32),
+                            ("variance", 64), ("integer_precision", 32), ("modulus", 0), ("key_type", 16),
+                            ("input_lwe_dim", 32)])
+    assert bsk == K.BSK_PARAMS_OFF and w == K.BSK_PARAMS_WORDS
+    ksk, w = _capnp_layout([("level_count", 32), ("base_log", 32), ("variance", 64), ("integer_precision", 32),
+                            ("modulus", 0), ("key_type", 16), ("input_lwe_dim", 32), ("output_lwe_dim", 32)])
+    assert ksk == K.KSK_PARAMS_OFF and w == K.KSK_PARAMS_WORDS
+
+
+# ---- (b) round trips ------------------------------------------------------------------------
+class _P:  # a small backend.PbsParams-like parameter set
+    n, k, N, level, base_log, ks_level, ks_base_log = 5, 1, 16, 2, 7, 3, 4
+    big_n = 16
+
+
+def _keys(rng, n_bsk=2, n_ksk=1):
+    bsks, ksks = [], []
+    for i in range(n_bsk):
+        info = K.bsk_info(_P, id=i, input_id=2 * i, output_id=2 * i + 1, variance=2.0 ** -60 * (i + 1))
+        bsks.append((info, rng.integers(0, 2 ** 64, size=info.bsk_words(), dtype=np.uint64)))
+    for i in range(n_ksk):
+        info = K.ksk_info(_P, id=10 + i, input_id=1, output_id=0, variance=2.0 ** -30, key_type=0)
+        ksks.append((info, rng.integers(0, 2 ** 64, size=info.ksk_words(), dtype=np.uint64)))
+    return bsks, ksks
+
+
+def _check(sk, bsks, ksks):
+    assert len(sk.bootstrap_keys) == len(bsks) and len(sk.keyswitch_keys) == len(ksks)
+    for i, (info, payload) in enumerate(bsks):
+        got = sk.bootstrap_keys[i]
+        for f in ("id", "input_id", "output_id", "level_count", "base_log", "glwe_dim", "poly_size",
+                  "input_lwe_dim", "integer_precision", "key_type", "compression", "variance"):
+            assert getattr(got, f) == getattr(info, f), f
+        assert got.output_lwe_dim == info.glwe_dim * info.poly_size
+        assert got.payload_words == payload.size == got.key_words
+        assert np.array_equal(sk.bsk(i), payload)
+    for i, (info, payload) in enumerate(ksks):
+        got = sk.keyswitch_keys[i]
+        for f in ("id", "input_id", "output_id", "level_count", "base_log", "input_lwe_dim", "output_lwe_dim",
+                  "integer_precision", "variance"):
+            assert getattr(got, f) == getattr(info, f), f
+        assert np.array_equal(sk.ksk(i), payload)
+
+
+@pytest.mark.parametrize("layout", ["flat", "single_far", "double_far", "mixed"])
+@pytest.mark.parametrize("blob_words", [K.BLOB_WORDS, 7])
+def test_server_keyset_round_trip(layout, blob_words):
+    rng = np.random.default_rng(1)
+    bsks, ksks = _keys(rng)
+    data = K.serialize_server_keyset(bsks, ksks, layout=layout, blob_words=blob_words)
+    nseg = struct.unpack_from("<I", data)[0] + 1
+    assert (nseg == 1) == (layout == "flat")
+    _check(K.ServerKeyset.deserialize(data), bsks, ksks)
+
+
+def test_keyset_and_single_key_roots(tmp_path):
+    rng = np.random.default_rng(2)
+    bsks, ksks = _keys(rng, 1, 2)
+    _check(K.ServerKeyset.deserialize(K.serialize_server_keyset(bsks, ksks, root="keyset", layout="mixed"),
+                                      root="keyset"), bsks, ksks)
+    one = K.serialize_server_keyset(bsks, root="bootstrap_key", layout="single_far")
+    _check(K.ServerKeyset.deserialize(one, root="bootstrap_key"), bsks, [])
+    one = K.serialize_server_keyset(ksks=ksks[1:], root="keyswitch_key")
+    _check(K.ServerKeyset.deserialize(one, root="keyswitch_key"), [], ksks[1:])
+    path = tmp_path / "server.keys"
+    path.write_bytes(K.serialize_server_keyset(bsks, ksks, layout="double_far"))
+    _check(K.ServerKeyset.load(path), bsks, ksks)
+    empty = K.ServerKeyset.deserialize(K.serialize_server_keyset())
+    assert empty.bootstrap_keys == [] and empty.keyswitch_keys == []
+
+
+def test_unaligned_input_is_copied():
+    rng = np.random.default_rng(3)
+    bsks, ksks = _keys(rng, 1, 1)
+    data = K.serialize_server_keyset(bsks, ksks)
+    buf = np.zeros(len(data) + 8, dtype=np.uint8)
+    raw = buf[1:1 + len(data)]
+    raw[:] = np.frombuffer(data, dtype=np.uint8)
+    lib = _native.lib()
+    h = C.c_void_p()
+    _native.check(lib.concrete_hip_server_keyset_deserialize(raw.ctypes.data, len(data), 0, C.byref(h)), "deser")
+    sk = K.ServerKeyset(h.value)
+    _check(sk, bsks, ksks)
+
+
+# ---- (c) refusals -----------------------------------------------------------------------------
+def _deser_rc(data: bytes, root=0):
+    lib = _native.lib()
+    h = C.c_void_p()
+    buf = np.frombuffer(data, dtype=np.uint8).copy() if data else np.zeros(8, np.uint8)
+    rc = lib.concrete_hip_server_keyset_deserialize(buf.ctypes.data, len(data), root, C.byref(h))
+    if rc == 0:
+        lib.concrete_hip_server_keyset_destroy(h.value)
+    return rc
+
+
+def test_malformed_messages_are_refused():
+    rng = np.random.default_rng(4)
+    bsks, ksks = _keys(rng, 1, 1)
+    good = K.serialize_server_keyset(bsks, ksks, layout="mixed")
+    assert _deser_rc(good) == 0
+    assert _deser_rc(b"") < 0
+    assert _deser_rc(good[:-8]) < 0  # last segment truncated
+    assert _deser_rc(good[:-3]) < 0  # not whole words
+    assert _deser_rc(struct.pack("<II", 10000, 1) + b"\0" * 8) < 0  # absurd segment count
+    # root pointer aimed past the segment
+    bad = bytearray(good)
+    nseg = struct.unpack_from("<I", bad)[0] + 1
+    hdr = ((4 * (1 + nseg) + 7) // 8) * 8
+    struct.pack_into("<Q", bad, hdr, (0x1000 << 2) | (3 << 48))
+    assert _deser_rc(bytes(bad)) < 0
+    # a far pointer into a segment that does not exist
+    struct.pack_into("<Q", bad, hdr, 2 | (0 << 3) | (77 << 32))
+    assert _deser_rc(bytes(bad)) < 0
+    # a capability pointer as root
+    struct.pack_into("<Q", bad, hdr, 3)
+    assert _deser_rc(bytes(bad)) < 0
+    assert _deser_rc(good, root=9) < 0
+
+
+def test_unsupported_and_mismatched_keys_are_refused():
+    rng = np.random.default_rng(5)
+    (info, payload), = _keys(rng, 1, 0)[0]
+    short = K.serialize_server_keyset([(info, payload[:-1])])
+    sk = K.ServerKeyset.deserialize(short)  # parses: sizes are checked when the key is read
+    with pytest.raises(RuntimeError, match="payload has"):
+        sk.bsk(0)
+    info32 = K.KeyInfo(**{**info.__dict__, "integer_precision": 32})
+    sk = K.ServerKeyset.deserialize(K.serialize_server_keyset([(info32, payload)]))
+    with pytest.raises(RuntimeError, match="64-bit"):
+        sk.bsk(0)
+    pow2 = K.KeyInfo(**{**info.__dict__, "modulus_kind": 1, "modulus_value": 62})
+    sk = K.ServerKeyset.deserialize(K.serialize_server_keyset([(pow2, payload)]))
+    assert sk.bootstrap_keys[0].modulus_kind == 1 and sk.bootstrap_keys[0].modulus_value == 62
+    with pytest.raises(RuntimeError, match="native modulus"):
+        sk.bsk(0)
+
+
+# ---- (d) seeded keys --------------------------------------------------------------------------
+class _U128(C.Structure):
+    _fields_ = [("little_endian_bytes", C.c_uint8 * 16)]
+
+
+_BSK_DEC = C.CFUNCTYPE(None, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_size_t, C.c_size_t, C.c_size_t,
+                       C.c_size_t, C.c_size_t, _U128, C.c_uint32)
+_KSK_DEC = C.CFUNCTYPE(None, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_size_t, C.c_size_t, C.c_size_t,
+                       C.c_size_t, _U128, C.c_uint32)
+
+
+def test_seeded_keys_use_the_installed_decompressors():
+    lib = _native.lib()
+    calls = []
+
+    def fake_mask(seed_bytes, i):  # stand-in for concrete-csprng's mask stream (test only)
+        return (int.from_bytes(seed_bytes, "little") * 0x9E3779B97F4A7C15 + i) % 2 ** 64
+
+    @_BSK_DEC
+    def bsk_dec(out, seeded, n, N, k, l, logB, seed, par):
+        sb = bytes(seed.little_endian_bytes)
+        calls.append(("bsk", n, N, k, l, logB, sb, par))
+        # standard layout [n][l][k+1 rows][k+1 polys][N]: masks from the "stream", bodies copied
+        body = 0
+        for row in range(n * l * (k + 1)):
+            for poly in range(k + 1):
+                for c in range(N):
+                    dst = (row * (k + 1) + poly) * N + c
+                    if poly == k:
+                        out[dst] = seeded[body]
+                        body += 1
+                    else:
+                        out[dst] = fake_mask(sb, dst)
+
+    @_KSK_DEC
+    def ksk_dec(out, seeded, n_in, n_out, l, logB, seed, par):
+        sb = bytes(seed.little_endian_bytes)
+        calls.append(("ksk", n_in, n_out, l, logB, sb, par))
+        for row in range(n_in * l):
+            for c in range(n_out):
+                out[row * (n_out + 1) + c] = fake_mask(sb, row * (n_out + 1) + c)
+            out[row * (n_out + 1) + n_out] = seeded[row]
+
+    rng = np.random.default_rng(6)
+    bi = K.bsk_info(_P, compression=1)
+    ki = K.ksk_info(_P, compression=1)
+    seed = [0x0706050403020100, 0x0F0E0D0C0B0A0908]  # writeSeed: byte b at word b // 8, bits 8 (b % 8)
+    b_bodies = rng.integers(0, 2 ** 64, size=_P.n * _P.level * (_P.k + 1) * _P.N, dtype=np.uint64)
+    k_bodies = rng.integers(0, 2 ** 64, size=_P.big_n * _P.ks_level, dtype=np.uint64)
+    data = K.serialize_server_keyset([(bi, np.concatenate([np.array(seed, np.uint64), b_bodies]))],
+                                     [(ki, np.concatenate([np.array(seed, np.uint64), k_bodies]))])
+    sk = K.ServerKeyset.deserialize(data)
+    assert sk.bootstrap_keys[0].compression == 1
+    assert sk.bootstrap_keys[0].payload_words == 2 + b_bodies.size
+    assert sk.bootstrap_keys[0].key_words == bi.bsk_words()
+    lib.concrete_hip_set_seeded_key_decompressors(None, None)
+    with pytest.raises(RuntimeError, match="seeded"):
+        sk.bsk(0)
+    lib.concrete_hip_set_seeded_key_decompressors(C.cast(bsk_dec, C.c_void_p), C.cast(ksk_dec, C.c_void_p))
+    try:
+        b = sk.bsk(0).reshape(_P.n * _P.level * (_P.k + 1), _P.k + 1, _P.N)
+        kk = sk.ksk(0).reshape(_P.big_n * _P.ks_level, _P.n + 1)
+    finally:
+        lib.concrete_hip_set_seeded_key_decompressors(None, None)
+    sb = bytes(range(16))
+    assert calls[0] == ("bsk", _P.n, _P.N, _P.k, _P.level, _P.base_log, sb, 1)
+    assert calls[1] == ("ksk", _P.big_n, _P.n, _P.ks_level, _P.ks_base_log, sb, 1)
+    assert np.array_equal(b[:, _P.k, :].ravel(), b_bodies)
+    assert int(b[0, 0, 3]) == fake_mask(sb, 3)
+    assert np.array_equal(kk[:, _P.n], k_bodies)
+    # a seeded payload of the wrong size is refused before the decompressor runs
+    bad = K.serialize_server_keyset([(bi, np.concatenate([np.array(seed, np.uint64), b_bodies[:-1]]))])
+    with pytest.raises(RuntimeError, match="seeded payload"):
+        K.ServerKeyset.deserialize(bad).bsk(0)

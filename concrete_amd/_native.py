@@ -124,7 +124,7 @@ SIGNATURES = {
     "stream_emulator_make_memref_batch_stream": (vp, [C.c_char_p, i32]),
     "stream_emulator_put_memref_batch": (None, [vp, vp, vp, u64, u64, u64, u64, u64, u64]),
     "stream_emulator_get_memref_batch": (None, [vp, vp, vp, u64, u64, u64, u64, u64]),
-    # Part 5: key wire-format import (concrete-protocol.capnp)
+    # Part 6: key wire-format import (concrete-protocol.capnp)
     "concrete_hip_server_keyset_deserialize": (i32, [vp, u64, u32, C.POINTER(vp)]),
     "concrete_hip_server_keyset_load_file": (i32, [C.c_char_p, u32, C.POINTER(vp)]),
     "concrete_hip_server_keyset_destroy": (None, [vp]),

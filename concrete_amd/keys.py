@@ -1,6 +1,6 @@
 """Key wire format: concrete keysets as Cap'n Proto messages.
 
-Reading is native (``concrete_amd/csrc/keyio.cpp``, include/concrete_hip.h Part 5): a server
+Reading is native (``concrete_amd/csrc/keyio.cpp``, include/concrete_hip.h Part 6): a server
 keyset written by the reference's ``ServerKeyset.serialize()`` / ``Keyset.serialize()``
 (capnp::writeMessage, compiler include/concretelang/Common/Protocol.h:158-175; schema
 tools/concrete-protocol/src/concrete-protocol.capnp:149-297) loads into a runtime keyset under

@@ -393,7 +393,7 @@ void stream_emulator_get_memref_batch(void *stream, uint64_t *out_allocated, uin
                                       uint64_t out_stride0, uint64_t out_stride1);
 
 /* ------------------------------------------------------------------------------------------
- * Part 5: key wire-format import (concrete_amd/csrc/keyio.cpp).
+ * Part 6: key wire-format import (concrete_amd/csrc/keyio.cpp).
  * Reads the evaluation keys of a serialized concrete keyset — the Cap'n Proto messages
  * `ServerKeyset.serialize()` / `Keyset.serialize()` write (capnp::writeMessage, unpacked framing,
  * include/concretelang/Common/Protocol.h:158-175; schema tools/concrete-protocol/src/

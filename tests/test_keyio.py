@@ -1,4 +1,4 @@
-"""Key wire-format import (include/concrete_hip.h Part 5, concrete_amd/csrc/keyio.cpp): CPU tests.
+"""Key wire-format import (include/concrete_hip.h Part 6, concrete_amd/csrc/keyio.cpp): CPU tests.
 
 Parity unpinned: the reference holds no serialized keyset (no capnp library or fixture in the
 image), so these tests pin the reader against (a) capnp's struct-layout rule recomputed here from

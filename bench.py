@@ -30,14 +30,17 @@ FP64_PEAK_TFS = 78.6
 METRIC = "PBS/sec (whole node) at N=1024 batch=4096; achieved HBM GB/s"
 
 
-KERNEL_SOURCES = ("concrete_amd/csrc/pbs.hip", "concrete_amd/csrc/pbs2048.hip", "concrete_amd/csrc/pbs.hpp",
-                  "concrete_amd/csrc/fft512.hpp", "concrete_amd/csrc/kernel_util.hpp", "concrete_amd/csrc/common.hpp")
+# the sources a config's PMC record was measured on (a record is used only while they are unchanged)
+KERNEL_HEADERS = ("concrete_amd/csrc/pbs.hpp", "concrete_amd/csrc/fft512.hpp", "concrete_amd/csrc/kernel_util.hpp",
+                  "concrete_amd/csrc/common.hpp")
+KERNEL_SOURCES = {"cfg2": ("concrete_amd/csrc/pbs.hip",) + KERNEL_HEADERS,
+                  "cfg4": ("concrete_amd/csrc/pbs2048.hip",) + KERNEL_HEADERS}
 
 
-def kernel_source_hash() -> str:
+def kernel_source_hash(config: str = "cfg2") -> str:
     import hashlib
     h = hashlib.sha1()
-    for f in KERNEL_SOURCES:
+    for f in KERNEL_SOURCES.get(config, ("concrete_amd/csrc/pbs_generic.hip",) + KERNEL_HEADERS):
         with open(os.path.join(ROOT, f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]
@@ -53,7 +56,7 @@ def pmc_records(config: str):
     for f in sorted(files, key=os.path.basename, reverse=True):
         with open(f) as fh:
             rec = json.load(fh)
-        if rec.get("source_hash") == kernel_source_hash() and rec.get("config", "cfg2") == config:
+        if rec.get("source_hash") == kernel_source_hash(config) and rec.get("config", "cfg2") == config:
             rec["src"] = os.path.relpath(f, ROOT)
             out.append(rec)
     return out

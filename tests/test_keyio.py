@@ -272,3 +272,43 @@ def test_seeded_keys_use_the_installed_decompressors():
     bad = K.serialize_server_keyset([(bi, np.concatenate([np.array(seed, np.uint64), b_bodies[:-1]]))])
     with pytest.raises(RuntimeError, match="seeded payload"):
         K.ServerKeyset.deserialize(bad).bsk(0)
+
+
+# ---- (e) the C boundary ------------------------------------------------------------------------
+def _fnv(words: np.ndarray) -> int:
+    h = 1469598103934665603
+    for w in words.tolist():
+        h = ((h ^ w) * 1099511628211) % 2 ** 64
+    return h
+
+
+def test_c_client_reads_the_same_keys(tmp_path):
+    """tests/c_client/keyio_client.c (C99) loads the file and reports every key's info and a
+    checksum of its words: the C struct layout and the ctypes one agree."""
+    import os
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not installed")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    libdir = os.path.join(root, "concrete_amd")
+    exe = tmp_path / "keyio_client"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(root, "include"),
+                    os.path.join(root, "tests", "c_client", "keyio_client.c"), "-L", libdir, "-lconcrete_hip",
+                    f"-Wl,-rpath,{libdir}", "-o", str(exe)], check=True)
+    rng = np.random.default_rng(7)
+    bsks, ksks = _keys(rng, 2, 2)
+    path = tmp_path / "server.keys"
+    path.write_bytes(K.serialize_server_keyset(bsks, ksks, layout="mixed", blob_words=9))
+    out = subprocess.run([str(exe), str(path)], check=True, capture_output=True, text=True, timeout=60).stdout
+    want = []
+    for kind, keys in (("bsk", bsks), ("ksk", ksks)):
+        for i, (info, payload) in enumerate(keys):
+            n_out = info.glwe_dim * info.poly_size if kind == "bsk" else info.output_lwe_dim
+            want.append(f"{kind} {i} {info.id} {info.level_count} {info.base_log} {info.glwe_dim} {info.poly_size} "
+                        f"{info.input_lwe_dim} {n_out} {info.compression} {payload.size} {_fnv(payload)}")
+    assert out.split("\n")[:-1] == want
+    bad = tmp_path / "bad.keys"
+    bad.write_bytes(path.read_bytes()[:-8])
+    r = subprocess.run([str(exe), str(bad)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "segment" in r.stderr

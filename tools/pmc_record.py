@@ -37,7 +37,7 @@ def main():
     src, dst, config, batch = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
     kname = KERNEL.get(config, config)
     v = collect(src, kname)
-    rec = {"kernel": kname, "config": config, "batch": batch, "source_hash": kernel_source_hash(), "pmc_dir": src,
+    rec = {"kernel": kname, "config": config, "batch": batch, "source_hash": kernel_source_hash(config), "pmc_dir": src,
            "counters": v}
     if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
         rec["traffic_bytes"] = int(round((2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024))

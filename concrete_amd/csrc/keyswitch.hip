@@ -29,7 +29,8 @@ constexpr int KS_TILE = 8;
 constexpr int KS_THREADS = 256;
 constexpr int KS_ICHUNK = 32;
 constexpr int KS_MAX_U = 4;                       // output words per thread per sample
-constexpr int KS_MAX_OUT = KS_MAX_U * KS_THREADS;  // n_out + 1 <= 1024 (the optimizer's n <= 1006 rows)
+constexpr int KS_MAX_OUT = KS_MAX_U * KS_THREADS;  // output words per block (wider rows: windows in blockIdx.z)
+constexpr uint32_t KS_MAX_ROW = 1u << 16;           // n_out + 1 accepted (LWE dimensions are far below)
 constexpr int KS_MAX_L = 8;
 // batches from this size take the MFMA path when it is exact (CONCRETE_HIP_KS_PATH: 0 = never,
 // 1 = always when exact; A/B and test switch)
@@ -65,6 +66,7 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
   const uint32_t s0 = blockIdx.x * KS_TILE;
   const int tid = threadIdx.x;
   const uint32_t W = n_out + 1;
+  const uint32_t jz = blockIdx.z * (uint32_t)KS_MAX_OUT;  // this block's window of output words
   uint64_t acc[KS_TILE][U];
 #pragma unroll
   for (int s = 0; s < KS_TILE; ++s)
@@ -102,7 +104,7 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
             const uint64_t* row = ksk + ((uint64_t)(i0 + ii) * level + t) * W;
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-              const uint32_t j = tid + u * KS_THREADS;
+              const uint32_t j = jz + tid + u * KS_THREADS;
               const uint64_t kv = j < W ? row[j] : 0ull;
               int32_t kc[NCH];
               if constexpr (NCH == 3) {
@@ -139,7 +141,7 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
           const uint64_t* row = ksk + ((uint64_t)(i0 + ii) * level + t) * W;
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            const uint32_t j = tid + u * KS_THREADS;
+            const uint32_t j = jz + tid + u * KS_THREADS;
             const uint64_t kv = j < W ? row[j] : 0ull;
 #pragma unroll
             for (int s = 0; s < KS_TILE; ++s) acc[s][u] -= (uint64_t)dig[ii][t][s] * kv;
@@ -156,7 +158,7 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
     uint64_t* co = out + (out_idx ? out_idx[smp] : smp) * (uint64_t)W;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t j = tid + u * KS_THREADS;
+      const uint32_t j = jz + tid + u * KS_THREADS;
       if (j >= W) continue;
       const uint64_t v = acc[s][u] + (j == n_out && (!SPLIT || blockIdx.y == 0) ? ci[n_in] : 0ull);
       if constexpr (SPLIT) atomicAdd((unsigned long long*)&co[j], (unsigned long long)v);
@@ -588,7 +590,7 @@ static int keyswitch_mfma_launch(const KsArgs& a) {
 }
 
 int keyswitch_launch(const KsArgs& a) {
-  if (a.n_out + 1 > (uint32_t)KS_MAX_OUT || a.level > (uint32_t)KS_MAX_L || a.level == 0 ||
+  if (a.n_out + 1 > KS_MAX_ROW || a.level > (uint32_t)KS_MAX_L || a.level == 0 ||
       a.level * a.base_log >= 64 || a.base_log == 0) {
     set_error("unsupported keyswitch parameters: n_out=%u level=%u base_log=%u", a.n_out, a.level, a.base_log);
     return -2;
@@ -600,7 +602,9 @@ int keyswitch_launch(const KsArgs& a) {
     const int rc = keyswitch_mfma_launch(a);
     if (rc != -5) return rc;  // -5: operand memory unavailable, run the VALU kernel below
   }
-  const uint32_t U = (a.n_out + 1 + KS_THREADS - 1) / KS_THREADS;
+  // output words in windows of KS_MAX_OUT (blockIdx.z): U words per thread in each
+  const uint32_t zw = (a.n_out + 1 + KS_MAX_OUT - 1) / KS_MAX_OUT;
+  const uint32_t U = (std::min<uint32_t>(a.n_out + 1, KS_MAX_OUT) + KS_THREADS - 1) / KS_THREADS;
   // enough workgroups for 256 CUs: split the mask positions when the batch alone is short
   uint32_t splits = 1;
   if (blocks < 512) splits = std::min<uint32_t>((512 + blocks - 1) / blocks, std::max<uint32_t>(1, a.n_in / 128));
@@ -620,11 +624,11 @@ int keyswitch_launch(const KsArgs& a) {
                   : dmax <= 0x7fffffffull / ((uint64_t)KS_ICHUNK * 65535ull) ? 4 : 0;
 #define KS_LAUNCH2(UU, CH)                                                                                         \
   if (splits > 1)                                                                                                  \
-    hipLaunchKernelGGL((keyswitch_kernel<UU, true, CH>), dim3(blocks, splits), dim3(KS_THREADS), 0, a.stream,     \
+    hipLaunchKernelGGL((keyswitch_kernel<UU, true, CH>), dim3(blocks, splits, zw), dim3(KS_THREADS), 0, a.stream,     \
                        a.out, a.out_idx, a.in, a.in_idx, a.ksk, a.n_in, a.n_out, a.base_log, a.level,              \
                        a.num_samples, per);                                                                        \
   else                                                                                                             \
-    hipLaunchKernelGGL((keyswitch_kernel<UU, false, CH>), dim3(blocks), dim3(KS_THREADS), 0, a.stream, a.out,     \
+    hipLaunchKernelGGL((keyswitch_kernel<UU, false, CH>), dim3(blocks, 1, zw), dim3(KS_THREADS), 0, a.stream, a.out,     \
                        a.out_idx, a.in, a.in_idx, a.ksk, a.n_in, a.n_out, a.base_log, a.level, a.num_samples, per)
 #define KS_LAUNCH(UU)          \
   if (nch == 3) {              \

@@ -402,7 +402,7 @@ int concrete_hip_keyset_add_bsk(concrete_hip_keyset* ks, uint32_t bsk_index, con
 
 int concrete_hip_keyset_add_ksk(concrete_hip_keyset* ks, uint32_t ksk_index, const uint64_t* ksk, uint32_t level,
                                 uint32_t base_log, uint32_t input_lwe_dim, uint32_t output_lwe_dim) {
-  if (!ks || !ksk || level == 0 || base_log == 0 || level * base_log >= 64 || output_lwe_dim + 1 > 1024) {
+  if (!ks || !ksk || level == 0 || base_log == 0 || level * base_log >= 64 || output_lwe_dim + 1 > (1u << 16)) {
     set_error("keyset_add_ksk: bad argument");
     return -3;
   }

@@ -535,3 +535,22 @@ def test_pbs_pairs_per_workgroup(B, oracle, torch_cuda, monkeypatch, pairs, leve
     assert np.array_equal(got, exp)
     r = float(np.array([int(resid.cpu()[0])], dtype=np.int64).view(np.float64)[0])
     assert r < oracle.fft_error_bound(S.op, S.fbsk_cpu) < 0.5
+
+
+@pytest.mark.parametrize("n_out,ks_l,ks_logB,nb", [(1024, 4, 3, 37), (1500, 4, 3, 37), (1500, 2, 11, 21),
+                                                   (2100, 3, 4, 96), (1024, 4, 3, 80)])
+def test_keyswitch_wide_output_rows(B, oracle, torch_cuda, n_out, ks_l, ks_logB, nb):
+    """Output LWE dimensions past 1023 (the VALU kernel's 1024-word block, now windows of 1024
+    words in blockIdx.z; the matrix-core path from 64 samples): n + 1 = 1025 (a one-word second
+    window), 1501, 2101; int32-chunk and 64-bit product forms; bit-exact vs the oracle."""
+    p = replace(B.CFG2, n=n_out, ks_level=ks_l, ks_base_log=ks_logB)
+    glwe_sk = B.binary_key(p.big_n, 8700 + n_out)
+    lwe_sk = B.binary_key(p.n, 8800 + n_out)
+    ksk = B.ksk_generate(p, glwe_sk, lwe_sk, 8900 + n_out)
+    rng = np.random.RandomState(n_out + nb)
+    cts = rng.randint(0, 2 ** 63, size=(nb, p.big_n + 1), dtype=np.int64).astype(np.uint64) * np.uint64(2) + \
+        np.uint64(1)
+    out = B.keyswitch(p, B.to_device(ksk, "cuda:0"), B.to_device(cts, "cuda:0"))
+    torch_cuda.cuda.synchronize()
+    op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, ks_l=ks_l, ks_logB=ks_logB)
+    assert np.array_equal(B.to_host(out), oracle.keyswitch_batch(op, cts, ksk))

@@ -22,7 +22,7 @@ i64p = C.POINTER(C.c_int64)
 f64p = C.POINTER(C.c_double)
 sz = C.c_size_t
 
-MODE_SCHOOLBOOK, MODE_KARATSUBA, MODE_FFT = 0, 1, 2
+MODE_SCHOOLBOOK, MODE_KARATSUBA, MODE_FFT, MODE_FFT64 = 0, 1, 2, 3  # FFT64: approximate (tfhe_oracle.h)
 
 
 def build():

@@ -286,6 +286,10 @@ void ora_limb_widths(size_t L, int *w) {
 }
 void ora_limb_split(uint64_t g, size_t L, int64_t *limbs) {
     int w[16];
+    if (L == 1) { /* one 64-bit limb: the signed value (fft64's u64 -> i64 reading) */
+        limbs[0] = (int64_t)g;
+        return;
+    }
     ora_limb_widths(L, w);
     uint64_t rem = g;
     for (size_t i = 0; i < L; i++) {
@@ -480,6 +484,15 @@ double ora_fft_error_bound(const double *fbsk, size_t n, size_t k, size_t N, siz
     return rows * dnorm * maxG * (4.0 * gamma + 3.0 * u) * 1.0001 + 4.0 * u * max_out;
 }
 
+/* an integer-valued double of any magnitude, reduced mod 2^64 (exact: x - q 2^64 is a multiple of
+ * x's ulp and lies in [0, 2^64)) */
+static inline uint64_t wrap_u64(double x) {
+    double q = floor(ldexp(x, -64));
+    double r = x - ldexp(q, 64);
+    if (r >= 0x1p63) r -= 0x1p64;
+    return (uint64_t)(int64_t)r;
+}
+
 /* ======================================================================================
  * external product / CMUX / blind rotate / PBS (tfhe 0.10 fft64 add_external_product_assign,
  * blind_rotate_assign, programmable_bootstrap_lwe_ciphertext_mem_optimized; call site
@@ -552,6 +565,13 @@ void ora_external_product_acc(uint64_t *acc, const uint64_t *ggsw_std, const dou
                 double cr = yr[j] * zr + yi[j] * zi;
                 double ci = yi[j] * zr - yr[j] * zi;
                 double rr = nearbyint(cr), ri = nearbyint(ci);
+                if (mode == ORA_MODE_FFT64) {
+                    /* one 64-bit key limb (concrete-cpu's fft64): the products exceed 2^53, so the
+                     * low bits carry f64 rounding noise; the rounded value is reduced mod 2^64 */
+                    acc[col * N + j] += wrap_u64(rr);
+                    acc[col * N + j + M] += wrap_u64(ri);
+                    continue;
+                }
                 if (max_resid) {
                     double e1 = fabs(cr - rr), e2 = fabs(ci - ri);
                     if (e1 > *max_resid) *max_resid = e1;

@@ -93,7 +93,11 @@ void ora_bsk_to_fourier(double *fbsk, const uint64_t *bsk, size_t n, size_t k, s
 double ora_fft_error_bound(const double *fbsk, size_t n, size_t k, size_t N, size_t l, size_t logB, size_t L);
 
 /* ---------------- PBS / KS ---------------- */
-enum { ORA_MODE_SCHOOLBOOK = 0, ORA_MODE_KARATSUBA = 1, ORA_MODE_FFT = 2 };
+/* ORA_MODE_FFT64: the limb-FFT path with ONE 64-bit key limb (fbsk from limbs = 1), i.e. the
+ * arithmetic of concrete-cpu's fft64 (tfhe 0.10: u64 -> i64 -> f64 key spectrum, f64 products,
+ * rounding mod 2^64): NOT exact (the low output bits carry FFT noise, which decryption absorbs);
+ * bench.py times it as the closer-to-reference CPU baseline, never as a parity check. */
+enum { ORA_MODE_SCHOOLBOOK = 0, ORA_MODE_KARATSUBA = 1, ORA_MODE_FFT = 2, ORA_MODE_FFT64 = 3 };
 /* acc (k+1)N in/out: acc += ExtProd(GGSW_i, ct1) */
 void ora_external_product_acc(uint64_t *acc, const uint64_t *ggsw_std, const double *ggsw_fourier,
                               const uint64_t *ct1, size_t k, size_t N, size_t l, size_t logB, size_t L,

@@ -372,3 +372,26 @@ def test_generic_error_bound_matches_the_kernel_gate(oracle):
             else:  # a one-value "key" whose spectrum magnitude is maxg (scaled by 1/M like the device key)
                 py = oracle.generic_error_bound(k, N, l, logB, bits.value, np.array([maxg / (N / 2), 0.0]))
             assert abs(c_val - py) <= 1e-12 * max(1.0, abs(py)), (k, N, l, logB, maxg, c_val, py)
+
+
+@pytest.mark.parametrize("cfg", ["CFG2", "CFG4"])
+def test_pbs_fft64_mode_decrypts(oracle, cfg):
+    """ORA_MODE_FFT64 (the CPU baseline bench.py times): concrete-cpu's fft64 arithmetic — one f64
+    spectrum of the u64 key, f64 products rounded mod 2^64.  Not exact (its ciphertexts diverge from
+    the exact path's after the first rounding difference changes a digit), but every output decrypts
+    to the LUT value."""
+    from dataclasses import replace
+    p0 = getattr(oracle, cfg)
+    p = replace(p0, n=64, limbs=1)
+    lwe_sk = oracle.binary_key(p.n, 201)
+    glwe_sk = oracle.binary_key(p.k * p.N, 202)
+    bsk = oracle.keygen_bsk(p, lwe_sk, glwe_sk, 203)
+    width = 3 if cfg == "CFG2" else 5
+    rng = np.random.RandomState(1)
+    table = rng.randint(0, 1 << width, size=1 << width).astype(np.uint64)
+    acc = oracle.trivial_glwe(p, oracle.expand_lut(table, p.N, width))[None, :]
+    msgs = np.arange(12) % (1 << width)
+    cts = oracle.lwe_encrypt_batch(lwe_sk, [oracle.encode(m, width) for m in msgs], p.n, 2.0 ** -25, 204)
+    out, _ = oracle.pbs_batch(p, cts, acc, fbsk=oracle.bsk_to_fourier(p, bsk), mode=oracle.MODE_FFT64)
+    dec = oracle.lwe_decrypt_batch(glwe_sk, out, p.big_n)
+    assert [oracle.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]

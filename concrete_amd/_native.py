@@ -48,6 +48,9 @@ SIGNATURES = {
     "concrete_hip_pbs": (i32, [vp, u32, vp, vp, vp, vp, vp, vp, vp, u32, u32, u32, u32, u32, u32, vp]),
     "concrete_hip_keyswitch": (i32, [vp, u32, vp, vp, vp, vp, vp, u32, u32, u32, u32, u32]),
     "concrete_hip_lookup_bsk": (vp, [vp]),
+    "concrete_hip_generic_bsk_size_bytes": (u64, [u32, u32, u32, u32]),
+    "concrete_hip_convert_bsk_generic": (i32, [vp, u32, vp, vp, i32, u32, u32, u32, u32]),
+    "concrete_hip_pbs_generic": (i32, [vp, u32, vp, vp, vp, vp, vp, vp, vp, u32, u32, u32, u32, u32, u32, vp]),
     "concrete_hip_device_count": (i32, []),
     "concrete_hip_device_status": (i32, [u32]),
     "concrete_hip_set_spin_limit": (None, [u32]),

@@ -117,6 +117,88 @@ int take_device_status(int gpu) {
 }
 
 
+// ---- general-format companion keys (pbs_needs_generic_key) ------------------------------
+// A primary device key in a hand-tuned kernel's format (N = 1024 / 2048) whose standard-domain
+// source the backend can reach — the keyset's host copy, or the `dest` buffer of
+// cuda_convert_lwe_programmable_bootstrap_key_64, which holds the standard key on the device — is
+// registered with that source; the first PBS with digits wider than the hand-tuned kernel accepts
+// converts it once into the general path's format (its companion), kept until the primary goes.
+struct StdSource {
+  const uint64_t* src;
+  bool on_device;
+  uint32_t gpu, n, k, level, N;
+  void* companion;  // general-format key, built on first use
+};
+static std::mutex g_src_mu;
+static std::unordered_map<const void*, StdSource> g_src;
+
+void register_std_source(const void* primary, const uint64_t* src, bool on_device, uint32_t gpu, uint32_t n,
+                         uint32_t k, uint32_t level, uint32_t N) {
+  void* old = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_src_mu);
+    auto it = g_src.find(primary);
+    if (it != g_src.end()) old = it->second.companion;
+    g_src[primary] = StdSource{src, on_device, gpu, n, k, level, N, nullptr};
+  }
+  if (old) CHIP_CHECK(hipFree(old));
+}
+
+void release_std_source(const void* primary) {
+  void* c = nullptr;
+  int gpu = 0;
+  {
+    std::lock_guard<std::mutex> g(g_src_mu);
+    auto it = g_src.find(primary);
+    if (it == g_src.end()) return;
+    c = it->second.companion;
+    gpu = (int)it->second.gpu;
+    g_src.erase(it);
+  }
+  if (c) {
+    int prev = 0;
+    CHIP_CHECK(hipGetDevice(&prev));
+    CHIP_CHECK(hipSetDevice(gpu));
+    CHIP_CHECK(hipFree(c));
+    CHIP_CHECK(hipSetDevice(prev));
+  }
+}
+
+// The companion of `primary` for (n, k, l, N), converted on `s` (and synchronised: published
+// complete, context.h:110-113) on first use; nullptr when the primary has no registered source or
+// other parameters.
+const void* generic_companion_key(const void* primary, uint32_t n, uint32_t k, uint32_t level, uint32_t N,
+                                  hipStream_t s) {
+  std::lock_guard<std::mutex> g(g_src_mu);  // held across the one-time conversion
+  auto it = g_src.find(primary);
+  if (it == g_src.end()) return nullptr;
+  StdSource& e = it->second;
+  if (e.n != n || e.k != k || e.level != level || e.N != N) return nullptr;
+  if (e.companion) return e.companion;
+  const uint64_t bytes = generic_fourier_bsk_bytes(n, k, level, N);
+  if (!bytes) return nullptr;
+  void* d = nullptr;
+  CHIP_CHECK(hipMalloc(&d, bytes));
+  const uint64_t std_bytes = (uint64_t)n * level * (k + 1) * (k + 1) * N * 8ull;
+  const uint64_t* src_dev = e.src;
+  void* tmp = nullptr;
+  if (!e.on_device) {
+    CHIP_CHECK(hipMalloc(&tmp, std_bytes));
+    CHIP_CHECK(hipMemcpyAsync(tmp, e.src, std_bytes, hipMemcpyHostToDevice, s));
+    src_dev = (const uint64_t*)tmp;
+  }
+  ConvertArgs a{s, d, src_dev, n, k, level, N, generic_key_format(k, N, level).limbs};
+  const int rc = convert_bsk_generic_launch(a);
+  CHIP_CHECK(hipStreamSynchronize(s));
+  if (tmp) CHIP_CHECK(hipFree(tmp));
+  if (rc != 0) {
+    CHIP_CHECK(hipFree(d));
+    return nullptr;
+  }
+  e.companion = d;
+  return d;
+}
+
 }  // namespace chip
 
 using namespace chip;
@@ -171,7 +253,10 @@ static void release_registered(void* ptr) {
       g_keys.erase(it);
     }
   }
-  if (f) CHIP_CHECK(hipFree(f));
+  if (f) {
+    release_std_source(f);
+    CHIP_CHECK(hipFree(f));
+  }
 }
 
 void cuda_drop(void* ptr, uint32_t gpu_index) {
@@ -223,7 +308,10 @@ int concrete_hip_device_count(void) {
 
 int concrete_hip_pbs_supported(uint32_t glwe_dim, uint32_t polynomial_size, uint32_t level_count,
                                uint32_t base_log) {
-  return pbs_params_ok(glwe_dim, polynomial_size, level_count, base_log) ? 1 : 0;
+  return pbs_params_ok(glwe_dim, polynomial_size, level_count, base_log) ||
+                 pbs_needs_generic_key(glwe_dim, polynomial_size, level_count, base_log)
+             ? 1
+             : 0;
 }
 
 uint32_t concrete_hip_bsk_limbs(uint32_t polynomial_size, uint32_t level_count, uint32_t base_log) {
@@ -295,12 +383,29 @@ int concrete_hip_pbs(void* stream, uint32_t gpu_index, uint64_t* lwe_array_out, 
     set_error("pbs: lwe_dimension must be > 0");
     return -3;
   }
-  if (!pbs_params_ok(glwe_dimension, polynomial_size, level_count, base_log)) {
+  const bool generic = !pbs_params_ok(glwe_dimension, polynomial_size, level_count, base_log);
+  if (generic && !pbs_needs_generic_key(glwe_dimension, polynomial_size, level_count, base_log)) {
     set_error("pbs: unsupported parameters k=%u N=%u level=%u base_log=%u", glwe_dimension, polynomial_size,
               level_count, base_log);
     return -2;
   }
   set_device(gpu_index);
+  const void* key = fourier_bsk;
+  uint32_t limbs = default_limbs(glwe_dimension, polynomial_size, level_count);
+  if (generic) {
+    // digits wider than the hand-tuned kernel takes: the general path, on this key's companion
+    key = generic_companion_key(fourier_bsk, lwe_dimension, glwe_dimension, level_count, polynomial_size,
+                                (hipStream_t)stream);
+    if (!key) {
+      set_error("pbs: k=%u N=%u level=%u base_log=%u runs on the general path, whose key format this key is not "
+                "in and cannot be derived from (convert it through a keyset or "
+                "cuda_convert_lwe_programmable_bootstrap_key_64, or use concrete_hip_convert_bsk_generic + "
+                "concrete_hip_pbs_generic)",
+                glwe_dimension, polynomial_size, level_count, base_log);
+      return -2;
+    }
+    limbs = generic_key_format(glwe_dimension, polynomial_size, level_count).limbs;
+  }
   PbsArgs a{(hipStream_t)stream,
             lwe_array_out,
             lwe_output_indexes,
@@ -308,17 +413,77 @@ int concrete_hip_pbs(void* stream, uint32_t gpu_index, uint64_t* lwe_array_out, 
             lut_vector_indexes,
             lwe_array_in,
             lwe_input_indexes,
-            fourier_bsk,
+            key,
             lwe_dimension,
             glwe_dimension,
             polynomial_size,
             base_log,
             level_count,
-            default_limbs(glwe_dimension, polynomial_size, level_count),
+            limbs,
             num_samples,
             (unsigned long long*)resid_bits,
             sync_guard((int)gpu_index)};
-  return pbs_launch(a);
+  return generic ? pbs_generic_launch(a) : pbs_launch(a);
+}
+
+uint64_t concrete_hip_generic_bsk_size_bytes(uint32_t input_lwe_dim, uint32_t glwe_dim, uint32_t level_count,
+                                             uint32_t polynomial_size) {
+  return generic_fourier_bsk_bytes(input_lwe_dim, glwe_dim, level_count, polynomial_size);
+}
+
+int concrete_hip_convert_bsk_generic(void* stream, uint32_t gpu_index, void* dest, const void* src, int src_is_device,
+                                     uint32_t input_lwe_dim, uint32_t glwe_dim, uint32_t level_count,
+                                     uint32_t polynomial_size) {
+  if (!dest || !src) {
+    set_error("convert_bsk_generic: null pointer");
+    return -1;
+  }
+  const KeyFormat f = generic_key_format(glwe_dim, polynomial_size, level_count);
+  if (f.kind != KeyKind::GENERIC) {
+    set_error("convert_bsk_generic: k=%u N=%u level=%u is not on the general path", glwe_dim, polynomial_size,
+              level_count);
+    return -2;
+  }
+  set_device(gpu_index);
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t std_bytes =
+      (uint64_t)input_lwe_dim * level_count * (glwe_dim + 1) * (glwe_dim + 1) * polynomial_size * 8ull;
+  const uint64_t* src_dev = (const uint64_t*)src;
+  void* tmp = nullptr;
+  keep_pool_memory();
+  if (!src_is_device) {
+    CHIP_CHECK(hipMallocAsync(&tmp, std_bytes, s));
+    CHIP_CHECK(hipMemcpyAsync(tmp, src, std_bytes, hipMemcpyHostToDevice, s));
+    src_dev = (const uint64_t*)tmp;
+  }
+  ConvertArgs a{s, dest, src_dev, input_lwe_dim, glwe_dim, level_count, polynomial_size, f.limbs};
+  const int rc = convert_bsk_generic_launch(a);
+  if (tmp) CHIP_CHECK(hipFreeAsync(tmp, s));
+  return rc;
+}
+
+int concrete_hip_pbs_generic(void* stream, uint32_t gpu_index, uint64_t* lwe_array_out,
+                             const uint64_t* lwe_output_indexes, const uint64_t* lut_vector,
+                             const uint64_t* lut_vector_indexes, const uint64_t* lwe_array_in,
+                             const uint64_t* lwe_input_indexes, const void* generic_bsk, uint32_t lwe_dimension,
+                             uint32_t glwe_dimension, uint32_t polynomial_size, uint32_t base_log,
+                             uint32_t level_count, uint32_t num_samples, uint64_t* resid_bits) {
+  if (num_samples == 0) return 0;
+  if (!lwe_array_out || !lut_vector || !lwe_array_in || !generic_bsk || lwe_dimension == 0) {
+    set_error("pbs_generic: null pointer or zero dimension");
+    return -1;
+  }
+  if (!generic_pbs_ok(glwe_dimension, polynomial_size, level_count, base_log)) {
+    set_error("pbs_generic: k=%u N=%u level=%u base_log=%u outside the general path's exact range", glwe_dimension,
+              polynomial_size, level_count, base_log);
+    return -2;
+  }
+  set_device(gpu_index);
+  PbsArgs a{(hipStream_t)stream, lwe_array_out, lwe_output_indexes, lut_vector, lut_vector_indexes, lwe_array_in,
+            lwe_input_indexes, generic_bsk, lwe_dimension, glwe_dimension, polynomial_size, base_log, level_count,
+            generic_key_format(glwe_dimension, polynomial_size, level_count).limbs, num_samples,
+            (unsigned long long*)resid_bits, sync_guard((int)gpu_index)};
+  return pbs_generic_launch(a);
 }
 
 int concrete_hip_keyswitch(void* stream, uint32_t gpu_index, uint64_t* lwe_array_out,
@@ -370,8 +535,13 @@ void cuda_convert_lwe_programmable_bootstrap_key_64(void* stream, uint32_t gpu_i
   }
   if (old) {
     CHIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    release_std_source(old);
     CHIP_CHECK(hipFree(old));
   }
+  // dest keeps the standard key: the source of a general-format companion for wide-digit calls
+  if (key_format(glwe_dim, polynomial_size, level_count).kind != KeyKind::GENERIC)
+    register_std_source(f, (const uint64_t*)dest, true, gpu_index, input_lwe_dim, glwe_dim, level_count,
+                        polynomial_size);
 }
 
 void scratch_cuda_programmable_bootstrap_64(void* stream, uint32_t gpu_index, int8_t** pbs_buffer,

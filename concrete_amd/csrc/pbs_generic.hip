@@ -89,9 +89,7 @@ uint32_t generic_limb_bits(uint32_t k, uint32_t N, uint32_t level) {
   return 0;
 }
 
-KeyFormat key_format(uint32_t k, uint32_t N, uint32_t level) {
-  if (k == 1 && N == 1024 && level >= 1 && level <= 3) return {KeyKind::N1024, 3, 22};
-  if (k == 1 && N == 2048 && level == 1) return {KeyKind::N2048, (uint32_t)PBS2_LIMBS, 16};
+KeyFormat generic_key_format(uint32_t k, uint32_t N, uint32_t level) {
   if (generic_shape_ok(k, N, level)) {
     const uint32_t b = generic_limb_bits(k, N, level);
     const uint32_t L = b ? (64 + b - 1) / b : 0;
@@ -100,8 +98,16 @@ KeyFormat key_format(uint32_t k, uint32_t N, uint32_t level) {
   return {KeyKind::NONE, 0, 0};
 }
 
+KeyFormat key_format(uint32_t k, uint32_t N, uint32_t level) {
+  if (k == 1 && N == 1024 && level >= 1 && level <= 3) return {KeyKind::N1024, 3, 22};
+  if (k == 1 && N == 2048 && level == 1) return {KeyKind::N2048, (uint32_t)PBS2_LIMBS, 16};
+  return generic_key_format(k, N, level);
+}
+
+// The general path's own gate, for its key format (also for the shapes whose primary key is a
+// hand-tuned kernel's: their wide-digit PBS runs here on a companion key, pbs_needs_generic_key).
 bool generic_pbs_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
-  const KeyFormat f = key_format(k, N, level);
+  const KeyFormat f = generic_key_format(k, N, level);
   if (f.kind != KeyKind::GENERIC || base_log < 1 || (uint64_t)level * base_log > 64) return false;
   const uint32_t T = (base_log + f.bits - 1) / f.bits;
   if ((k + 1) * level * T > (uint32_t)GEN_MAX_TERMS) return false;
@@ -1680,7 +1686,7 @@ static bool tile_dispatch(uint32_t N, uint32_t K1, uint32_t KL, uint32_t T, uint
 }  // namespace gen
 
 uint64_t generic_scratch_bytes_per_sample(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
-  const KeyFormat f = key_format(k, N, level);
+  const KeyFormat f = generic_key_format(k, N, level);
   if (f.kind != KeyKind::GENERIC) return 0;
   const uint64_t K1 = k + 1, M = N / 2, T = (base_log + f.bits - 1) / f.bits;
   return K1 * level * T * M * 16 + K1 * f.limbs * M * 16 + K1 * N * 8;
@@ -1710,7 +1716,7 @@ int pbs_generic_launch(const PbsArgs& a) {
               a.base_log);
     return -2;
   }
-  const KeyFormat fmt = key_format(a.k, a.N, a.level);
+  const KeyFormat fmt = generic_key_format(a.k, a.N, a.level);
   const uint32_t K1 = a.k + 1, M = a.N / 2, L = fmt.limbs, b = fmt.bits;
   const uint32_t T = (a.base_log + b - 1) / b;
   const Tables tb = tables_for(a.N);
@@ -1824,7 +1830,7 @@ int pbs_generic_launch(const PbsArgs& a) {
 
 int convert_bsk_generic_launch(const ConvertArgs& a) {
   using namespace gen;
-  const KeyFormat fmt = key_format(a.k, a.N, a.level);
+  const KeyFormat fmt = generic_key_format(a.k, a.N, a.level);
   if (fmt.kind != KeyKind::GENERIC) {
     set_error("generic BSK conversion: unsupported k=%u N=%u level=%u", a.k, a.N, a.level);
     return -2;

@@ -90,6 +90,9 @@ void* keyset_bsk_on(concrete_hip_keyset* ks, uint32_t idx, uint32_t gpu, hipStre
   }
   // publication only after the key is complete (context.h:110-113)
   CHIP_CHECK(hipStreamSynchronize(s));
+  // the host copy is the source of a general-format companion for wide-digit calls
+  if (key_format(e->k, e->N, e->level).kind != KeyKind::GENERIC)
+    register_std_source(d, e->host.data(), false, gpu, e->n, e->k, e->level, e->N);
   e->dev[gpu] = d;
   return d;
 }
@@ -332,6 +335,7 @@ void free_keys(concrete_hip_keyset* ks) {
     for (int d = 0; d < RT_MAX_DEV; ++d)
       if (e->dev[d]) {
         CHIP_CHECK(hipSetDevice(d));
+        release_std_source(e->dev[d]);  // and its general-format companion, if one was built
         CHIP_CHECK(hipFree(e->dev[d]));
       }
     delete e;

@@ -111,7 +111,7 @@ void cuda_negate_lwe_ciphertext_vector_64(void *stream, uint32_t gpu_index, void
 uint32_t concrete_hip_abi_version(void);
 /* thread-local message of the last failed concrete_hip_* call */
 const char *concrete_hip_last_error(void);
-/* 1 if (k, N, level, base_log) has a compiled PBS kernel, else 0 */
+/* 1 if (k, N, level, base_log) has a compiled PBS kernel (wide digits: the general path), else 0 */
 int concrete_hip_pbs_supported(uint32_t glwe_dim, uint32_t polynomial_size, uint32_t level_count,
                                uint32_t base_log);
 /* number of exact key limbs the device format uses for these parameters */
@@ -133,6 +133,23 @@ uint64_t concrete_hip_fourier_bsk_size_bytes(uint32_t input_lwe_dim, uint32_t gl
 int concrete_hip_convert_bsk(void *stream, uint32_t gpu_index, void *dest_fourier, const void *src,
                              int src_is_device, uint32_t input_lwe_dim, uint32_t glwe_dim, uint32_t level_count,
                              uint32_t polynomial_size);
+/* Wide digits.  A (k, N, l) with a hand-tuned kernel (k = 1, N = 1024 / 2048) accepts only digits
+ * that kernel keeps exact (N = 1024: (k+1) l 2^logB <= 4096; N = 2048: logB <= 24); wider ones run
+ * on the general path (pbs_generic.hip), which needs the key in its own format.  Keys converted
+ * through a keyset or cuda_convert_lwe_programmable_bootstrap_key_64 get that companion built from
+ * their standard key on first use (concrete_hip_pbs, the memref / stream-emulator routes); a
+ * caller holding its own key converts it with these two and calls concrete_hip_pbs_generic. */
+uint64_t concrete_hip_generic_bsk_size_bytes(uint32_t input_lwe_dim, uint32_t glwe_dim, uint32_t level_count,
+                                             uint32_t polynomial_size);
+int concrete_hip_convert_bsk_generic(void *stream, uint32_t gpu_index, void *dest, const void *src,
+                                     int src_is_device, uint32_t input_lwe_dim, uint32_t glwe_dim,
+                                     uint32_t level_count, uint32_t polynomial_size);
+int concrete_hip_pbs_generic(void *stream, uint32_t gpu_index, uint64_t *lwe_array_out,
+                             const uint64_t *lwe_output_indexes, const uint64_t *lut_vector,
+                             const uint64_t *lut_vector_indexes, const uint64_t *lwe_array_in,
+                             const uint64_t *lwe_input_indexes, const void *generic_bsk, uint32_t lwe_dimension,
+                             uint32_t glwe_dimension, uint32_t polynomial_size, uint32_t base_log,
+                             uint32_t level_count, uint32_t num_samples, uint64_t *resid_bits);
 /* batched PBS on a caller-owned Fourier key (no registry lookup); index arrays may be NULL
  * (identity for in/out, LUT 0 for lut).  resid_bits: optional device u64 receiving the f64
  * bits of max |x - round(x)| seen in the exact recombination (diagnostics; slower kernel). */

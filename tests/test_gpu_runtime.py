@@ -295,3 +295,75 @@ def test_keyset_from_wire_format(env, layout):
     assert np.array_equal(small, O.keyswitch_batch(env["op"], big, env["ksk"]))
     dec = B.lwe_decrypt(env["glwe_sk"], out, p.big_n)
     assert [B.decode(d, width) for d in dec] == [int(table[table[m]]) for m in msgs]
+
+
+@pytest.mark.parametrize("level,base_log", [(1, 15), (2, 12), (1, 23)])
+def test_wide_digits_on_the_general_path(env, level, base_log):
+    """k = 1, N = 1024 with digits wider than the pair kernel's exactness gate ((k+1) l 2^logB <=
+    4096): the general path runs them on a general-format companion of the key, built from the
+    standard key the keyset holds (memref route) or that the legacy conversion left in `dest`
+    (cuda_* route), and on a caller-converted key (concrete_hip_pbs_generic); bit-exact vs the
+    oracle's pure-integer Karatsuba PBS (these sets were refused)."""
+    import ctypes as C
+    from concrete_amd import _native
+    B, R, O = env["B"], env["R"], env["O"]
+    L = _native.lib()
+    p = replace(B.CFG2, n=12, level=level, base_log=base_log)
+    assert L.concrete_hip_pbs_supported(p.k, p.N, p.level, p.base_log) == 1
+    lwe_sk = B.binary_key(p.n, 81)
+    glwe_sk = B.binary_key(p.big_n, 82)
+    bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 83)
+    width = 3
+    table = np.array([4, 1, 6, 3, 0, 7, 2, 5], dtype=np.uint64)
+    tlu = B.expand_lut(table, p.N, width)
+    acc = B.trivial_glwe(p, tlu)
+    rng = np.random.RandomState(level * 100 + base_log)
+    msgs = rng.randint(0, 1 << width, size=9)
+    cts = B.lwe_encrypt(lwe_sk, [B.encode(m, width) for m in msgs], p.n, 2.0 ** -25, 84)
+    op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
+    ref, _ = O.pbs_batch(op, cts, acc[None, :], bsk=bsk, mode=O.MODE_KARATSUBA)
+    dec = B.lwe_decrypt(glwe_sk, ref, p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+    # memref route: keyset on [0, 0] (two slices)
+    ks = R.Keyset([0, 0])
+    ks.add_bsk(0, bsk, p)
+    got = R.batched_bootstrap(ks, p, cts, tlu)
+    again = R.batched_bootstrap(ks, p, cts, tlu)  # companion already built
+    ks.close()
+    assert np.array_equal(got, ref) and np.array_equal(again, ref)
+    # cuda_* route: the registry's conversion, then the runtime's PBS call
+    s = L.cuda_create_stream(0)
+    d_bsk = L.cuda_malloc_async(bsk.nbytes, s, 0)
+    L.cuda_convert_lwe_programmable_bootstrap_key_64(s, 0, d_bsk, bsk.ctypes.data, p.n, p.k, p.level, p.N)
+    nb = len(msgs)
+    d_in = L.cuda_malloc_async(cts.nbytes, s, 0)
+    L.cuda_memcpy_async_to_gpu(d_in, cts.ctypes.data, cts.nbytes, s, 0)
+    d_out = L.cuda_malloc_async(nb * (p.k * p.N + 1) * 8, s, 0)
+    d_acc = L.cuda_malloc_async(acc.nbytes, s, 0)
+    L.cuda_memcpy_async_to_gpu(d_acc, acc.ctypes.data, acc.nbytes, s, 0)
+    idx = np.arange(nb, dtype=np.uint64)
+    zeros = np.zeros(nb, dtype=np.uint64)
+    d_idx = L.cuda_malloc_async(idx.nbytes, s, 0)
+    d_lidx = L.cuda_malloc_async(idx.nbytes, s, 0)
+    L.cuda_memcpy_async_to_gpu(d_idx, idx.ctypes.data, idx.nbytes, s, 0)
+    L.cuda_memcpy_async_to_gpu(d_lidx, zeros.ctypes.data, zeros.nbytes, s, 0)
+    L.cuda_programmable_bootstrap_lwe_ciphertext_vector_64(s, 0, d_out, d_idx, d_acc, d_lidx, d_in, d_idx, d_bsk,
+                                                          None, p.n, p.k, p.N, p.base_log, p.level, nb, 1, 1)
+    out = np.zeros((nb, p.k * p.N + 1), dtype=np.uint64)
+    L.cuda_memcpy_async_to_cpu(out.ctypes.data, d_out, out.nbytes, s, 0)
+    L.cuda_synchronize_device(0)
+    # caller-held key in the general format: concrete_hip_pbs_generic
+    gbytes = L.concrete_hip_generic_bsk_size_bytes(p.n, p.k, p.level, p.N)
+    d_g = L.cuda_malloc_async(gbytes, s, 0)
+    _native.check(L.concrete_hip_convert_bsk_generic(s, 0, d_g, bsk.ctypes.data, 0, p.n, p.k, p.level, p.N),
+                  "convert_bsk_generic")
+    _native.check(L.concrete_hip_pbs_generic(s, 0, d_out, None, d_acc, None, d_in, None, d_g, p.n, p.k, p.N,
+                                             p.base_log, p.level, nb, None), "pbs_generic")
+    out2 = np.zeros_like(out)
+    L.cuda_memcpy_async_to_cpu(out2.ctypes.data, d_out, out2.nbytes, s, 0)
+    L.cuda_synchronize_device(0)
+    for ptr in (d_in, d_out, d_acc, d_idx, d_lidx, d_g):
+        L.cuda_drop_async(ptr, s, 0)
+    L.cuda_drop(d_bsk, 0)
+    L.cuda_destroy_stream(s, 0)
+    assert np.array_equal(out, ref) and np.array_equal(out2, ref)

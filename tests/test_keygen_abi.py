@@ -25,12 +25,15 @@ def test_abi_version_and_queries():
     assert L.concrete_hip_abi_version() == 2
     assert L.concrete_hip_pbs_supported(1, 1024, 3, 7) == 1
     assert L.concrete_hip_pbs_supported(1, 1024, 3, 30) == 0  # l * logB >= 64
-    # the exactness gate: (k+1) l 2^logB <= 4096 (3-limb rounding bound < 1/4)
+    # the pair kernel's exactness gate is (k+1) l 2^logB <= 4096 (3-limb rounding bound < 1/4);
+    # wider digits run on the general path (a general-format companion key) while its bound holds
     assert L.concrete_hip_pbs_supported(1, 1024, 3, 9) == 1
-    assert L.concrete_hip_pbs_supported(1, 1024, 3, 10) == 0
+    assert L.concrete_hip_pbs_supported(1, 1024, 3, 10) == 1
     assert L.concrete_hip_pbs_supported(1, 1024, 2, 10) == 1
     assert L.concrete_hip_pbs_supported(1, 1024, 1, 11) == 1
-    assert L.concrete_hip_pbs_supported(1, 1024, 1, 15) == 0
+    assert L.concrete_hip_pbs_supported(1, 1024, 1, 15) == 1
+    assert L.concrete_hip_pbs_supported(1, 1024, 1, 23) == 1
+    assert L.concrete_hip_pbs_supported(1, 1024, 2, 33) == 0  # l * logB > 64
     assert L.concrete_hip_pbs_supported(2, 1024, 3, 7) == 1  # k = 2: the general path
     assert L.concrete_hip_pbs_supported(1, 32768, 1, 7) == 0
     assert L.concrete_hip_bsk_limbs(1024, 3, 7) == 3
@@ -99,7 +102,10 @@ def test_key_formats_and_exact_range():
     # cfg4 key: 4 limbs of g only (the digit is split on the limb grid, pbs2048.hip)
     assert L.concrete_hip_fourier_bsk_size_bytes(742, 1, 1, 2048) == 742 * 4 * 4 * 1024 * 16
     assert L.concrete_hip_pbs_supported(1, 2048, 1, 24) == 1
-    assert L.concrete_hip_pbs_supported(1, 2048, 1, 25) == 0
+    assert L.concrete_hip_pbs_supported(1, 2048, 1, 25) == 1  # past the cfg4 kernel: the general path
+    # the general-format key of the hand-tuned shapes (wide digits): its own limbs
+    assert L.concrete_hip_generic_bsk_size_bytes(10, 1, 1, 2048) > 0
+    assert L.concrete_hip_generic_bsk_size_bytes(10, 1, 1, 32768) == 0
     for k, N, l, logB in [(5, 256, 1, 15), (6, 256, 1, 18), (3, 512, 1, 18), (2, 1024, 1, 23), (1, 4096, 1, 22),
                           (1, 8192, 1, 22), (1, 16384, 2, 15), (1, 2048, 2, 10)]:
         kind, limbs, bits = fmt(k, N, l)

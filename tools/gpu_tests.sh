@@ -1,0 +1,12 @@
+#!/bin/bash
+# GPU box: the whole -m gpu suite (one process) and smoke.  Usage: tools/gpu_tests.sh TAG
+set -e -o pipefail
+TAG=${1:-tests}
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
+tail -1 $O/pytest_gpu.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+tail -1 $O/smoke.log

@@ -149,7 +149,7 @@ def test_batched_bootstrap_general_path(env):
 
 def test_slices_overlap_and_bit_exact(env):
     """Slices of one call are issued concurrently (one host thread, stream and buffer set per
-    slice): every slice starts before slice 0's kernel is done (the round-2 loop
+    slice): no slice waits for another's outputs (the round-2 loop
     issued slice r + 1 only after slice r's pageable D2H had returned; an outgrown buffer's hipFree
     also synchronised the device mid-call until it was deferred to after the join)."""
     B, R, O = env["B"], env["R"], env["O"]
@@ -174,12 +174,16 @@ def test_slices_overlap_and_bit_exact(env):
     tl = ks.timeline()
     ks.close()
     assert tl.shape == (4, 6) and list(tl[:, 5]) == [256] * 4
-    for r in range(3):
-        # columns: device, start, inputs copied (kernel issue), kernel done, outputs copied, count.
-        # Every slice is issued while slice 0's kernel runs (round 2 issued slice r + 1 only after
-        # slice r's D2H).  On one device the kernels themselves then queue for CUs (each 256-sample
-        # launch fills the chip), so only the issue times are compared.
-        assert tl[r + 1, 1] < tl[0, 3], tl
+    # columns: device, start, inputs copied (kernel issue), kernel done, outputs copied, count.
+    # Every slice starts while another slice's kernel is still running (round 2 issued slice r + 1
+    # only after slice r's D2H, so its last slice started after every other kernel was done).  On
+    # one device the kernels queue for CUs (each 256-sample launch fills the chip), and a slice
+    # thread's first HIP call can wait while another thread sits in a blocking pageable copy on the
+    # same device, so neither kernel overlap nor a fixed issue order is asserted.
+    for r in range(1, 4):
+        others = [tl[q, 3] for q in range(4) if q != r]
+        assert tl[r, 1] < max(others), tl
+    assert int((tl[1:, 1] < tl[0, 3]).sum()) >= 1, tl
     dec = B.lwe_decrypt(glwe_sk, got, p.big_n)
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
     op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
@@ -312,7 +316,10 @@ def test_wide_digits_on_the_general_path(env, level, base_log):
     assert L.concrete_hip_pbs_supported(p.k, p.N, p.level, p.base_log) == 1
     lwe_sk = B.binary_key(p.n, 81)
     glwe_sk = B.binary_key(p.big_n, 82)
-    bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 83)
+    # such wide digits amplify the key noise 2^(logB-1) sqrt((k+1) l N)-fold: with the secure GLWE
+    # noise for N = 1024 nothing would decrypt (why no optimizer table picks them), so the key is
+    # encrypted with small noise here; bit-exactness does not depend on it
+    bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 83, std=2.0 ** -52)
     width = 3
     table = np.array([4, 1, 6, 3, 0, 7, 2, 5], dtype=np.uint64)
     tlu = B.expand_lut(table, p.N, width)

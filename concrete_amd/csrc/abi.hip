@@ -12,6 +12,7 @@
 #include "../../include/concrete_hip.h"
 #include "common.hpp"
 #include "pbs.hpp"
+#include "companion.hpp"
 
 namespace chip {
 

@@ -1,0 +1,40 @@
+// companion.hpp — general-format companion keys (host side of libconcrete_hip).
+//
+// A PBS whose digits are wider than the hand-tuned kernel of its (k, N, l) accepts (N = 1024: the
+// gate (k+1) l 2^logB <= 4096, pbs.hpp pbs1024_exact; N = 2048: logB <= 24) but which the general
+// path (pbs_generic.hip) runs exactly runs there, on a companion key in the general format built
+// from the standard key (abi.hip generic_companion_key; concrete_hip_pbs_generic for caller-held
+// keys).  Kept apart from pbs.hpp, whose contents are the kernels' geometry.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pbs.hpp"
+
+namespace chip {
+
+KeyFormat generic_key_format(uint32_t k, uint32_t N, uint32_t level);  // pbs_generic.hip: any shape it runs
+
+inline bool pbs_needs_generic_key(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
+  const KeyFormat f = key_format(k, N, level);
+  if (f.kind == KeyKind::N1024 && !pbs1024_exact(k, level, base_log)) return generic_pbs_ok(k, N, level, base_log);
+  if (f.kind == KeyKind::N2048 && !(base_log >= 1 && base_log <= PBS2_MAX_LOGB))
+    return generic_pbs_ok(k, N, level, base_log);
+  return false;
+}
+
+// Size in bytes of a general-format key ([n][col][limb][row][q][N/2] complex f64).
+inline uint64_t generic_fourier_bsk_bytes(uint32_t n, uint32_t k, uint32_t level, uint32_t N) {
+  const KeyFormat f = generic_key_format(k, N, level);
+  return f.kind == KeyKind::GENERIC ? (uint64_t)n * level * (k + 1) * (k + 1) * f.limbs * (N / 2) * 16ull : 0;
+}
+
+// abi.hip: companions of hand-tuned-format keys.  `src` is the standard key (host or device
+// memory) and must outlive the registration.
+void register_std_source(const void* primary, const uint64_t* src, bool on_device, uint32_t gpu, uint32_t n,
+                         uint32_t k, uint32_t level, uint32_t N);
+void release_std_source(const void* primary);
+const void* generic_companion_key(const void* primary, uint32_t n, uint32_t k, uint32_t level, uint32_t N,
+                                  hipStream_t s);
+
+}  // namespace chip

@@ -55,7 +55,6 @@ constexpr int GEN_MAX_K = 8;       // GLWE dimension
 constexpr int GEN_MAX_LIMBS = 8;   // key limbs
 constexpr int GEN_MAX_TERMS = 24; // (k+1) * l * sub-digits per slot product
 KeyFormat key_format(uint32_t k, uint32_t N, uint32_t level);                              // pbs_generic.hip
-KeyFormat generic_key_format(uint32_t k, uint32_t N, uint32_t level);  // the general path's format, any shape it runs
 bool generic_pbs_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log);            // pbs_generic.hip
 uint32_t generic_limb_bits(uint32_t k, uint32_t N, uint32_t level);                        // pbs_generic.hip
 double generic_error_bound(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log, uint32_t bits,
@@ -84,24 +83,6 @@ inline bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_
     case KeyKind::GENERIC: return generic_pbs_ok(k, N, level, base_log);
     default: return false;
   }
-}
-
-// A PBS whose digits are wider than the hand-tuned kernel of its (k, N, l) accepts (N = 1024: the
-// gate (k+1) l 2^logB <= 4096; N = 2048: logB <= 24) but which the general path runs exactly: it
-// runs there, on a companion key in the general format built from the standard key
-// (abi.hip generic_companion_key; concrete_hip_pbs_generic for caller-held keys).
-inline bool pbs_needs_generic_key(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
-  const KeyFormat f = key_format(k, N, level);
-  if (f.kind == KeyKind::N1024 && !pbs1024_exact(k, level, base_log)) return generic_pbs_ok(k, N, level, base_log);
-  if (f.kind == KeyKind::N2048 && !(base_log >= 1 && base_log <= PBS2_MAX_LOGB))
-    return generic_pbs_ok(k, N, level, base_log);
-  return false;
-}
-
-// Size in bytes of a general-format key ([n][col][limb][row][q][N/2] complex f64).
-inline uint64_t generic_fourier_bsk_bytes(uint32_t n, uint32_t k, uint32_t level, uint32_t N) {
-  const KeyFormat f = generic_key_format(k, N, level);
-  return f.kind == KeyKind::GENERIC ? (uint64_t)n * level * (k + 1) * (k + 1) * f.limbs * (N / 2) * 16ull : 0;
 }
 
 // Size in bytes of the device Fourier bootstrapping key.
@@ -133,13 +114,6 @@ struct PbsArgs {
 };
 
 int pbs_launch(const PbsArgs& a);
-// abi.hip: general-format companions of hand-tuned-format keys (pbs_needs_generic_key).  `src` is
-// the standard key (host or device memory) and must outlive the registration.
-void register_std_source(const void* primary, const uint64_t* src, bool on_device, uint32_t gpu, uint32_t n,
-                         uint32_t k, uint32_t level, uint32_t N);
-void release_std_source(const void* primary);
-const void* generic_companion_key(const void* primary, uint32_t n, uint32_t k, uint32_t level, uint32_t N,
-                                  hipStream_t s);
 int pbs2048_launch(const PbsArgs& a);         // pbs2048.hip
 int pbs_generic_launch(const PbsArgs& a);     // pbs_generic.hip
 

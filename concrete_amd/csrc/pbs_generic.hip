@@ -36,6 +36,7 @@
 #include "fft512.hpp"
 #include "kernel_util.hpp"
 #include "pbs.hpp"
+#include "companion.hpp"
 
 namespace chip {
 

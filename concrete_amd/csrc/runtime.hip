@@ -29,6 +29,7 @@
 
 #include "common.hpp"
 #include "pbs.hpp"
+#include "companion.hpp"
 #include "runtime.hpp"
 
 namespace chip {

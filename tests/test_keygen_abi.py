@@ -116,3 +116,15 @@ def test_key_formats_and_exact_range():
     assert fmt(1, 32768, 2)[0] == 0
     assert L.concrete_hip_pbs_supported(1, 32768, 2, 15) == 0
     assert L.concrete_hip_pbs_supported(1, 4096, 1, 40) == 0
+
+
+def test_committed_pmc_records_match_the_kernel_sources():
+    """bench.py reports roofline.traffic / dram / valu only from a PMC record measured on the
+    current kernel sources (bench.KERNEL_SOURCES, hashed per config): a kernel edit without a new
+    record would silently drop those fields from the round's bench line."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    for config in ("cfg2", "cfg4"):
+        assert bench.pmc_traffic(4096, config)[0], f"no PMC traffic record for the current {config} sources"
+        assert bench.pmc_f64_flop(4096, config)[0], f"no PMC f64 record for the current {config} sources"

@@ -2,6 +2,7 @@
 declares, its host-side client helpers agree bit-for-bit with the oracle, and its
 status-returning entry points reject bad arguments before touching a device."""
 import ctypes as C
+import os
 
 import numpy as np
 import pytest

@@ -407,6 +407,101 @@ __global__ void __launch_bounds__(512) ks_mfma_lds_kernel(uint64_t* __restrict__
   }
 }
 
+// Four-wave form of the LDS-staged kernel (same stages, same operand layout): each wave covers 64
+// samples (two 32-row tiles) x 32 words, so every key-chunk fragment it reads from LDS serves two
+// MFMAs (16 per 32-k step from 10 fragment reads, against 8 from 9 in the eight-wave form): LDS
+// reads per MFMA fall from 1.125 to 0.625 fragments, for one wave per SIMD whose 256 accumulator
+// registers (AGPRs) leave room for the next step's fragments (read ahead of the MFMAs).
+constexpr int KSL4_PPW = KSL_PIECES / 4;  // 10 DMA pieces per wave per stage
+__global__ void __launch_bounds__(256) ks_mfma_lds4_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx,
+                                                         const uint64_t* __restrict__ in,
+                                                         const uint64_t* __restrict__ in_idx, const int8_t* __restrict__ A,
+                                                         const int8_t* __restrict__ Bt, uint32_t n_in, uint32_t n_out,
+                                                         uint32_t num_samples, uint32_t NP, uint32_t Kp,
+                                                         uint32_t Ks, uint32_t k_per_split) {
+  extern __shared__ __attribute__((aligned(16))) v4i lds[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int rh = w >> 1, ch = w & 1;  // rows 64 rh .. + 63 (two 32-row tiles), words 32 ch .. + 31
+  const uint32_t row_base = blockIdx.y * KSL_ROWS, col_base = blockIdx.x * KSL_COLS;
+  const uint32_t k_begin = blockIdx.z * k_per_split, k_end = min(Kp, k_begin + k_per_split);
+  const uint32_t nst = (k_end - k_begin) / KSL_KB;
+  const bool split = gridDim.z > 1;
+  const uint64_t cstride = (uint64_t)NP * Ks;
+  const int8_t* src[KSL4_PPW];
+  int dst[KSL4_PPW];
+#pragma unroll
+  for (int q = 0; q < KSL4_PPW; ++q) {
+    const int p = w * KSL4_PPW + q;
+    if (p < 8) {  // A: kc = p >> 1, rows 64 (p & 1) .. + 63
+      const int kc = p >> 1, r2 = p & 1;
+      src[q] = A + (uint64_t)(row_base + 64 * r2 + lane) * Ks + 16 * kc;
+      dst[q] = kc * KSL_ROWS + 64 * r2;
+    } else {  // B: c, kc
+      const int pb = p - 8, c = pb >> 2, kc = pb & 3;
+      src[q] = Bt + c * cstride + (uint64_t)(col_base + lane) * Ks + 16 * kc;
+      dst[q] = KSL_A_CELLS + (c * 4 + kc) * KSL_COLS;
+    }
+  }
+  auto issue = [&](uint32_t t) __attribute__((always_inline)) {
+    const uint32_t kb = k_begin + t * KSL_KB;
+    v4i* stage = lds + (t % KSL_RS) * KSL_STAGE_CELLS;
+#pragma unroll
+    for (int q = 0; q < KSL4_PPW; ++q)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[q] + kb), (lds_ptr_t)(stage + dst[q]), 16, 0, 0);
+  };
+  v16i acc[2][8];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][c][r] = 0;
+  if (nst > 0) issue(0);
+  if (nst > 1) issue(1);
+  const int r32 = lane & 31, h = lane >> 5;
+  for (uint32_t t = 0; t < nst; ++t) {
+    if (t + 1 < nst) wait_vmcnt<KSL4_PPW>();
+    else wait_vmcnt<0>();
+    pair_barrier();
+    if (t + 2 < nst) issue(t + 2);
+    const v4i* stage = lds + (t % KSL_RS) * KSL_STAGE_CELLS;
+    v4i av[2][2], bv[2][8];
+#pragma unroll
+    for (int s4 = 0; s4 < KSL_KB / 32; ++s4) {
+      const int kc = 2 * s4 + h;
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) av[s4][rt] = stage[kc * KSL_ROWS + 64 * rh + 32 * rt + r32];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) bv[s4][c] = stage[KSL_A_CELLS + (c * 4 + kc) * KSL_COLS + 32 * ch + r32];
+    }
+#pragma unroll
+    for (int s4 = 0; s4 < KSL_KB / 32; ++s4)
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+          acc[rt][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[s4][rt], bv[s4][c], acc[rt][c], 0, 0, 0);
+  }
+  const uint32_t W = n_out + 1;
+  const uint32_t j = col_base + 32 * ch + r32;
+  if (j >= W) return;
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t b = row_base + 64 * rh + 32 * rt + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (b >= num_samples) continue;
+      uint64_t sum = 0ull;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) sum += (uint64_t)(int64_t)acc[rt][c][r] << (8 * c);
+      uint64_t v = 0ull - sum;
+      if (j == n_out && blockIdx.z == 0) v += in[(in_idx ? in_idx[b] : b) * (uint64_t)(n_in + 1) + n_in];
+      uint64_t* o = out + (out_idx ? out_idx[b] : b) * (uint64_t)W + j;
+      if (split) atomicAdd((unsigned long long*)o, (unsigned long long)v);
+      else *o = v;
+    }
+}
+
 // Whether the MFMA path is exact for these parameters (int8 digits, int32 sums): a sum has K =
 // n_in l products of |d| <= 2^(logB-1) and |k_c| <= 128 (the zero padding adds nothing).
 static bool ks_mfma_ok(const KsArgs& a) {
@@ -540,8 +635,11 @@ static int keyswitch_mfma_launch(const KsArgs& a) {
   // serves every batch size
   const uint32_t Ks = (kb + 7) * KSM_KB;
   static_assert(KSL_ROWS == KSM_ROWS && KSL_COLS == KSM_COLS && KSL_KB == KSM_KB, "one padding for both kernels");
-  if (KS_LDS) CHIP_CHECK(hipFuncSetAttribute((const void*)ks_mfma_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)KSL_LDS));
+  // CONCRETE_HIP_KS_WAVES=4: the four-wave LDS kernel (A/B), read per call
+  const char* kw = getenv("CONCRETE_HIP_KS_WAVES");
+  const bool four = KS_LDS && kw && atoi(kw) == 4;
+  if (KS_LDS) CHIP_CHECK(hipFuncSetAttribute(four ? (const void*)ks_mfma_lds4_kernel : (const void*)ks_mfma_lds_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)KSL_LDS));
   keep_pool_memory();
   // test hook: refuse operand scratch above this many bytes (the VALU fallback then runs)
   if (const char* lim = getenv("CONCRETE_HIP_KS_SCRATCH_LIMIT"))
@@ -572,7 +670,10 @@ static int keyswitch_mfma_launch(const KsArgs& a) {
       hipLaunchKernelGGL(keyswitch_zero_kernel, dim3((uint32_t)std::min<uint64_t>((total + 255) / 256, 4096)),
                          dim3(256), 0, a.stream, out, out_idx, W, cn);
     }
-    if (KS_LDS)
+    if (four)
+      hipLaunchKernelGGL(ks_mfma_lds4_kernel, dim3(NP / KSL_COLS, Bp / KSL_ROWS, splits), dim3(256), KSL_LDS, a.stream,
+                         out, out_idx, in, in_idx, A, Bt, a.n_in, a.n_out, cn, NP, Kp, Ks, k_per_split);
+    else if (KS_LDS)
       hipLaunchKernelGGL(ks_mfma_lds_kernel, dim3(NP / KSL_COLS, Bp / KSL_ROWS, splits), dim3(512), KSL_LDS, a.stream,
                          out, out_idx, in, in_idx, A, Bt, a.n_in, a.n_out, cn, NP, Kp, Ks, k_per_split);
     else

@@ -554,3 +554,32 @@ def test_keyswitch_wide_output_rows(B, oracle, torch_cuda, n_out, ks_l, ks_logB,
     torch_cuda.cuda.synchronize()
     op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, ks_l=ks_l, ks_logB=ks_logB)
     assert np.array_equal(B.to_host(out), oracle.keyswitch_batch(op, cts, ksk))
+
+
+@pytest.mark.parametrize("ks_l,ks_logB,nb", [(4, 3, 4096), (4, 3, 300), (7, 3, 129), (2, 7, 70)])
+def test_keyswitch_mfma_four_wave_kernel(B, oracle, torch_cuda, monkeypatch, ks_l, ks_logB, nb):
+    """The four-wave LDS matrix-core keyswitch (CONCRETE_HIP_KS_WAVES=4: two 32-row tiles per wave,
+    each key fragment serving two MFMAs): bit-exact vs the oracle at the cfg2 batch (split-K
+    over 4 workgroups), ragged batches, the widest digits, and permuted index arrays."""
+    monkeypatch.setenv("CONCRETE_HIP_KS_WAVES", "4")
+    p = replace(B.CFG2, ks_level=ks_l, ks_base_log=ks_logB)
+    glwe_sk = B.binary_key(p.big_n, 9400 + ks_logB + ks_l)
+    lwe_sk = B.binary_key(p.n, 9500 + ks_logB + ks_l)
+    ksk = B.ksk_generate(p, glwe_sk, lwe_sk, 9600 + ks_logB + ks_l)
+    rng = np.random.RandomState(nb + 7)
+    cts = rng.randint(0, 2 ** 63, size=(nb, p.big_n + 1), dtype=np.int64).astype(np.uint64) * np.uint64(2) + \
+        np.uint64(1)
+    dev = "cuda:0"
+    d_ksk = B.to_device(ksk, dev)
+    op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, ks_l=ks_l, ks_logB=ks_logB)
+    rows = np.arange(nb) if nb <= 300 else np.r_[0:64, nb - 64:nb]
+    ref = oracle.keyswitch_batch(op, cts[rows], ksk)
+    out = B.keyswitch(p, d_ksk, B.to_device(cts, dev))
+    torch_cuda.cuda.synchronize()
+    assert np.array_equal(B.to_host(out)[rows], ref)
+    in_idx = rng.permutation(nb).astype(np.uint64)
+    out2 = B.keyswitch(p, d_ksk, B.to_device(cts, dev), in_idx=B.to_device(in_idx, dev))
+    torch_cuda.cuda.synchronize()
+    sel = rows[: min(len(rows), 64)]
+    exp = oracle.keyswitch_batch(op, cts[in_idx[sel].astype(np.int64)], ksk)
+    assert np.array_equal(B.to_host(out2)[sel], exp)

@@ -30,6 +30,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <exception>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -75,6 +76,11 @@ class Reader {
   };
 
   bool ok() const { return err_.empty(); }
+  uint64_t message_bytes() const {
+    uint64_t w = 0;
+    for (uint64_t x : size_) w += x;
+    return w * 8;
+  }
   const std::string& err() const { return err_; }
 
   uint64_t word(uint32_t seg, uint64_t i) const { return w_[start_[seg] + i]; }
@@ -331,6 +337,13 @@ bool read_payload(Reader& r, const Reader::Struct& key, std::vector<uint64_t>& o
       return false;
     }
     total += parts[i].present ? parts[i].count : 0;
+    // blobs may alias (several pointers to one Data): cap the payload at the message's own size,
+    // so a crafted message cannot make the reader allocate more than it was given (capnp's
+    // traversal limit plays this role)
+    if (total > r.message_bytes()) {
+      set_error("key payload: blobs total more bytes than the message holds (aliased blobs?)");
+      return false;
+    }
   }
   if (total % 8) {
     set_error("key payload: %llu bytes is not a whole number of u64 words", (unsigned long long)total);
@@ -412,7 +425,19 @@ bool read_keys(Reader& r, const Reader::List& list, bool is_bsk, std::vector<con
   return true;
 }
 
+int parse_impl(const uint64_t* words, uint64_t n_words, uint32_t root, concrete_hip_server_keyset** out);
+
+// no C++ exception crosses the C ABI: allocation failures (a 1 GB key on a short host) are errors
 int parse(const uint64_t* words, uint64_t n_words, uint32_t root, concrete_hip_server_keyset** out) {
+  try {
+    return parse_impl(words, n_words, root, out);
+  } catch (const std::exception& e) {
+    set_error("deserialize: %s", e.what());
+    return -3;
+  }
+}
+
+int parse_impl(const uint64_t* words, uint64_t n_words, uint32_t root, concrete_hip_server_keyset** out) {
   if (n_words < 1) {
     set_error("deserialize: empty input");
     return -3;
@@ -537,6 +562,29 @@ int expand(const concrete_hip_server_keyset::Key& k, bool is_bsk, uint64_t* dst,
 
 }  // namespace
 
+static int add_server_keyset(concrete_hip_keyset* ks, const concrete_hip_server_keyset* sk) {
+  std::vector<uint64_t> buf;
+  for (uint32_t i = 0; i < sk->bsk.size(); ++i) {
+    const concrete_hip_key_info& k = sk->bsk[i].info;
+    buf.assign(k.key_words, 0);
+    int rc = expand(sk->bsk[i], true, buf.data(), buf.size());
+    if (rc) return rc;
+    rc = concrete_hip_keyset_add_bsk(ks, i, buf.data(), k.input_lwe_dim, k.glwe_dim, k.level_count, k.base_log,
+                                     k.poly_size);
+    if (rc) return rc;
+  }
+  for (uint32_t i = 0; i < sk->ksk.size(); ++i) {
+    const concrete_hip_key_info& k = sk->ksk[i].info;
+    buf.assign(k.key_words, 0);
+    int rc = expand(sk->ksk[i], false, buf.data(), buf.size());
+    if (rc) return rc;
+    rc = concrete_hip_keyset_add_ksk(ks, i, buf.data(), k.level_count, k.base_log, k.input_lwe_dim,
+                                     k.output_lwe_dim);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 extern "C" {
 
 int concrete_hip_server_keyset_deserialize(const void* bytes, uint64_t size, uint32_t root,
@@ -551,9 +599,14 @@ int concrete_hip_server_keyset_deserialize(const void* bytes, uint64_t size, uin
     return -3;
   }
   if ((uintptr_t)bytes % 8 == 0) return parse((const uint64_t*)bytes, size / 8, root, out);
-  std::vector<uint64_t> copy(size / 8);
-  memcpy(copy.data(), bytes, size);
-  return parse(copy.data(), copy.size(), root, out);
+  try {
+    std::vector<uint64_t> copy(size / 8);
+    memcpy(copy.data(), bytes, size);
+    return parse(copy.data(), copy.size(), root, out);
+  } catch (const std::exception& e) {
+    set_error("server_keyset_deserialize: %s", e.what());
+    return -3;
+  }
 }
 
 int concrete_hip_server_keyset_load_file(const char* path, uint32_t root, concrete_hip_server_keyset** out) {
@@ -569,12 +622,18 @@ int concrete_hip_server_keyset_load_file(const char* path, uint32_t root, concre
   }
   std::vector<uint64_t> buf;
   uint64_t got = 0;
-  if (fseek(f, 0, SEEK_END) == 0) {
-    long len = ftell(f);
-    if (len > 0 && len % 8 == 0 && fseek(f, 0, SEEK_SET) == 0) {
-      buf.resize((uint64_t)len / 8);
-      got = fread(buf.data(), 1, (size_t)len, f);
+  try {
+    if (fseek(f, 0, SEEK_END) == 0) {
+      long len = ftell(f);
+      if (len > 0 && len % 8 == 0 && fseek(f, 0, SEEK_SET) == 0) {
+        buf.resize((uint64_t)len / 8);
+        got = fread(buf.data(), 1, (size_t)len, f);
+      }
     }
+  } catch (const std::exception& e) {
+    fclose(f);
+    set_error("server_keyset_load_file: %s", e.what());
+    return -3;
   }
   fclose(f);
   if (buf.empty() || got != buf.size() * 8) {
@@ -642,26 +701,12 @@ int concrete_hip_keyset_add_server_keyset(concrete_hip_keyset* ks, const concret
     set_error("keyset_add_server_keyset: bad argument");
     return -3;
   }
-  std::vector<uint64_t> buf;
-  for (uint32_t i = 0; i < sk->bsk.size(); ++i) {
-    const concrete_hip_key_info& k = sk->bsk[i].info;
-    buf.assign(k.key_words, 0);
-    int rc = expand(sk->bsk[i], true, buf.data(), buf.size());
-    if (rc) return rc;
-    rc = concrete_hip_keyset_add_bsk(ks, i, buf.data(), k.input_lwe_dim, k.glwe_dim, k.level_count, k.base_log,
-                                     k.poly_size);
-    if (rc) return rc;
+  try {
+    return add_server_keyset(ks, sk);
+  } catch (const std::exception& e) {
+    set_error("keyset_add_server_keyset: %s", e.what());
+    return -3;
   }
-  for (uint32_t i = 0; i < sk->ksk.size(); ++i) {
-    const concrete_hip_key_info& k = sk->ksk[i].info;
-    buf.assign(k.key_words, 0);
-    int rc = expand(sk->ksk[i], false, buf.data(), buf.size());
-    if (rc) return rc;
-    rc = concrete_hip_keyset_add_ksk(ks, i, buf.data(), k.level_count, k.base_log, k.input_lwe_dim,
-                                     k.output_lwe_dim);
-    if (rc) return rc;
-  }
-  return 0;
 }
 
 }  // extern "C"

@@ -312,3 +312,31 @@ def test_c_client_reads_the_same_keys(tmp_path):
     bad.write_bytes(path.read_bytes()[:-8])
     r = subprocess.run([str(exe), str(bad)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 1 and "segment" in r.stderr
+
+
+def test_aliased_blobs_cannot_amplify_the_payload():
+    """A crafted List(Data) whose many pointers all name one blob would make a naive reader
+    allocate (pointers x blob) bytes; the reader caps a payload at the message's own size."""
+    m = K._Message("flat")
+    key = m.new_struct(0, 2)
+    m.set_root(key)
+    info = K.bsk_info(_P)
+    inf = m.new_struct(K.INFO_WORDS, 1)
+    par = m.new_struct(K.BSK_PARAMS_WORDS, 1)
+    for name, off in K.BSK_PARAMS_OFF.items():
+        fmt = "d" if name == "variance" else ("H" if name == "key_type" else "I")
+        m.set_data(par, off, fmt, getattr(info, name))
+    m.set_struct_ptr(inf, 0, par)
+    m.set_struct_ptr(key, 0, inf)
+    pl = m.new_struct(0, 1)
+    n_ptr = 4096
+    plist = m.new_ptr_list(n_ptr)
+    blob = m.new_data(b"\x01" * 4096)
+    for b in range(n_ptr):
+        m.set_list_elem_ptr(plist, b, blob)  # every element points at the same 4 KB
+    m.set_list_ptr(pl, 0, plist)
+    m.set_struct_ptr(key, 1, pl)
+    data = m.to_bytes()
+    assert len(data) < 64 * 1024  # 16 MB of payload if the aliases were followed
+    assert _deser_rc(data, root=2) < 0
+    assert "aliased" in _native.lib().concrete_hip_last_error().decode()

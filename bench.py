@@ -122,6 +122,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", type=int, default=8, help="rows checked bit-exactly against the oracle (rank 0)")
     ap.add_argument("--no-ks", action="store_true", help="skip the secondary keyswitch measurement")
+    ap.add_argument("--no-sdfg", action="store_true", help="skip the stream-emulator (SDFG route) measurement")
     ap.add_argument("--check-gather", action="store_true",
                     help="rank 0 checks the whole gathered batch: every row decrypts to its rank's LUT[m], and "
                          "two rows per rank are bit-exact vs the oracle (inputs regenerated from the seeds)")
@@ -290,6 +291,46 @@ def main():
     torch.cuda.synchronize()
     e2e = args.batch * args.steps / (time.perf_counter() - t0)
 
+    # ---- the circuit-facing SDFG route (the default GPU route of a compiled circuit,
+    # stream_emulator_*): a KS -> PBS table lookup on host memrefs, timed end to end per run (put
+    # the batch, get the outputs: H2D, keyswitch, bootstrap, D2H, intermediates resident in HBM)
+    sdfg_res = None
+    if world == 1 and args.config == "cfg2" and not args.no_ks and not args.no_sdfg:
+        from concrete_amd import runtime as R
+        width_s = 2  # KS -> PBS chains keep p <= 2 at the cfg2 keyswitch noise
+        table_s = np.array([3, 0, 2, 1], dtype=np.uint64)
+        rng_s = np.random.RandomState(17)
+        msgs_s = rng_s.randint(0, 1 << width_s, size=args.batch)
+        big_in = B.lwe_encrypt(glwe_sk, [B.encode(m, width_s) for m in msgs_s], p.big_n, 2.0 ** -30, 18)
+        kset = R.Keyset([local])
+        kset.add_bsk(0, bsk if bsk is not None else B.bsk_generate(p, lwe_sk, glwe_sk, 3), p)
+        kset.add_ksk(0, ksk, p)
+        ctx = 0x5DF6  # the RuntimeContext pointer a circuit would pass (bound, never dereferenced)
+        kset.bind(ctx)
+        g = R.Dfg()
+        s_in = g.batch_stream("in", R.TS_X86_TO_TOPO)
+        s_lut = g.memref_stream("lut", R.TS_X86_TO_TOPO)
+        s_mid = g.batch_stream("mid")
+        s_res = g.batch_stream("out", R.TS_TOPO_TO_X86)
+        g.keyswitch(s_in, s_mid, p, ctx)
+        g.bootstrap(s_mid, s_lut, s_res, p, ctx)
+        g.run()
+        g.put_memref(s_lut, B.expand_lut(table_s, p.N, width_s))
+        g.put_batch(s_in, big_in)
+        res = g.get_batch(s_res, args.batch, p.lwe_out_size)  # warm-up: device keys, buffers
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            g.put_batch(s_in, big_in)
+            res = g.get_batch(s_res, args.batch, p.lwe_out_size)
+        sdfg_s = (time.perf_counter() - t0) / args.steps
+        dec_s = B.lwe_decrypt(glwe_sk, res, p.big_n)
+        ok_s = int(sum(B.decode(d, width_s) == int(table_s[m]) for d, m in zip(dec_s, msgs_s)))
+        sdfg_res = {"metric": "KS -> PBS table lookups/sec through stream_emulator_* (host memrefs in and out)",
+                    "value": round(args.batch / sdfg_s, 1), "unit": "TLU/s", "ms_per_run": round(sdfg_s * 1e3, 3),
+                    "decrypt_ok": f"{ok_s}/{args.batch}"}
+        g.close()
+        kset.close()
+
     # ---- final gather of the output rows onto rank 0 (outside the timed PBS region)
     t_gather = 0.0
     gather_check = None
@@ -418,7 +459,7 @@ def main():
                          "kernel_ms": round(kern_ms, 3), "bytes_per_pbs": bytes_per_pbs,
                          "dram": dram, "valu": valu},
             "cpu_baseline": cpu,
-            "secondary": {"keyswitch": ks_res,
+            "secondary": {"keyswitch": ks_res, "sdfg_route": sdfg_res,
                           "pcie_inclusive_pbs_per_s": round(e2e * world, 1)},
             "checks": {"decrypt_ok": f"{ok_all}/{global_batch}", "bitexact_rows": args.verify, "gather": gather_check,
                        "bitexact": bitexact},

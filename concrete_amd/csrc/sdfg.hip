@@ -47,11 +47,77 @@ enum ProcKind { P_ADD, P_ADD_PT, P_MUL_CT, P_NEG, P_KS, P_PBS };
 struct Dfg;
 struct Proc;
 
+// A stream's host copy: grow-only page-locked memory (hipHostMalloc), so the shard threads' H2D /
+// D2H copies are DMA at link speed and asynchronous (pageable copies are staged by the runtime in
+// small blocking pieces: the KS -> PBS route at cfg2 spent ~25 of its 66 ms per 4096 samples in
+// them); pageable fallback when pinning fails.  Contents are not zeroed on growth.
+class HostBuf {
+ public:
+  HostBuf() = default;
+  HostBuf(const HostBuf&) = delete;
+  HostBuf& operator=(const HostBuf&) = delete;
+  ~HostBuf() { release(); }
+  uint64_t* data() { return p_; }
+  const uint64_t* data() const { return p_; }
+  uint64_t size() const { return n_; }
+  uint64_t& operator[](uint64_t i) { return p_[i]; }
+  const uint64_t* begin() const { return p_; }
+  const uint64_t* end() const { return p_ + n_; }
+  void resize(uint64_t n) {
+    if (n > cap_) {
+      uint64_t* q = nullptr;
+      bool pinned = hipHostMalloc((void**)&q, std::max<uint64_t>(n, 1) * 8, hipHostMallocDefault) == hipSuccess;
+      if (!pinned) {
+        (void)hipGetLastError();
+        q = (uint64_t*)malloc(std::max<uint64_t>(n, 1) * 8);
+        if (!q) rt_die("stream_emulator: out of host memory (%llu words)", (unsigned long long)n);
+      }
+      if (n_) memcpy(q, p_, n_ * 8);
+      release();
+      p_ = q, cap_ = n, pinned_ = pinned;
+    }
+    n_ = n;
+  }
+
+ private:
+  void release() {
+    if (!p_) return;
+    if (pinned_) (void)hipHostFree(p_);
+    else free(p_);
+    p_ = nullptr, cap_ = 0;
+  }
+  uint64_t* p_ = nullptr;
+  uint64_t n_ = 0, cap_ = 0;
+  bool pinned_ = false;
+};
+
+// Row-wise copy between host memrefs and stream buffers, split over a few threads for large
+// batches (a single core moves ~10 GB/s: 3-4 ms per 4096 x 1025 words).
+void copy_rows(uint64_t* dst, uint64_t dst_stride, const uint64_t* src, uint64_t src_stride, uint64_t rows,
+               uint64_t cols) {
+  auto part = [&](uint64_t r0, uint64_t r1) {
+    if (dst_stride == cols && src_stride == cols) {
+      memcpy(dst + r0 * cols, src + r0 * cols, (r1 - r0) * cols * 8);
+      return;
+    }
+    for (uint64_t r = r0; r < r1; ++r) memcpy(dst + r * dst_stride, src + r * src_stride, cols * 8);
+  };
+  const uint64_t bytes = rows * cols * 8;
+  const uint64_t nt = std::min<uint64_t>(std::min<uint64_t>(8, rows), bytes >> 22);  // >= 4 MB per thread
+  if (nt <= 1) {
+    part(0, rows);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (uint64_t t = 0; t < nt; ++t) th.emplace_back(part, rows * t / nt, rows * (t + 1) / nt);
+  for (auto& x : th) x.join();
+}
+
 struct Stream {
   std::string name;
   int stype = 0;
   StreamKind kind = SK_MEMREF;
-  std::vector<uint64_t> host;  // rows x cols, row-major, valid when host_ok
+  HostBuf host;                // rows x cols, row-major, valid when host_ok
   uint64_t rows = 0, cols = 0;
   bool host_ok = false;
   uint64_t version = 0;        // put streams: clock value of the last put
@@ -350,7 +416,7 @@ void run_chunk(const Plan& P, Slot& sl, uint64_t start, uint64_t cnt) {
     const uint64_t rows = in.broadcast ? 1 : cnt;
     uint64_t* d = alloc(rows * in.width * 8);
     const uint64_t* src = in.s->host.data() + (in.broadcast ? 0 : start * in.width);
-    CHIP_CHECK(hipMemcpyWithStream(d, src, rows * in.width * 8, hipMemcpyHostToDevice, s));
+    CHIP_CHECK(hipMemcpyAsync(d, src, rows * in.width * 8, hipMemcpyHostToDevice, s));
     dev[in.s] = d;
   }
   auto is_broadcast = [&](Stream* x) {
@@ -405,12 +471,12 @@ void run_chunk(const Plan& P, Slot& sl, uint64_t start, uint64_t cnt) {
         break;
     }
   }
-  // copies to and from pageable host memory are the blocking form (the host's vectors are the
-  // source and destination; the stream is idle when the chunk returns)
+  // copies to and from the streams' page-locked host buffers are stream-ordered DMA; the stream is
+  // idle when the chunk returns
   for (Stream* x : P.produced)
     if (P.download.count(x)) {
       const uint64_t w = P.width.at(x);
-      CHIP_CHECK(hipMemcpyWithStream(x->host.data() + start * w, dev.at(x), cnt * w * 8, hipMemcpyDeviceToHost, s));
+      CHIP_CHECK(hipMemcpyAsync(x->host.data() + start * w, dev.at(x), cnt * w * 8, hipMemcpyDeviceToHost, s));
     }
   CHIP_CHECK(hipStreamSynchronize(s));
   if (trace_on()) {
@@ -443,7 +509,7 @@ void execute(Dfg* g, Stream* target) {
   for (Stream* x : P.produced)
     if (P.download.count(x)) {
       x->rows = P.batch, x->cols = P.width.at(x);
-      x->host.assign(x->rows * x->cols, 0);
+      x->host.resize(x->rows * x->cols);  // every row is written by its shard's D2H
     }
   const uint64_t parts = std::max<uint64_t>(1, std::min<uint64_t>(g->devices.size(), P.batch));
   if (g->slots.size() < parts) g->slots.resize(parts);
@@ -509,7 +575,7 @@ void put(Stream* s, const uint64_t* data, uint64_t rows, uint64_t cols, uint64_t
   if (!s) rt_die("stream_emulator: null stream");
   s->rows = rows, s->cols = cols;
   s->host.resize(rows * cols);
-  for (uint64_t r = 0; r < rows; ++r) memcpy(s->host.data() + r * cols, data + r * stride0, cols * 8);
+  copy_rows(s->host.data(), cols, data, stride0, rows, cols);
   s->host_ok = true;
   s->version = ++g_clock;
   if (s->producer) {  // a value put on a produced stream stands until its inputs change
@@ -524,7 +590,7 @@ void copy_out(Stream* s, uint64_t* out, uint64_t rows, uint64_t cols, uint64_t s
     rt_die("stream_emulator: stream %s holds %llux%llu words, the output memref is %llux%llu", s->name.c_str(),
            (unsigned long long)s->rows, (unsigned long long)s->cols, (unsigned long long)rows,
            (unsigned long long)cols);
-  for (uint64_t r = 0; r < rows; ++r) memcpy(out + r * stride0, s->host.data() + r * cols, cols * 8);
+  copy_rows(out, stride0, s->host.data(), cols, rows, cols);
   if (trace_on()) {
     uint64_t h = 0;
     for (uint64_t v : s->host) h ^= v;

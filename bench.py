@@ -329,6 +329,24 @@ def main():
                     "value": round(args.batch / sdfg_s, 1), "unit": "TLU/s", "ms_per_run": round(sdfg_s * 1e3, 3),
                     "decrypt_ok": f"{ok_s}/{args.batch}"}
         g.close()
+        # the direct route (memref_batched_bootstrap_lwe_*_u64, wrappers.cpp:164-256): host rows in,
+        # host rows out, on the same keyset
+        tlu_d = B.expand_lut(table, p.N, width)
+        R.batched_bootstrap(kset, p, cts, tlu_d)  # warm-up
+        if os.environ.get("CONCRETE_HIP_BENCH_TIMELINE"):
+            kset.set_timing(True)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            res_d = R.batched_bootstrap(kset, p, cts, tlu_d)
+            if os.environ.get("CONCRETE_HIP_BENCH_TIMELINE"):
+                print("direct route timeline (dev, start, in, kernel, out, n):", kset.timeline().round(3).tolist(),
+                      f"wall {1e3 * (time.perf_counter() - t0):.2f} ms", file=sys.stderr, flush=True)
+        direct_s = (time.perf_counter() - t0) / args.steps
+        dec_d = B.lwe_decrypt(glwe_sk, res_d, p.big_n)
+        ok_d = int(sum(B.decode(d, width) == int(table[m]) for d, m in zip(dec_d, msgs)))
+        sdfg_res["direct_route"] = {"metric": "PBS/sec through memref_batched_bootstrap_lwe_*_u64 (host memrefs)",
+                                    "value": round(args.batch / direct_s, 1), "unit": "PBS/s",
+                                    "ms_per_call": round(direct_s * 1e3, 3), "decrypt_ok": f"{ok_d}/{args.batch}"}
         kset.close()
 
     # ---- final gather of the output rows onto rank 0 (outside the timed PBS region)

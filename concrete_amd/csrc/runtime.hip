@@ -14,9 +14,9 @@
 //     slice r + 1's copies and kernel are issued while slice r's are in flight;
 //   * accumulators are built on the device from the LUT rows (lut.hip), so only N words per LUT
 //     cross PCIe instead of the (k+1)N-word trivial GLWE (wrappers.cpp:199-209).
-// Copies from / to the caller's (pageable) memory use the blocking hipMemcpyWithStream: HIP stages
-// pageable copies, and the staged tail of an asynchronous D2H was seen to land after
-// hipStreamSynchronize had returned (sdfg.hip); each slice's thread blocks on its own copies only.
+// The caller's (pageable) ciphertext rows go through page-locked staging per slice slot (host
+// copies on a few threads, then asynchronous DMA; runtime.hpp HostBuf); LUT rows are small and
+// copied with the blocking hipMemcpyWithStream.  Each slice's thread waits on its own stream only.
 // Two name sets: memref_*_hip_u64 take the keyset handle itself; memref_*_cuda_u64 carry the
 // reference names and take the caller's runtime context pointer, resolved to a keyset through
 // concrete_hip_context_bind / concrete_hip_set_context_resolver.
@@ -282,7 +282,11 @@ void run_batched_pbs(concrete_hip_keyset* ks, uint64_t num_samples, const PbsCal
     uint64_t* d_acc = d_lut + rows * c.N;
     uint64_t* d_lidx = mapped ? slot_buf(sl, 3, count * 8) : nullptr;
     mark(ks, sl, 0);
-    CHIP_CHECK(hipMemcpyWithStream(d_in, c.ct0 + start * in_w, count * in_w * 8, hipMemcpyHostToDevice, sl.s));
+    // the caller's memref is pageable: its rows go through the slot's page-locked staging, whose
+    // copy to the device is asynchronous DMA
+    sl.stage_in.resize(count * in_w);
+    copy_rows(sl.stage_in.data(), in_w, c.ct0 + start * in_w, in_w, count, in_w);
+    CHIP_CHECK(copy_h2d(d_in, sl.stage_in, sl.stage_in.data(), count * in_w * 8, sl.s));
     // one LUT per sample: this slice's rows, indexed 0..count-1 (wrappers.cpp:317-325)
     const uint64_t* src = c.tlu + (mapped ? start * c.tlu_stride0 : 0);
     if (c.tlu_stride0 == c.N || rows == 1) {
@@ -299,9 +303,11 @@ void run_batched_pbs(concrete_hip_keyset* ks, uint64_t num_samples, const PbsCal
                          c.level, (uint32_t)count, nullptr) != 0)
       rt_die("%s", concrete_hip_last_error());
     mark(ks, sl, 2);
-    CHIP_CHECK(hipMemcpyWithStream(c.out + start * out_w, d_out, count * out_w * 8, hipMemcpyDeviceToHost, sl.s));
+    sl.stage_out.resize(count * out_w);
+    CHIP_CHECK(copy_d2h(sl.stage_out.data(), sl.stage_out, d_out, count * out_w * 8, sl.s));
     mark(ks, sl, 3);
     CHIP_CHECK(hipStreamSynchronize(sl.s));
+    copy_rows(c.out + start * out_w, out_w, sl.stage_out.data(), out_w, count, out_w);
   });
 }
 
@@ -318,15 +324,19 @@ void run_batched_ks(concrete_hip_keyset* ks, uint64_t num_samples, const uint64_
     uint64_t* d_in = slot_buf(sl, 0, count * in_w * 8);
     uint64_t* d_out = slot_buf(sl, 1, count * out_w * 8);
     mark(ks, sl, 0);
-    CHIP_CHECK(hipMemcpyWithStream(d_in, ct0 + start * in_w, count * in_w * 8, hipMemcpyHostToDevice, sl.s));
+    sl.stage_in.resize(count * in_w);
+    copy_rows(sl.stage_in.data(), in_w, ct0 + start * in_w, in_w, count, in_w);
+    CHIP_CHECK(copy_h2d(d_in, sl.stage_in, sl.stage_in.data(), count * in_w * 8, sl.s));
     mark(ks, sl, 1);
     if (concrete_hip_keyswitch(sl.s, sl.gpu, d_out, nullptr, d_in, nullptr, (const uint64_t*)dk, n_in, n_out, base_log,
                                level, (uint32_t)count) != 0)
       rt_die("%s", concrete_hip_last_error());
     mark(ks, sl, 2);
-    CHIP_CHECK(hipMemcpyWithStream(out + start * out_w, d_out, count * out_w * 8, hipMemcpyDeviceToHost, sl.s));
+    sl.stage_out.resize(count * out_w);
+    CHIP_CHECK(copy_d2h(sl.stage_out.data(), sl.stage_out, d_out, count * out_w * 8, sl.s));
     mark(ks, sl, 3);
     CHIP_CHECK(hipStreamSynchronize(sl.s));
+    copy_rows(out + start * out_w, out_w, sl.stage_out.data(), out_w, count, out_w);
   });
 }
 

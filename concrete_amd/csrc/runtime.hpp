@@ -6,7 +6,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/concrete_hip.h"
@@ -34,6 +39,96 @@ struct KskEntry {
   std::mutex m;
 };
 
+// Host memory the devices copy from and to: grow-only page-locked memory (hipHostMalloc), so H2D /
+// D2H copies are DMA at link speed and asynchronous (pageable copies are staged by the runtime in
+// small blocking pieces: the stream emulator's KS -> PBS route at cfg2 spent ~25 of its 66 ms per
+// 4096 samples in them); pageable fallback when pinning fails.  Contents are not zeroed on growth.
+// Used for the stream emulator's stream buffers (sdfg.hip) and the memref route's staging
+// (runtime.hip).
+class HostBuf {
+ public:
+  HostBuf() = default;
+  HostBuf(const HostBuf&) = delete;
+  HostBuf& operator=(const HostBuf&) = delete;
+  HostBuf(HostBuf&& o) noexcept : p_(o.p_), n_(o.n_), cap_(o.cap_), pinned_(o.pinned_) { o.p_ = nullptr, o.n_ = o.cap_ = 0; }
+  HostBuf& operator=(HostBuf&& o) noexcept {
+    if (this != &o) {
+      release();
+      p_ = o.p_, n_ = o.n_, cap_ = o.cap_, pinned_ = o.pinned_;
+      o.p_ = nullptr, o.n_ = o.cap_ = 0;
+    }
+    return *this;
+  }
+  ~HostBuf() { release(); }
+  uint64_t* data() { return p_; }
+  const uint64_t* data() const { return p_; }
+  uint64_t size() const { return n_; }
+  bool pinned() const { return pinned_; }
+  uint64_t& operator[](uint64_t i) { return p_[i]; }
+  const uint64_t* begin() const { return p_; }
+  const uint64_t* end() const { return p_ + n_; }
+  void resize(uint64_t n) {
+    if (n > cap_) {
+      uint64_t* q = nullptr;
+      bool pinned = hipHostMalloc((void**)&q, std::max<uint64_t>(n, 1) * 8, hipHostMallocDefault) == hipSuccess;
+      if (!pinned) {
+        (void)hipGetLastError();
+        q = (uint64_t*)malloc(std::max<uint64_t>(n, 1) * 8);
+        if (!q) rt_die("stream_emulator: out of host memory (%llu words)", (unsigned long long)n);
+      }
+      if (n_) memcpy(q, p_, n_ * 8);
+      release();
+      p_ = q, cap_ = n, pinned_ = pinned;
+    }
+    n_ = n;
+  }
+
+ private:
+  void release() {
+    if (!p_) return;
+    if (pinned_) (void)hipHostFree(p_);
+    else free(p_);
+    p_ = nullptr, cap_ = 0;
+  }
+  uint64_t* p_ = nullptr;
+  uint64_t n_ = 0, cap_ = 0;
+  bool pinned_ = false;
+};
+
+// Host <-> device copy of a HostBuf range: asynchronous DMA when page-locked; the blocking form
+// for the pageable fallback (the staged tail of an asynchronous pageable D2H was seen to land after
+// hipStreamSynchronize had returned).
+inline hipError_t copy_h2d(void* dev, const HostBuf& h, const uint64_t* src, uint64_t bytes, hipStream_t s) {
+  return h.pinned() ? hipMemcpyAsync(dev, src, bytes, hipMemcpyHostToDevice, s)
+                    : hipMemcpyWithStream(dev, src, bytes, hipMemcpyHostToDevice, s);
+}
+inline hipError_t copy_d2h(uint64_t* dst, const HostBuf& h, const void* dev, uint64_t bytes, hipStream_t s) {
+  return h.pinned() ? hipMemcpyAsync(dst, dev, bytes, hipMemcpyDeviceToHost, s)
+                    : hipMemcpyWithStream(dst, dev, bytes, hipMemcpyDeviceToHost, s);
+}
+
+// Row-wise copy between host memrefs and stream buffers, split over a few threads for large
+// batches (a single core moves ~10 GB/s: 3-4 ms per 4096 x 1025 words).
+inline void copy_rows(uint64_t* dst, uint64_t dst_stride, const uint64_t* src, uint64_t src_stride, uint64_t rows,
+               uint64_t cols) {
+  auto part = [&](uint64_t r0, uint64_t r1) {
+    if (dst_stride == cols && src_stride == cols) {
+      memcpy(dst + r0 * cols, src + r0 * cols, (r1 - r0) * cols * 8);
+      return;
+    }
+    for (uint64_t r = r0; r < r1; ++r) memcpy(dst + r * dst_stride, src + r * src_stride, cols * 8);
+  };
+  const uint64_t bytes = rows * cols * 8;
+  const uint64_t nt = std::min<uint64_t>(std::min<uint64_t>(8, rows), bytes >> 22);  // >= 4 MB per thread
+  if (nt <= 1) {
+    part(0, rows);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (uint64_t t = 0; t < nt; ++t) th.emplace_back(part, rows * t / nt, rows * (t + 1) / nt);
+  for (auto& x : th) x.join();
+}
+
 // Per-slice resources of the memref route, reused across calls (grow-only device buffers, one
 // non-blocking stream, timing events).  Slot r serves slice r of a call.
 struct SliceSlot {
@@ -43,6 +138,7 @@ struct SliceSlot {
   uint64_t cap[4] = {};   // bytes
   hipEvent_t ev[5] = {};  // start, after H2D, after kernel, after D2H; ev[4] unused
   std::vector<void*> retired;  // outgrown buffers, freed once every slice thread has joined
+  HostBuf stage_in, stage_out;  // page-locked staging of the caller's (pageable) memrefs
 };
 
 }  // namespace chip

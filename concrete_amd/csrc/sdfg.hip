@@ -47,72 +47,6 @@ enum ProcKind { P_ADD, P_ADD_PT, P_MUL_CT, P_NEG, P_KS, P_PBS };
 struct Dfg;
 struct Proc;
 
-// A stream's host copy: grow-only page-locked memory (hipHostMalloc), so the shard threads' H2D /
-// D2H copies are DMA at link speed and asynchronous (pageable copies are staged by the runtime in
-// small blocking pieces: the KS -> PBS route at cfg2 spent ~25 of its 66 ms per 4096 samples in
-// them); pageable fallback when pinning fails.  Contents are not zeroed on growth.
-class HostBuf {
- public:
-  HostBuf() = default;
-  HostBuf(const HostBuf&) = delete;
-  HostBuf& operator=(const HostBuf&) = delete;
-  ~HostBuf() { release(); }
-  uint64_t* data() { return p_; }
-  const uint64_t* data() const { return p_; }
-  uint64_t size() const { return n_; }
-  uint64_t& operator[](uint64_t i) { return p_[i]; }
-  const uint64_t* begin() const { return p_; }
-  const uint64_t* end() const { return p_ + n_; }
-  void resize(uint64_t n) {
-    if (n > cap_) {
-      uint64_t* q = nullptr;
-      bool pinned = hipHostMalloc((void**)&q, std::max<uint64_t>(n, 1) * 8, hipHostMallocDefault) == hipSuccess;
-      if (!pinned) {
-        (void)hipGetLastError();
-        q = (uint64_t*)malloc(std::max<uint64_t>(n, 1) * 8);
-        if (!q) rt_die("stream_emulator: out of host memory (%llu words)", (unsigned long long)n);
-      }
-      if (n_) memcpy(q, p_, n_ * 8);
-      release();
-      p_ = q, cap_ = n, pinned_ = pinned;
-    }
-    n_ = n;
-  }
-
- private:
-  void release() {
-    if (!p_) return;
-    if (pinned_) (void)hipHostFree(p_);
-    else free(p_);
-    p_ = nullptr, cap_ = 0;
-  }
-  uint64_t* p_ = nullptr;
-  uint64_t n_ = 0, cap_ = 0;
-  bool pinned_ = false;
-};
-
-// Row-wise copy between host memrefs and stream buffers, split over a few threads for large
-// batches (a single core moves ~10 GB/s: 3-4 ms per 4096 x 1025 words).
-void copy_rows(uint64_t* dst, uint64_t dst_stride, const uint64_t* src, uint64_t src_stride, uint64_t rows,
-               uint64_t cols) {
-  auto part = [&](uint64_t r0, uint64_t r1) {
-    if (dst_stride == cols && src_stride == cols) {
-      memcpy(dst + r0 * cols, src + r0 * cols, (r1 - r0) * cols * 8);
-      return;
-    }
-    for (uint64_t r = r0; r < r1; ++r) memcpy(dst + r * dst_stride, src + r * src_stride, cols * 8);
-  };
-  const uint64_t bytes = rows * cols * 8;
-  const uint64_t nt = std::min<uint64_t>(std::min<uint64_t>(8, rows), bytes >> 22);  // >= 4 MB per thread
-  if (nt <= 1) {
-    part(0, rows);
-    return;
-  }
-  std::vector<std::thread> th;
-  for (uint64_t t = 0; t < nt; ++t) th.emplace_back(part, rows * t / nt, rows * (t + 1) / nt);
-  for (auto& x : th) x.join();
-}
-
 struct Stream {
   std::string name;
   int stype = 0;
@@ -416,7 +350,7 @@ void run_chunk(const Plan& P, Slot& sl, uint64_t start, uint64_t cnt) {
     const uint64_t rows = in.broadcast ? 1 : cnt;
     uint64_t* d = alloc(rows * in.width * 8);
     const uint64_t* src = in.s->host.data() + (in.broadcast ? 0 : start * in.width);
-    CHIP_CHECK(hipMemcpyAsync(d, src, rows * in.width * 8, hipMemcpyHostToDevice, s));
+    CHIP_CHECK(copy_h2d(d, in.s->host, src, rows * in.width * 8, s));
     dev[in.s] = d;
   }
   auto is_broadcast = [&](Stream* x) {
@@ -476,7 +410,7 @@ void run_chunk(const Plan& P, Slot& sl, uint64_t start, uint64_t cnt) {
   for (Stream* x : P.produced)
     if (P.download.count(x)) {
       const uint64_t w = P.width.at(x);
-      CHIP_CHECK(hipMemcpyAsync(x->host.data() + start * w, dev.at(x), cnt * w * 8, hipMemcpyDeviceToHost, s));
+      CHIP_CHECK(copy_d2h(x->host.data() + start * w, x->host, dev.at(x), cnt * w * 8, s));
     }
   CHIP_CHECK(hipStreamSynchronize(s));
   if (trace_on()) {

@@ -74,7 +74,7 @@ class HostBuf {
       if (!pinned) {
         (void)hipGetLastError();
         q = (uint64_t*)malloc(std::max<uint64_t>(n, 1) * 8);
-        if (!q) rt_die("stream_emulator: out of host memory (%llu words)", (unsigned long long)n);
+        if (!q) rt_die("host buffer: out of host memory (%llu words)", (unsigned long long)n);
       }
       if (n_) memcpy(q, p_, n_ * 8);
       release();

@@ -14,15 +14,16 @@
 //     slice r + 1's copies and kernel are issued while slice r's are in flight;
 //   * accumulators are built on the device from the LUT rows (lut.hip), so only N words per LUT
 //     cross PCIe instead of the (k+1)N-word trivial GLWE (wrappers.cpp:199-209).
-// The caller's (pageable) ciphertext rows go through page-locked staging per slice slot (host
-// copies on a few threads, then asynchronous DMA; runtime.hpp HostBuf); LUT rows are small and
-// copied with the blocking hipMemcpyWithStream.  Each slice's thread waits on its own stream only.
+// The caller's (pageable) ciphertext and LUT rows go through page-locked staging per slice slot
+// (host copies on a few threads, then asynchronous DMA; runtime.hpp HostBuf), so issuing a slice
+// never blocks on a copy.  Each slice's thread waits on its own stream only.
 // Two name sets: memref_*_hip_u64 take the keyset handle itself; memref_*_cuda_u64 carry the
 // reference names and take the caller's runtime context pointer, resolved to a keyset through
 // concrete_hip_context_bind / concrete_hip_set_context_resolver.
 #include <stdarg.h>
 
 #include <algorithm>
+#include <chrono>
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
@@ -45,6 +46,16 @@ void rt_die(const char* fmt, ...) {
 }
 
 namespace {
+
+// CONCRETE_HIP_ROUTE_TRACE=1: host-side phase times of every memref-route PBS slice on stderr
+// (diagnostic; the device side is the keyset timeline)
+bool route_trace() {
+  static const bool on = getenv("CONCRETE_HIP_ROUTE_TRACE") != nullptr;
+  return on;
+}
+double ms_since(std::chrono::steady_clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
 
 template <class E>
 E* entry(std::vector<E*>& v, uint32_t idx, std::mutex& m, bool create) {
@@ -282,32 +293,43 @@ void run_batched_pbs(concrete_hip_keyset* ks, uint64_t num_samples, const PbsCal
     uint64_t* d_acc = d_lut + rows * c.N;
     uint64_t* d_lidx = mapped ? slot_buf(sl, 3, count * 8) : nullptr;
     mark(ks, sl, 0);
+    const auto t0 = std::chrono::steady_clock::now();
     // the caller's memref is pageable: its rows go through the slot's page-locked staging, whose
     // copy to the device is asynchronous DMA
     sl.stage_in.resize(count * in_w);
     copy_rows(sl.stage_in.data(), in_w, c.ct0 + start * in_w, in_w, count, in_w);
+    const double t_in = ms_since(t0);
     CHIP_CHECK(copy_h2d(d_in, sl.stage_in, sl.stage_in.data(), count * in_w * 8, sl.s));
+    const double t_h2d = ms_since(t0);
     // one LUT per sample: this slice's rows, indexed 0..count-1 (wrappers.cpp:317-325)
+    // (packed into page-locked staging too: a blocking pageable copy here was seen to stall the
+    // issue of the call for tens of ms on some boxes)
     const uint64_t* src = c.tlu + (mapped ? start * c.tlu_stride0 : 0);
-    if (c.tlu_stride0 == c.N || rows == 1) {
-      CHIP_CHECK(hipMemcpyWithStream(d_lut, src, rows * c.N * 8, hipMemcpyHostToDevice, sl.s));
-    } else {
-      std::vector<uint64_t> packed(rows * c.N);
-      for (uint64_t r = 0; r < rows; ++r) std::copy(src + r * c.tlu_stride0, src + r * c.tlu_stride0 + c.N, &packed[r * c.N]);
-      CHIP_CHECK(hipMemcpyWithStream(d_lut, packed.data(), rows * c.N * 8, hipMemcpyHostToDevice, sl.s));
-    }
+    sl.stage_lut.resize(rows * c.N);
+    copy_rows(sl.stage_lut.data(), c.N, src, c.tlu_stride0, rows, c.N);
+    CHIP_CHECK(copy_h2d(d_lut, sl.stage_lut, sl.stage_lut.data(), rows * c.N * 8, sl.s));
+    const double t_lut = ms_since(t0);
     launch_trivial_glwe(sl.s, d_acc, d_lut, rows, c.k, c.N);
     if (mapped) launch_iota(sl.s, d_lidx, count);
     mark(ks, sl, 1);
+    const double t_acc = ms_since(t0);
     if (concrete_hip_pbs(sl.s, sl.gpu, d_out, nullptr, d_acc, d_lidx, d_in, nullptr, fbsk, c.n, c.k, c.N, c.base_log,
                          c.level, (uint32_t)count, nullptr) != 0)
       rt_die("%s", concrete_hip_last_error());
     mark(ks, sl, 2);
+    const double t_pbs = ms_since(t0);
     sl.stage_out.resize(count * out_w);
     CHIP_CHECK(copy_d2h(sl.stage_out.data(), sl.stage_out, d_out, count * out_w * 8, sl.s));
     mark(ks, sl, 3);
+    const double t_issue = ms_since(t0);
     CHIP_CHECK(hipStreamSynchronize(sl.s));
+    const double t_wait = ms_since(t0);
     copy_rows(c.out + start * out_w, out_w, sl.stage_out.data(), out_w, count, out_w);
+    if (route_trace())
+      fprintf(stderr, "route trace: slice %llu (%llu rows): stage-in %.2f, h2d %.2f, lut %.2f, acc %.2f, pbs %.2f, "
+              "issued %.2f, synced %.2f, copied out %.2f ms\n",
+              (unsigned long long)start, (unsigned long long)count, t_in, t_h2d, t_lut, t_acc, t_pbs, t_issue, t_wait,
+              ms_since(t0));
   });
 }
 

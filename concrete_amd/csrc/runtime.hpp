@@ -138,7 +138,7 @@ struct SliceSlot {
   uint64_t cap[4] = {};   // bytes
   hipEvent_t ev[5] = {};  // start, after H2D, after kernel, after D2H; ev[4] unused
   std::vector<void*> retired;  // outgrown buffers, freed once every slice thread has joined
-  HostBuf stage_in, stage_out;  // page-locked staging of the caller's (pageable) memrefs
+  HostBuf stage_in, stage_out, stage_lut;  // page-locked staging of the caller's (pageable) memrefs
 };
 
 }  // namespace chip

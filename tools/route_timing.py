@@ -8,6 +8,13 @@ sys.path.insert(0, ".")
 from concrete_amd import backend as B  # noqa: E402
 from concrete_amd import runtime as R  # noqa: E402
 
+if "--torch" in sys.argv:  # torch's GPU context and streams in the same process, as in bench.py
+    import torch
+    a = torch.randn(2048, 2048, device="cuda")
+    for _ in range(10):
+        a = (a @ a).tanh()
+    torch.cuda.synchronize()
+
 p = B.CFG2
 lwe_sk = B.binary_key(p.n, 1)
 glwe_sk = B.binary_key(p.big_n, 2)

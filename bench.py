@@ -129,6 +129,8 @@ def parse():
     return ap.parse_args()
 
 
+
+
 def main():
     args = parse()
     import torch
@@ -329,16 +331,18 @@ def main():
                     "value": round(args.batch / sdfg_s, 1), "unit": "TLU/s", "ms_per_run": round(sdfg_s * 1e3, 3),
                     "decrypt_ok": f"{ok_s}/{args.batch}"}
         g.close()
-        # the direct route (memref_batched_bootstrap_lwe_*_u64, wrappers.cpp:164-256): host rows in,
-        # host rows out, on the same keyset
+            # the direct route (memref_batched_bootstrap_lwe_*_u64, wrappers.cpp:164-256): host rows in,
+        # host rows out, on the same keyset, into one caller-owned output memref reused across calls
+        # (a fresh 33.6 MB array per call is unmapped the next call, and in this process that stalls
+        # the GPU queue ~25 ms on alternate calls: DESIGN.md §7)
         tlu_d = B.expand_lut(table, p.N, width)
-        R.batched_bootstrap(kset, p, cts, tlu_d)  # warm-up
+        res_d = R.batched_bootstrap(kset, p, cts, tlu_d)  # warm-up
         if os.environ.get("CONCRETE_HIP_BENCH_TIMELINE"):
             kset.set_timing(True)
         t0 = time.perf_counter()
         for _ in range(args.steps):
             t_call = time.perf_counter()
-            res_d = R.batched_bootstrap(kset, p, cts, tlu_d)
+            res_d = R.batched_bootstrap(kset, p, cts, tlu_d, out=res_d)
             if os.environ.get("CONCRETE_HIP_BENCH_TIMELINE"):
                 print("direct route timeline (dev, start, in, kernel, out, n):", kset.timeline().round(3).tolist(),
                       f"call wall {1e3 * (time.perf_counter() - t_call):.2f} ms", file=sys.stderr, flush=True)

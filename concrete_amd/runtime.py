@@ -66,11 +66,16 @@ class Keyset:
         self.close()
 
 
-def batched_bootstrap(ks: Keyset, p, cts: np.ndarray, tlu: np.ndarray, bsk_index=0) -> np.ndarray:
-    """memref_batched_bootstrap_lwe_hip_u64: (B, n+1) ciphertexts, one N-entry LUT -> (B, kN+1)."""
+def batched_bootstrap(ks: Keyset, p, cts: np.ndarray, tlu: np.ndarray, bsk_index=0, out=None) -> np.ndarray:
+    """memref_batched_bootstrap_lwe_hip_u64: (B, n+1) ciphertexts, one N-entry LUT -> (B, kN+1)
+    (into `out` when given: a C-contiguous uint64 array of that shape)."""
     cts = np.ascontiguousarray(cts, dtype=np.uint64)
     tlu = np.ascontiguousarray(tlu, dtype=np.uint64)
-    out = np.zeros((cts.shape[0], p.k * p.N + 1), dtype=np.uint64)
+    shape = (cts.shape[0], p.k * p.N + 1)
+    if out is None:
+        out = np.zeros(shape, dtype=np.uint64)
+    elif out.shape != shape or out.dtype != np.uint64 or not out.flags.c_contiguous:
+        raise ValueError(f"out must be a C-contiguous uint64 array of shape {shape}")
     ks.lib.memref_batched_bootstrap_lwe_hip_u64(*_desc(out), *_desc(cts), *_desc(tlu), p.n, p.N, p.level,
                                                 p.base_log, p.k, bsk_index, ks.h)
     return out

@@ -52,9 +52,11 @@ def test_batched_bootstrap(env, devices, nb):
     ks = keyset(env, devices)
     got = R.batched_bootstrap(ks, p, cts, tlu)
     again = R.batched_bootstrap(ks, p, cts, tlu)  # device key already resident
+    into = np.full_like(got, 0xDEAD)
+    R.batched_bootstrap(ks, p, cts, tlu, out=into)  # a caller-owned output memref, overwritten
     ks.close()
     ref, _ = O.pbs_batch(env["op"], cts, B.trivial_glwe(p, tlu)[None, :], fbsk=env["fcpu"])
-    assert np.array_equal(got, ref) and np.array_equal(again, ref)
+    assert np.array_equal(got, ref) and np.array_equal(again, ref) and np.array_equal(into, ref)
     dec = B.lwe_decrypt(env["glwe_sk"], got, p.big_n)
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
 

@@ -205,8 +205,12 @@ class Dfg:
     def put_uint64(self, s, v: int):
         self.lib.stream_emulator_put_uint64(s, int(v))
 
-    def get_batch(self, s, rows, cols) -> np.ndarray:
-        out = np.zeros((rows, cols), dtype=np.uint64)
+    def get_batch(self, s, rows, cols, out=None) -> np.ndarray:
+        """The stream's (rows, cols) batch, into `out` when given (C-contiguous uint64 of that shape)."""
+        if out is None:
+            out = np.zeros((rows, cols), dtype=np.uint64)
+        elif out.shape != (rows, cols) or out.dtype != np.uint64 or not out.flags.c_contiguous:
+            raise ValueError(f"out must be a C-contiguous uint64 array of shape {(rows, cols)}")
         self.lib.stream_emulator_get_memref_batch(s, out.ctypes.data, out.ctypes.data, 0, rows, cols, cols, 1)
         return out
 

@@ -91,3 +91,45 @@ def test_sdfg_ks_pbs_circuit_replay(client, tmp_path, devices):
     assert [B.decode(d, width) for d in dec] == [int(c["tables"][0][m + 1]) for m in c["msgs"]]
     dec4 = B.lwe_decrypt(c["glwe_sk"], out[3], p.big_n)
     assert [B.decode(d, width) for d in dec4] == [int(c["tables"][i][m]) for i, m in enumerate(c["msgs"])]
+
+
+def test_sdfg_python_driver_reruns_into_caller_buffer(client):
+    """concrete_amd.runtime.Dfg (the bench's route): KS -> PBS in this process, two puts of different
+    batches read back into one caller-owned array, each bit-exact vs the oracle."""
+    from concrete_amd import backend as B
+    from concrete_amd import runtime as R
+    from oracle import pyoracle as O
+    p = replace(B.CFG2, n=24)
+    width = 2
+    nb = 6
+    c = _case(p, nb, 700, width)
+    kset = R.Keyset([0])
+    kset.add_bsk(0, c["bsk"], p)
+    kset.add_ksk(0, c["ksk"], p)
+    ctx = 0x7A11
+    kset.bind(ctx)
+    g = R.Dfg()
+    s_in = g.batch_stream("in", R.TS_X86_TO_TOPO)
+    s_lut = g.memref_stream("lut", R.TS_X86_TO_TOPO)
+    s_mid = g.batch_stream("mid")
+    s_res = g.batch_stream("out", R.TS_TOPO_TO_X86)
+    g.keyswitch(s_in, s_mid, p, ctx)
+    g.bootstrap(s_mid, s_lut, s_res, p, ctx)
+    g.run()
+    g.put_memref(s_lut, c["luts"][0])
+    op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, ks_l=p.ks_level, ks_logB=p.ks_base_log)
+    fcpu = O.bsk_to_fourier(op, c["bsk"])
+    acc0 = B.trivial_glwe(p, c["luts"][0])[None, :]
+    out = np.full((nb, p.big_n + 1), 0xBEEF, dtype=np.uint64)
+    try:
+        for batch in (c["cts"], c["cts"][::-1].copy()):
+            g.put_batch(s_in, batch)
+            got = g.get_batch(s_res, nb, p.big_n + 1, out=out)
+            assert got is out
+            ref, _ = O.pbs_batch(op, O.keyswitch_batch(op, batch, c["ksk"]), acc0, fbsk=fcpu)
+            assert np.array_equal(out, ref)
+        with pytest.raises(ValueError):
+            g.get_batch(s_res, nb, p.big_n + 1, out=np.zeros((nb, p.big_n), dtype=np.uint64))
+    finally:
+        g.close()
+        kset.close()

@@ -123,6 +123,8 @@ def parse():
     ap.add_argument("--verify", type=int, default=8, help="rows checked bit-exactly against the oracle (rank 0)")
     ap.add_argument("--no-ks", action="store_true", help="skip the secondary keyswitch measurement")
     ap.add_argument("--no-sdfg", action="store_true", help="skip the stream-emulator (SDFG route) measurement")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the PCIe-inclusive leg (PMC passes: exactly warmup + steps PBS calls per process)")
     ap.add_argument("--check-gather", action="store_true",
                     help="rank 0 checks the whole gathered batch: every row decrypts to its rank's LUT[m], and "
                          "two rows per rank are bit-exact vs the oracle (inputs regenerated from the seeds)")
@@ -282,16 +284,18 @@ def main():
 
     # ---- end-to-end including PCIe: host inputs -> H2D -> PBS -> D2H -> host outputs (DESIGN.md §6;
     # never `value`, which is the device-resident rate)
-    h_in = torch.from_numpy(cts.view(np.int64)).pin_memory()
-    h_out = torch.empty((args.batch, p.lwe_out_size), dtype=torch.int64).pin_memory()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        d_in.copy_(h_in, non_blocking=True)
-        step()
-        h_out.copy_(d_out, non_blocking=True)
-    torch.cuda.synchronize()
-    e2e = args.batch * args.steps / (time.perf_counter() - t0)
+    e2e = None
+    if not args.no_e2e:
+        h_in = torch.from_numpy(cts.view(np.int64)).pin_memory()
+        h_out = torch.empty((args.batch, p.lwe_out_size), dtype=torch.int64).pin_memory()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            d_in.copy_(h_in, non_blocking=True)
+            step()
+            h_out.copy_(d_out, non_blocking=True)
+        torch.cuda.synchronize()
+        e2e = args.batch * args.steps / (time.perf_counter() - t0)
 
     # ---- the circuit-facing SDFG route (the default GPU route of a compiled circuit,
     # stream_emulator_*): a KS -> PBS table lookup on host memrefs, timed end to end per run (put
@@ -483,7 +487,7 @@ def main():
                          "dram": dram, "valu": valu},
             "cpu_baseline": cpu,
             "secondary": {"keyswitch": ks_res, "sdfg_route": sdfg_res,
-                          "pcie_inclusive_pbs_per_s": round(e2e * world, 1)},
+                          "pcie_inclusive_pbs_per_s": None if e2e is None else round(e2e * world, 1)},
             "checks": {"decrypt_ok": f"{ok_all}/{global_batch}", "bitexact_rows": args.verify, "gather": gather_check,
                        "bitexact": bitexact},
         }

@@ -315,6 +315,11 @@ int concrete_hip_pbs_supported(uint32_t glwe_dim, uint32_t polynomial_size, uint
              : 0;
 }
 
+int concrete_hip_keyswitch_supported(uint32_t level_count, uint32_t base_log, uint32_t input_lwe_dim,
+                                     uint32_t output_lwe_dim) {
+  return keyswitch_params_ok(level_count, base_log, input_lwe_dim, output_lwe_dim) ? 1 : 0;
+}
+
 uint32_t concrete_hip_bsk_limbs(uint32_t polynomial_size, uint32_t level_count, uint32_t base_log) {
   (void)base_log;
   return default_limbs(1, polynomial_size, level_count);

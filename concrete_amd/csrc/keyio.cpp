@@ -31,6 +31,7 @@
 #include <string.h>
 
 #include <exception>
+#include <initializer_list>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -82,6 +83,15 @@ class Reader {
     return w * 8;
   }
   const std::string& err() const { return err_; }
+  // Payload bytes copied so far by the whole parse.  Blobs may alias (several pointers to one Data),
+  // and a composite list may hold many keys: the sum over every key stays within the message's own
+  // size, so a crafted message cannot make the reader allocate more than it was given (capnp's
+  // per-message traversal limit plays this role).
+  bool charge_payload(uint64_t bytes) {
+    if (bytes > message_bytes() - copied_) return false;
+    copied_ += bytes;
+    return true;
+  }
 
   uint64_t word(uint32_t seg, uint64_t i) const { return w_[start_[seg] + i]; }
 
@@ -143,6 +153,7 @@ class Reader {
   }
 
  private:
+  uint64_t copied_ = 0;
   const uint64_t* w_;
   std::vector<uint64_t> start_, size_;
   std::string err_;
@@ -337,13 +348,16 @@ bool read_payload(Reader& r, const Reader::Struct& key, std::vector<uint64_t>& o
       return false;
     }
     total += parts[i].present ? parts[i].count : 0;
-    // blobs may alias (several pointers to one Data): cap the payload at the message's own size,
-    // so a crafted message cannot make the reader allocate more than it was given (capnp's
-    // traversal limit plays this role)
+    // blobs may alias (several pointers to one Data): cap the payload at the message's own size
     if (total > r.message_bytes()) {
       set_error("key payload: blobs total more bytes than the message holds (aliased blobs?)");
       return false;
     }
+  }
+  // ... and every key's payload together (many keys naming one payload)
+  if (!r.charge_payload(total)) {
+    set_error("key payload: the keys' payloads total more bytes than the message holds (aliased blobs?)");
+    return false;
   }
   if (total % 8) {
     set_error("key payload: %llu bytes is not a whole number of u64 words", (unsigned long long)total);
@@ -360,18 +374,44 @@ bool read_payload(Reader& r, const Reader::Struct& key, std::vector<uint64_t>& o
   return true;
 }
 
-uint64_t bsk_words(const concrete_hip_key_info& k) {  // concrete_cpu_bootstrap_key_size_u64
+// Key sizes from the message's dimensions.  Those are untrusted u32 fields: every product is
+// checked (a wrapped size would let a seeded key's decompressor write the real size through a
+// buffer sized by the wrapped one), and read_info bounds the dimensions first.
+bool mul_words(std::initializer_list<uint64_t> f, uint64_t& out) {
+  uint64_t p = 1;
+  for (uint64_t x : f)
+    if (__builtin_mul_overflow(p, x, &p)) return false;
+  out = p;
+  return p <= MAX_WORDS;
+}
+bool bsk_words(const concrete_hip_key_info& k, uint64_t& w) {  // concrete_cpu_bootstrap_key_size_u64
   const uint64_t g = (uint64_t)k.glwe_dim + 1;
-  return (uint64_t)k.input_lwe_dim * k.level_count * g * g * k.poly_size;
+  return mul_words({k.input_lwe_dim, k.level_count, g, g, k.poly_size}, w);
 }
-uint64_t seeded_bsk_words(const concrete_hip_key_info& k) {  // 2 seed words + seeded GGSW bodies
-  return 2 + (uint64_t)k.input_lwe_dim * k.level_count * ((uint64_t)k.glwe_dim + 1) * k.poly_size;
+bool seeded_bsk_words(const concrete_hip_key_info& k, uint64_t& w) {  // 2 seed words + seeded GGSW bodies
+  if (!mul_words({k.input_lwe_dim, k.level_count, (uint64_t)k.glwe_dim + 1, k.poly_size}, w)) return false;
+  w += 2;
+  return true;
 }
-uint64_t ksk_words(const concrete_hip_key_info& k) {  // concrete_cpu_keyswitch_key_size_u64
-  return (uint64_t)k.input_lwe_dim * k.level_count * ((uint64_t)k.output_lwe_dim + 1);
+bool ksk_words(const concrete_hip_key_info& k, uint64_t& w) {  // concrete_cpu_keyswitch_key_size_u64
+  return mul_words({k.input_lwe_dim, k.level_count, (uint64_t)k.output_lwe_dim + 1}, w);
 }
-uint64_t seeded_ksk_words(const concrete_hip_key_info& k) {
-  return 2 + (uint64_t)k.input_lwe_dim * k.level_count;
+bool seeded_ksk_words(const concrete_hip_key_info& k, uint64_t& w) {
+  if (!mul_words({k.input_lwe_dim, k.level_count}, w)) return false;
+  w += 2;
+  return true;
+}
+
+// Dimension bounds a key must meet before anything is sized from it: a decomposition of at most
+// 64 bits, LWE dimensions up to 2^20, GLWE dimension up to 64 and a power-of-two polynomial of
+// at most 2^17 coefficients (concrete's optimizer tables stay far inside these).
+bool key_dims_ok(const concrete_hip_key_info& k, bool is_bsk) {
+  if (k.level_count < 1 || k.base_log < 1 || (uint64_t)k.level_count * k.base_log > 64) return false;
+  if (k.input_lwe_dim < 1 || k.input_lwe_dim > (1u << 20)) return false;
+  if (is_bsk)
+    return k.glwe_dim >= 1 && k.glwe_dim <= 64 && k.poly_size >= 2 && k.poly_size <= (1u << 17) &&
+           (k.poly_size & (k.poly_size - 1)) == 0;
+  return k.output_lwe_dim >= 1 && k.output_lwe_dim <= (1u << 20);
 }
 
 bool read_info(Reader& r, const Reader::Struct& key, bool is_bsk, concrete_hip_key_info& k) {
@@ -408,7 +448,17 @@ bool read_info(Reader& r, const Reader::Struct& key, bool is_bsk, concrete_hip_k
     k.output_lwe_dim = r.u32(p, 28);
   }
   if (!read_modulus(r, p, k)) return false;
-  k.key_words = is_bsk ? bsk_words(k) : ksk_words(k);  // the standard-domain (decompressed) size
+  if (!key_dims_ok(k, is_bsk)) {
+    set_error("%s %u: dimensions out of range (level %u, base_log %u, glwe %u, N %u, n_in %u, n_out %u)",
+              is_bsk ? "bootstrap key" : "keyswitch key", k.id, k.level_count, k.base_log, k.glwe_dim, k.poly_size,
+              k.input_lwe_dim, k.output_lwe_dim);
+    return false;
+  }
+  // the standard-domain (decompressed) size
+  if (!(is_bsk ? bsk_words(k, k.key_words) : ksk_words(k, k.key_words))) {
+    set_error("%s %u: key size overflows", is_bsk ? "bootstrap key" : "keyswitch key", k.id);
+    return false;
+  }
   return r.ok();
 }
 
@@ -532,8 +582,8 @@ int expand(const concrete_hip_server_keyset::Key& k, bool is_bsk, uint64_t* dst,
     set_error("%s %u: unsupported compression %u", what, i.id, i.compression);
     return -2;
   }
-  const uint64_t need = is_bsk ? seeded_bsk_words(i) : seeded_ksk_words(i);
-  if (k.payload.size() != need) {
+  uint64_t need = 0;
+  if (!(is_bsk ? seeded_bsk_words(i, need) : seeded_ksk_words(i, need)) || k.payload.size() != need) {
     set_error("%s %u: seeded payload has %llu words, its parameters need %llu", what, i.id,
               (unsigned long long)k.payload.size(), (unsigned long long)need);
     return -3;
@@ -563,6 +613,24 @@ int expand(const concrete_hip_server_keyset::Key& k, bool is_bsk, uint64_t* dst,
 }  // namespace
 
 static int add_server_keyset(concrete_hip_keyset* ks, const concrete_hip_server_keyset* sk) {
+  // every key's parameters are checked against what the backend runs before any key is expanded
+  // (a decompressor runs only on a key the keyset would accept)
+  for (uint32_t i = 0; i < sk->bsk.size(); ++i) {
+    const concrete_hip_key_info& k = sk->bsk[i].info;
+    if (!concrete_hip_pbs_supported(k.glwe_dim, k.poly_size, k.level_count, k.base_log)) {
+      set_error("keyset_add_server_keyset: bootstrap key %u: unsupported parameters k=%u N=%u level=%u base_log=%u",
+                i, k.glwe_dim, k.poly_size, k.level_count, k.base_log);
+      return -2;
+    }
+  }
+  for (uint32_t i = 0; i < sk->ksk.size(); ++i) {
+    const concrete_hip_key_info& k = sk->ksk[i].info;
+    if (!concrete_hip_keyswitch_supported(k.level_count, k.base_log, k.input_lwe_dim, k.output_lwe_dim)) {
+      set_error("keyset_add_server_keyset: keyswitch key %u: unsupported parameters level=%u base_log=%u n_out=%u", i,
+                k.level_count, k.base_log, k.output_lwe_dim);
+      return -2;
+    }
+  }
   std::vector<uint64_t> buf;
   for (uint32_t i = 0; i < sk->bsk.size(); ++i) {
     const concrete_hip_key_info& k = sk->bsk[i].info;

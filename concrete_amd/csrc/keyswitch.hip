@@ -31,7 +31,15 @@ constexpr int KS_ICHUNK = 32;
 constexpr int KS_MAX_U = 4;                       // output words per thread per sample
 constexpr int KS_MAX_OUT = KS_MAX_U * KS_THREADS;  // output words per block (wider rows: windows in blockIdx.z)
 constexpr uint32_t KS_MAX_ROW = 1u << 16;           // n_out + 1 accepted (LWE dimensions are far below)
-constexpr int KS_MAX_L = 8;
+// Levels: any l with l * logB < 64 (the optimizer's keyswitches reach l = 23 at logB = 1,
+// v0_last_128 9-bit log-norm2 16).  The VALU kernel stages the digits of KS_DIG_ROWS (position,
+// level) pairs per chunk in LDS: KS_ICHUNK positions up to KS_ICHUNK_L levels, fewer positions
+// per chunk above that.
+constexpr int KS_ICHUNK_L = 8;
+constexpr int KS_DIG_ROWS = KS_ICHUNK * KS_ICHUNK_L;
+__host__ __device__ constexpr uint32_t ks_ichunk(uint32_t level) {
+  return level <= (uint32_t)KS_ICHUNK_L ? (uint32_t)KS_ICHUNK : (uint32_t)KS_DIG_ROWS / level;
+}
 // batches from this size take the MFMA path when it is exact (CONCRETE_HIP_KS_PATH: 0 = never,
 // 1 = always when exact; A/B and test switch)
 constexpr uint32_t KS_MFMA_MIN_BATCH = 64;
@@ -62,7 +70,8 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
   // The chunked paths need |d| <= 2^(logB-1) small anyway (int32); the 64-bit path keeps int64
   // digits, so any base_log with level * base_log < 64 is exact (a balanced digit can be +2^31).
   using dig_t = typename std::conditional<NCH == 0, int64_t, int32_t>::type;
-  __shared__ __attribute__((aligned(16))) dig_t dig[KS_ICHUNK][KS_MAX_L][KS_TILE];
+  __shared__ __attribute__((aligned(16))) dig_t dig[KS_DIG_ROWS][KS_TILE];  // [position in chunk][level]
+  const uint32_t ich = ks_ichunk(level);
   const uint32_t s0 = blockIdx.x * KS_TILE;
   const int tid = threadIdx.x;
   const uint32_t W = n_out + 1;
@@ -76,18 +85,18 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
 
   const uint32_t i_begin = SPLIT ? blockIdx.y * i_per_split : 0u;
   const uint32_t i_end = SPLIT ? min(n_in, i_begin + i_per_split) : n_in;
-  for (uint32_t i0 = i_begin; i0 < i_end; i0 += KS_ICHUNK) {
+  for (uint32_t i0 = i_begin; i0 < i_end; i0 += ich) {
     __syncthreads();
-    for (int e = tid; e < KS_TILE * KS_ICHUNK; e += KS_THREADS) {
-      const int s = e / KS_ICHUNK, ii = e % KS_ICHUNK;
+    for (uint32_t e = tid; e < KS_TILE * ich; e += KS_THREADS) {
+      const uint32_t s = e / ich, ii = e % ich;
       const uint32_t smp = s0 + s, i = i0 + ii;
       uint64_t a = 0ull;
       if (smp < num_samples && i < i_end) a = in[(in_idx ? in_idx[smp] : smp) * (uint64_t)(n_in + 1) + i];
       uint64_t st = decomp_init(a, nrep);
-      for (uint32_t t = 0; t < level; ++t) dig[ii][t][s] = (dig_t)decomp_next64(st, (int)base_log);
+      for (uint32_t t = 0; t < level; ++t) dig[ii * level + t][s] = (dig_t)decomp_next64(st, (int)base_log);
     }
     __syncthreads();
-    const uint32_t iend = min(KS_ICHUNK, (int)(i_end - i0));
+    const uint32_t iend = min(ich, i_end - i0);
     if constexpr (NCH > 0) {
       constexpr int FP = NCH == 3 ? 16 : KS_ICHUNK;  // positions per int32 block
       for (uint32_t b0 = 0; b0 < iend; b0 += FP) {
@@ -117,7 +126,7 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
               }
 #pragma unroll
               for (int s = 0; s < KS_TILE; ++s) {
-                const int32_t d = dig[ii][t][s];
+                const int32_t d = dig[ii * level + t][s];
 #pragma unroll
                 for (int c = 0; c < NCH; ++c) ca[s][u][c] += __mul24(d, kc[c]);
               }
@@ -144,7 +153,7 @@ keyswitch_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
             const uint32_t j = jz + tid + u * KS_THREADS;
             const uint64_t kv = j < W ? row[j] : 0ull;
 #pragma unroll
-            for (int s = 0; s < KS_TILE; ++s) acc[s][u] -= (uint64_t)dig[ii][t][s] * kv;
+            for (int s = 0; s < KS_TILE; ++s) acc[s][u] -= (uint64_t)dig[ii * level + t][s] * kv;
           }
         }
       }
@@ -690,9 +699,15 @@ static int keyswitch_mfma_launch(const KsArgs& a) {
   return 0;
 }
 
+// parameters the keyswitch kernels accept (64-bit arithmetic: the arguments may come from an
+// imported key message, keyio.cpp)
+bool keyswitch_params_ok(uint32_t level, uint32_t base_log, uint32_t n_in, uint32_t n_out) {
+  return level >= 1 && base_log >= 1 && (uint64_t)level * base_log < 64 && n_in >= 1 &&
+         (uint64_t)n_out + 1 <= KS_MAX_ROW;
+}
+
 int keyswitch_launch(const KsArgs& a) {
-  if (a.n_out + 1 > KS_MAX_ROW || a.level > (uint32_t)KS_MAX_L || a.level == 0 ||
-      a.level * a.base_log >= 64 || a.base_log == 0) {
+  if (!keyswitch_params_ok(a.level, a.base_log, a.n_in, a.n_out)) {
     set_error("unsupported keyswitch parameters: n_out=%u level=%u base_log=%u", a.n_out, a.level, a.base_log);
     return -2;
   }

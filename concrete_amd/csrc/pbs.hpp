@@ -53,7 +53,7 @@ struct KeyFormat {
 };
 constexpr int GEN_MAX_K = 8;       // GLWE dimension
 constexpr int GEN_MAX_LIMBS = 8;   // key limbs
-constexpr int GEN_MAX_TERMS = 24; // (k+1) * l * sub-digits per slot product
+constexpr int GEN_MAX_TERMS = 24; // key values per register chunk of the generic product (gen_mac_kernel)
 KeyFormat key_format(uint32_t k, uint32_t N, uint32_t level);                              // pbs_generic.hip
 bool generic_pbs_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log);            // pbs_generic.hip
 uint32_t generic_limb_bits(uint32_t k, uint32_t N, uint32_t level);                        // pbs_generic.hip
@@ -136,6 +136,7 @@ struct KsArgs {
   uint32_t n_in, n_out, base_log, level, num_samples;
 };
 int keyswitch_launch(const KsArgs& a);
+bool keyswitch_params_ok(uint32_t level, uint32_t base_log, uint32_t n_in, uint32_t n_out);  // keyswitch.hip
 // keyswitch.hip: drop the int8 key bytes cached for the KSK at device pointer p (freed on stream s,
 // or synchronously when s is null; untrack when p itself is being freed); returns the number of
 // entries released.  track_device_buffer: p's lifetime is visible to the backend (cuda_malloc_async,

@@ -77,16 +77,18 @@ double generic_error_bound(uint32_t k, uint32_t N, uint32_t level, uint32_t base
   return R * dnorm * (maxG * (4.0 * gamma + 3.0 * u) + gamma * gnorm) * 1.0001 + 4.0 * u * max_out;
 }
 
+// Levels up to 64 (l logB <= 64: the optimizer's rows reach l = 44 at logB = 1, v0_last_128).
 static bool generic_shape_ok(uint32_t k, uint32_t N, uint32_t level) {
-  if (k < 1 || k > (uint32_t)GEN_MAX_K || level < 1 || level > 16) return false;
+  if (k < 1 || k > (uint32_t)GEN_MAX_K || level < 1 || level > 64) return false;
   return N >= 256 && N <= 16384 && (N & (N - 1)) == 0;
 }
 
 // Limb width b for (k, N, l): the widest b whose bound holds for digits of up to 2b bits
-// (T <= 2 sub-digits), which covers every logB the optimizer pairs with these sizes.
+// (T <= 2 sub-digits), which covers every logB the optimizer pairs with these sizes; a digit is
+// never wider than 64 / l bits (l logB <= 64), so many-level keys get wider limbs.
 uint32_t generic_limb_bits(uint32_t k, uint32_t N, uint32_t level) {
   for (uint32_t b = 24; b >= 8; --b)
-    if (generic_error_bound(k, N, level, 2 * b, b, 0.0) < 0.25) return b;
+    if (generic_error_bound(k, N, level, std::min<uint32_t>(2 * b, 64 / level), b, 0.0) < 0.25) return b;
   return 0;
 }
 
@@ -110,8 +112,8 @@ KeyFormat key_format(uint32_t k, uint32_t N, uint32_t level) {
 bool generic_pbs_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
   const KeyFormat f = generic_key_format(k, N, level);
   if (f.kind != KeyKind::GENERIC || base_log < 1 || (uint64_t)level * base_log > 64) return false;
-  const uint32_t T = (base_log + f.bits - 1) / f.bits;
-  if ((k + 1) * level * T > (uint32_t)GEN_MAX_TERMS) return false;
+  // any number of product terms (k + 1) l T: the register-tiled products cover the optimizer's
+  // log-norm2-0 shapes, gen_mac_kernel the rest in chunks of GEN_MAX_TERMS
   return generic_error_bound(k, N, level, base_log, f.bits, 0.0) < 0.25;
 }
 
@@ -959,6 +961,8 @@ struct MacArgs {
 #define MAC_CTS 16  // ciphertexts per block (key values loaded once per tile)
 #endif
 
+// Any number of terms: the key values of GEN_MAX_TERMS terms at a time in registers, the slot
+// sum carried through Y between the chunks (each thread re-reads only what it wrote).
 __global__ void __launch_bounds__(256) gen_mac_kernel(MacArgs a) {
   const uint32_t f = blockIdx.x * 256 + threadIdx.x;
   const uint32_t K1 = a.k + 1, L = a.limbs, T = a.subs;
@@ -966,28 +970,33 @@ __global__ void __launch_bounds__(256) gen_mac_kernel(MacArgs a) {
   const uint32_t terms = K1 * a.level * T;
   const uint64_t M = a.M;
   if (f >= M) return;
-  cplx kv[GEN_MAX_TERMS];
-#pragma unroll
-  for (int x = 0; x < GEN_MAX_TERMS; ++x) {
-    kv[x] = {0.0, 0.0};
-    if ((uint32_t)x < terms) {
-      const uint32_t t = x % T, rq = x / T;  // x = (r l + q) T + t
-      if (m >= t && m - t < L) kv[x] = a.G[((((uint64_t)a.i * K1 + c) * L + (m - t)) * K1 * a.level + rq) * M + f];
-    }
-  }
   const uint32_t ct0 = blockIdx.z * MAC_CTS;
-  for (uint32_t ct = ct0; ct < ct0 + MAC_CTS && ct < a.count; ++ct) {
-    const cplx* Xct = a.X + (uint64_t)ct * terms * M + f;
-    cplx y = {0.0, 0.0};
+#pragma unroll 1
+  for (uint32_t x0 = 0; x0 < terms; x0 += GEN_MAX_TERMS) {
+    cplx kv[GEN_MAX_TERMS];
 #pragma unroll
     for (int x = 0; x < GEN_MAX_TERMS; ++x) {
-      if ((uint32_t)x < terms) {
-        const cplx xv = Xct[(uint64_t)x * M];
-        y.re = __builtin_fma(xv.re, kv[x].re, __builtin_fma(-xv.im, kv[x].im, y.re));
-        y.im = __builtin_fma(xv.re, kv[x].im, __builtin_fma(xv.im, kv[x].re, y.im));
+      kv[x] = {0.0, 0.0};
+      const uint32_t xx = x0 + x;
+      if (xx < terms) {
+        const uint32_t t = xx % T, rq = xx / T;  // xx = (r l + q) T + t
+        if (m >= t && m - t < L) kv[x] = a.G[((((uint64_t)a.i * K1 + c) * L + (m - t)) * K1 * a.level + rq) * M + f];
       }
     }
-    a.Y[(((uint64_t)ct * K1 + c) * L + m) * M + f] = y;
+    for (uint32_t ct = ct0; ct < ct0 + MAC_CTS && ct < a.count; ++ct) {
+      const cplx* Xct = a.X + (uint64_t)ct * terms * M + f;
+      cplx* Yp = a.Y + (((uint64_t)ct * K1 + c) * L + m) * M + f;
+      cplx y = x0 ? *Yp : cplx{0.0, 0.0};
+#pragma unroll
+      for (int x = 0; x < GEN_MAX_TERMS; ++x) {
+        if (x0 + x < terms) {
+          const cplx xv = Xct[(uint64_t)(x0 + x) * M];
+          y.re = __builtin_fma(xv.re, kv[x].re, __builtin_fma(-xv.im, kv[x].im, y.re));
+          y.im = __builtin_fma(xv.re, kv[x].im, __builtin_fma(xv.im, kv[x].re, y.im));
+        }
+      }
+      *Yp = y;
+    }
   }
 }
 

@@ -431,7 +431,7 @@ int concrete_hip_keyset_add_bsk(concrete_hip_keyset* ks, uint32_t bsk_index, con
       set_error("keyset_add_bsk: index %u already resident", bsk_index);
       return -3;
     }
-  const uint64_t len = (uint64_t)input_lwe_dim * level * (glwe_dim + 1) * (glwe_dim + 1) * poly_size;
+  const uint64_t len = (uint64_t)input_lwe_dim * level * ((uint64_t)glwe_dim + 1) * ((uint64_t)glwe_dim + 1) * poly_size;
   e->host.assign(bsk, bsk + len);
   e->n = input_lwe_dim, e->k = glwe_dim, e->level = level, e->base_log = base_log, e->N = poly_size;
   return 0;
@@ -439,9 +439,15 @@ int concrete_hip_keyset_add_bsk(concrete_hip_keyset* ks, uint32_t bsk_index, con
 
 int concrete_hip_keyset_add_ksk(concrete_hip_keyset* ks, uint32_t ksk_index, const uint64_t* ksk, uint32_t level,
                                 uint32_t base_log, uint32_t input_lwe_dim, uint32_t output_lwe_dim) {
-  if (!ks || !ksk || level == 0 || base_log == 0 || level * base_log >= 64 || output_lwe_dim + 1 > (1u << 16)) {
+  if (!ks || !ksk) {
     set_error("keyset_add_ksk: bad argument");
     return -3;
+  }
+  // 64-bit checks: the parameters may come from an imported key message (keyio.cpp)
+  if (!keyswitch_params_ok(level, base_log, input_lwe_dim, output_lwe_dim)) {
+    set_error("keyset_add_ksk: unsupported parameters level=%u base_log=%u n_in=%u n_out=%u", level, base_log,
+              input_lwe_dim, output_lwe_dim);
+    return -2;
   }
   KskEntry* e = entry(ks->ksk, ksk_index, ks->m, true);
   std::lock_guard<std::mutex> g(e->m);
@@ -450,7 +456,7 @@ int concrete_hip_keyset_add_ksk(concrete_hip_keyset* ks, uint32_t ksk_index, con
       set_error("keyset_add_ksk: index %u already resident", ksk_index);
       return -3;
     }
-  const uint64_t len = (uint64_t)input_lwe_dim * level * (output_lwe_dim + 1);
+  const uint64_t len = (uint64_t)input_lwe_dim * level * ((uint64_t)output_lwe_dim + 1);
   e->host.assign(ksk, ksk + len);
   e->level = level, e->base_log = base_log, e->n_in = input_lwe_dim, e->n_out = output_lwe_dim;
   return 0;

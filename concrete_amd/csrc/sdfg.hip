@@ -169,12 +169,13 @@ Proc* make(void* dfg, ProcKind k, void* sin1, void* sin2, void* sout) {
 
 // ---- scheduling ------------------------------------------------------------------------------
 
-// newest put reaching s (memoised per get)
+// newest put reaching s (memoised per get).  A produced stream counts its own puts too: a value
+// put on an intermediate stream makes every consumer computed before it stale.
 uint64_t eff(Stream* s, std::unordered_map<Stream*, uint64_t>& memo) {
   if (!s->producer) return s->version;
   auto it = memo.find(s);
   if (it != memo.end()) return it->second;
-  uint64_t v = 0;
+  uint64_t v = s->version;
   for (Stream* i : s->producer->in)
     if (i) v = std::max(v, eff(i, memo));
   memo[s] = v;
@@ -287,19 +288,36 @@ Plan plan_for(Stream* target) {
   return P;
 }
 
+// The registered key of a KS / PBS process must have the process's parameters (as the memref
+// route asserts, runtime.hip run_batched_pbs / run_batched_ks): the device key's layout and size
+// follow them, so a mismatch would read past the key or reinterpret it.
 void check_proc(const Proc* p, const Plan& P) {
   const uint64_t w0 = P.width.at(p->in[0]);
   switch (p->kind) {
-    case P_KS:
+    case P_KS: {
       RT_ASSERT(w0 == (uint64_t)p->n_in + 1);
       RT_ASSERT(P.width.at(p->out) == (uint64_t)p->n_out + 1);
+      KskEntry* e = keyset_ksk_entry(keyset_of_context(p->ctx), p->key_index);
+      if (!e) rt_die("stream_emulator: keyswitch key index %u not registered", p->key_index);
+      if (e->level != p->level || e->base_log != p->base_log || e->n_in != p->n_in || e->n_out != p->n_out)
+        rt_die("stream_emulator: keyswitch key %u is (l=%u, logB=%u, %u -> %u), the process asks (l=%u, logB=%u, "
+               "%u -> %u)", p->key_index, e->level, e->base_log, e->n_in, e->n_out, p->level, p->base_log, p->n_in,
+               p->n_out);
       break;
-    case P_PBS:
+    }
+    case P_PBS: {
       // GPUDFG.cpp:1116
       RT_ASSERT(p->output_size == p->glwe * p->poly + 1);
       RT_ASSERT(w0 == (uint64_t)p->n_in + 1);
       RT_ASSERT(P.width.at(p->in[1]) == p->poly);
+      BskEntry* e = keyset_bsk_entry(keyset_of_context(p->ctx), p->key_index);
+      if (!e) rt_die("stream_emulator: bootstrap key index %u not registered", p->key_index);
+      if (e->n != p->n_in || e->k != p->glwe || e->N != p->poly || e->level != p->level || e->base_log != p->base_log)
+        rt_die("stream_emulator: bootstrap key %u is (n=%u, k=%u, N=%u, l=%u, logB=%u), the process asks (n=%u, k=%u, "
+               "N=%u, l=%u, logB=%u)", p->key_index, e->n, e->k, e->N, e->level, e->base_log, p->n_in, p->glwe,
+               p->poly, p->level, p->base_log);
       break;
+    }
     case P_ADD:
       RT_ASSERT(P.width.at(p->in[1]) == w0);
       break;

@@ -114,6 +114,10 @@ const char *concrete_hip_last_error(void);
 /* 1 if (k, N, level, base_log) has a compiled PBS kernel (wide digits: the general path), else 0 */
 int concrete_hip_pbs_supported(uint32_t glwe_dim, uint32_t polynomial_size, uint32_t level_count,
                                uint32_t base_log);
+/* 1 if the batched keyswitch runs (level, base_log, n_in -> n_out): level * base_log < 64,
+ * n_out + 1 <= 65536; else 0 (round 4) */
+int concrete_hip_keyswitch_supported(uint32_t level_count, uint32_t base_log, uint32_t input_lwe_dim,
+                                     uint32_t output_lwe_dim);
 /* number of exact key limbs the device format uses for these parameters */
 uint32_t concrete_hip_bsk_limbs(uint32_t polynomial_size, uint32_t level_count, uint32_t base_log);
 /* device key format of (k, N, l): 0 unsupported, 1 / 2 the N = 1024 / 2048 (k = 1) kernels' layouts,

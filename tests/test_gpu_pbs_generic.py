@@ -323,3 +323,48 @@ def test_configs4_atomic_pattern_8bit(B, oracle, torch_cuda):
     assert np.array_equal(B.to_host(d_lut), host_luts)
     dec = B.lwe_decrypt(glwe_sk, B.to_host(out), p.big_n)
     assert [B.decode(d, bits, sg) for d, (_, sg) in zip(dec, expect)] == [e for e, _ in expect]
+
+
+# v0_last_128 rows at non-zero log norm2 (tests/golden/v0_last_128_rows.json): per width the row
+# with the most decomposition levels (the caps lifted in round 4: many-level keys, (k + 1) l T
+# product terms past the register-tiled products), plus the 8-bit log-norm2-17 row (14 levels of
+# 3 bits).  (label, k, N, n reduced, l, logB, message bits, full n, ks_l, ks_logB)
+LN2_CASES = [
+    ("1bit_ln2_30", 4, 512, 8, 22, 2, 1, 625, 12, 1),
+    ("2bit_ln2_29", 4, 512, 6, 44, 1, 2, 629, 12, 1),
+    ("3bit_ln2_27", 4, 512, 8, 22, 2, 3, 690, 7, 2),
+    ("4bit_ln2_26", 2, 1024, 6, 44, 1, 4, 727, 14, 1),
+    ("5bit_ln2_24", 1, 2048, 6, 22, 2, 5, 806, 8, 2),
+    ("6bit_ln2_22", 1, 4096, 4, 42, 1, 6, 833, 17, 1),
+    ("7bit_ln2_20", 1, 8192, 3, 42, 1, 7, 898, 18, 1),
+    ("8bit_ln2_17", 1, 16384, 2, 14, 3, 8, 1007, 11, 2),
+    ("8bit_ln2_18", 1, 16384, 2, 41, 1, 8, 985, 21, 1),
+]
+
+
+@pytest.mark.parametrize("case", LN2_CASES, ids=[c[0] for c in LN2_CASES])
+def test_optimizer_rows_at_nonzero_log_norm2(B, oracle, torch_cuda, case):
+    """PBS bit-exact vs the exact oracle (n reduced) and the row's keyswitch into its full n
+    bit-exact, at optimizer rows whose decompositions have up to 44 levels."""
+    label, k, N, n, l, logB, width, n_full, ks_l, ks_logB = case
+    p, glwe_sk, bsk, fbsk, cts, acc, table, msgs, got, resid = run_case(
+        B, oracle, torch_cuda, (label, k, N, n, l, logB, width), 7600, batch=4)
+    op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
+    ref, _ = oracle.pbs_batch(op, cts, acc[None, :], bsk=bsk, mode=oracle.MODE_KARATSUBA)
+    assert np.array_equal(got, ref), f"{label}: GPU differs from the exact oracle"
+    assert resid < 0.5
+    dec = B.lwe_decrypt(glwe_sk, got, p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+    # the row's keyswitch (ks_l, ks_logB) into the row's full n, from up to 4096 input words (the
+    # 8-bit row's whole 16384 x 21 x 986-word key would be 2.7 GB)
+    kN = min(k * N, 4096)
+    pk = B.PbsParams(n=n_full, k=1, N=kN, level=l, base_log=logB, ks_level=ks_l, ks_base_log=ks_logB)
+    lwe_sk = B.binary_key(n_full, 7610)
+    ksk = B.ksk_generate(pk, B.binary_key(kN, 7611), lwe_sk, 7620)
+    rng = np.random.RandomState(ks_l)
+    big = rng.randint(0, 2 ** 63, size=(5, pk.big_n + 1), dtype=np.int64).astype(np.uint64) * np.uint64(2) + \
+        np.uint64(1)
+    out = B.keyswitch(pk, B.to_device(ksk, "cuda:0"), B.to_device(big, "cuda:0"))
+    torch_cuda.cuda.synchronize()
+    opk = oracle.Params(n=n_full, k=1, N=kN, l=l, logB=logB, ks_l=ks_l, ks_logB=ks_logB)
+    assert np.array_equal(B.to_host(out), oracle.keyswitch_batch(opk, big, ksk))

@@ -130,6 +130,13 @@ def test_sdfg_python_driver_reruns_into_caller_buffer(client):
             assert np.array_equal(out, ref)
         with pytest.raises(ValueError):
             g.get_batch(s_res, nb, p.big_n + 1, out=np.zeros((nb, p.big_n), dtype=np.uint64))
+        # a put on the intermediate stream makes the downstream result stale (eff() had
+        # ignored puts on produced streams, so this get returned the previous run's outputs)
+        small = O.keyswitch_batch(op, c["cts"], c["ksk"])
+        g.put_batch(s_mid, small)
+        got = g.get_batch(s_res, nb, p.big_n + 1, out=out)
+        ref, _ = O.pbs_batch(op, small, acc0, fbsk=fcpu)
+        assert np.array_equal(got, ref)
     finally:
         g.close()
         kset.close()

@@ -129,3 +129,23 @@ def test_committed_pmc_records_match_the_kernel_sources():
     for config in ("cfg2", "cfg4"):
         assert bench.pmc_traffic(4096, config)[0], f"no PMC traffic record for the current {config} sources"
         assert bench.pmc_f64_flop(4096, config)[0], f"no PMC f64 record for the current {config} sources"
+
+
+def test_optimizer_table_coverage():
+    """Every row of the optimizer's reference table (tests/golden/v0_last_128_rows.json, from
+    v0-parameters/ref/v0_last_128 by tests/golden/make_v0_rows.py) from 1 to 8 bits, at every log
+    norm2, has a PBS (k, N, br_l, br_b) and a keyswitch (ks_l, ks_b, kN -> n) the backend runs
+    exactly; the 9- and 10-bit rows (N = 2^15, 2^16) are refused, as DESIGN.md states."""
+    import json
+
+    L = _native.lib()
+    rows = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "v0_last_128_rows.json")))["rows"]
+    assert len(rows) == 235
+    runs = lambda r: (L.concrete_hip_pbs_supported(r["k"], r["N"], r["br_l"], r["br_b"]) == 1 and  # noqa: E731
+                      L.concrete_hip_keyswitch_supported(r["ks_l"], r["ks_b"], r["k"] * r["N"], r["n"]) == 1)
+    small = [r for r in rows if r["bits"] <= 8]
+    assert len(small) == 204
+    assert [r for r in small if not runs(r)] == []
+    big = [r for r in rows if r["bits"] > 8]
+    assert all(r["N"] >= 32768 for r in big)
+    assert [r for r in big if L.concrete_hip_keyswitch_supported(r["ks_l"], r["ks_b"], r["k"] * r["N"], r["n"]) != 1] == []

@@ -340,3 +340,62 @@ def test_aliased_blobs_cannot_amplify_the_payload():
     assert len(data) < 64 * 1024  # 16 MB of payload if the aliases were followed
     assert _deser_rc(data, root=2) < 0
     assert "aliased" in _native.lib().concrete_hip_last_error().decode()
+
+
+def test_many_keys_sharing_one_payload_are_refused():
+    """the aliasing cap was per key, so a composite list of K keys naming one payload
+    could allocate ~K x message bytes; the budget is now one per parse."""
+    m = K._Message("flat")
+    srv = m.new_struct(0, 3)
+    m.set_root(srv)
+    n_keys = 64
+    lst, elems = m.new_struct_list(n_keys, 0, 2)
+    m.set_list_ptr(srv, 0, lst)
+    info = K.bsk_info(_P)
+    inf = m.new_struct(K.INFO_WORDS, 1)
+    par = m.new_struct(K.BSK_PARAMS_WORDS, 1)
+    for name, off in K.BSK_PARAMS_OFF.items():
+        fmt = "d" if name == "variance" else ("H" if name == "key_type" else "I")
+        m.set_data(par, off, fmt, getattr(info, name))
+    m.set_struct_ptr(inf, 0, par)
+    pl = m.new_struct(0, 1)
+    plist = m.new_ptr_list(1)
+    m.set_list_elem_ptr(plist, 0, m.new_data(b"\x02" * 4096))
+    m.set_list_ptr(pl, 0, plist)
+    for el in elems:  # every key: the same info, the same 4 KB payload
+        m.set_struct_ptr(el, 0, inf)
+        m.set_struct_ptr(el, 1, pl)
+    data = m.to_bytes()
+    assert len(data) < 8 * 1024  # 256 KB of payload copies if every alias were followed
+    assert _deser_rc(data) < 0
+    assert "payloads total" in _native.lib().concrete_hip_last_error().decode()
+
+
+@pytest.mark.parametrize("dims,msg", [
+    # u32 products that wrapped to a tiny size before round 4 (ADVICE r3)
+    ({"input_lwe_dim": 1 << 31, "level_count": 2, "base_log": 2, "glwe_dim": 1, "poly_size": 4}, "out of range"),
+    ({"input_lwe_dim": 8, "level_count": 1 << 31, "base_log": 2, "glwe_dim": 1, "poly_size": 4}, "out of range"),
+    ({"input_lwe_dim": 8, "level_count": 2, "base_log": 7, "glwe_dim": 1, "poly_size": 3}, "out of range"),
+    # within every per-dimension bound, but the product exceeds the size bound
+    ({"input_lwe_dim": 1 << 20, "level_count": 16, "base_log": 4, "glwe_dim": 64, "poly_size": 1 << 17}, "overflows"),
+])
+def test_key_dimensions_are_bounded_before_anything_is_sized(dims, msg):
+    """A seeded key whose dimensions make its size wrap would have passed the 2-word payload check
+    and let the decompressor write the real size through a short buffer: the dimensions are now
+    bounded and the sizes computed with overflow checks when the message is parsed."""
+    info = K.KeyInfo(**{**K.bsk_info(_P, compression=1).__dict__, **dims})
+    data = K.serialize_server_keyset([(info, np.array([1, 2], np.uint64))])
+    assert _deser_rc(data) < 0
+    assert msg in _native.lib().concrete_hip_last_error().decode()
+
+
+def test_keyswitch_support_is_checked_before_expansion():
+    """keyset_add_server_keyset checks every key's parameters against the kernels before any key is
+    expanded (a decompressor never runs for a key the keyset would refuse)."""
+    lib = _native.lib()
+    assert lib.concrete_hip_keyswitch_supported(_P.ks_level, _P.ks_base_log, _P.big_n, _P.n) == 1
+    assert lib.concrete_hip_keyswitch_supported(23, 1, 16384, 1006) == 1  # v0_last_128 9-bit log-norm2 16
+    assert lib.concrete_hip_keyswitch_supported(16, 4, 1024, 600) == 0   # 64 bits of digits
+    assert lib.concrete_hip_keyswitch_supported(2, 4, 1024, 65535) == 1
+    assert lib.concrete_hip_keyswitch_supported(2, 4, 1024, 65536) == 0
+    assert lib.concrete_hip_keyswitch_supported(2, 4, 1024, 0xFFFFFFFF) == 0  # n_out + 1 wraps in u32

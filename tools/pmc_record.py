@@ -22,14 +22,27 @@ sys.path.insert(0, ROOT)
 from bench import kernel_source_hash  # noqa: E402
 
 KERNEL = {"cfg2": "pbs1024", "cfg4": "pbs2048"}
+# the general path (optB configs) runs several launches per PBS call (pbs_generic.hip): the record
+# sums every gen_* dispatch of the process's single call (tools/pmc.sh: --steps 1 --warmup 0 --no-e2e),
+# except the once-per-key conversion
+GENERIC_PREFIX = "gen_"
+GENERIC_SKIP = ("gen_convert",)
 
 
 def collect(src, kname):
     vals = {}
+    generic = kname.startswith("opt")
     for f in glob.glob(f"{src}/**/run_counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
-            if kname in row.get("Kernel_Name", ""):
+            name = row.get("Kernel_Name", "")
+            if generic:
+                hit = name.startswith(GENERIC_PREFIX) and not any(x in name for x in GENERIC_SKIP)
+            else:
+                hit = kname in name
+            if hit:
                 vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+    if generic:  # one PBS call = the sum of its launches
+        return {k: sum(v) for k, v in vals.items()}
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
@@ -37,7 +50,7 @@ def main():
     src, dst, config, batch = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
     kname = KERNEL.get(config, config)
     v = collect(src, kname)
-    rec = {"kernel": kname, "config": config, "batch": batch, "source_hash": kernel_source_hash(config), "pmc_dir": src,
+    rec = {"kernel": kname if not kname.startswith("opt") else "gen_* (sum over one PBS call)", "config": config, "batch": batch, "source_hash": kernel_source_hash(config), "pmc_dir": src,
            "counters": v}
     if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
         rec["traffic_bytes"] = int(round((2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024))

@@ -25,7 +25,7 @@ KERNEL = {"cfg2": "pbs1024", "cfg4": "pbs2048"}
 # the general path (optB configs) runs several launches per PBS call (pbs_generic.hip): the record
 # sums every gen_* dispatch of the process's single call (tools/pmc.sh: --steps 1 --warmup 0 --no-e2e),
 # except the once-per-key conversion
-GENERIC_PREFIX = "gen_"
+GENERIC_PREFIX = "chip::gen::gen_"
 GENERIC_SKIP = ("gen_convert",)
 
 
@@ -36,7 +36,7 @@ def collect(src, kname):
         for row in csv.DictReader(open(f)):
             name = row.get("Kernel_Name", "")
             if generic:
-                hit = name.startswith(GENERIC_PREFIX) and not any(x in name for x in GENERIC_SKIP)
+                hit = GENERIC_PREFIX in name and not any(x in name for x in GENERIC_SKIP)
             else:
                 hit = kname in name
             if hit:

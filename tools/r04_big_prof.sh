@@ -10,10 +10,14 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
+# heartbeat: a PMC pass over the 8-bit row runs minutes without printing
+( while sleep 30; do date +%T >> $O/heartbeat.log; done ) &
+HB=$!
+trap "kill $HB" EXIT
 for C in $CFGS; do
   echo "trace $C $(date +%T)"
   cd /tmp
-  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$C -o run -- \
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$C -o run -- \
     python3 $R/bench.py --config $C --steps 2 --warmup 1 --no-cpu-baseline --verify 0 --no-ks --no-e2e \
     > $O/trace_$C.log 2>&1
   cd $R

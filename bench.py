@@ -1,10 +1,11 @@
 """Benchmark: batched programmable bootstrap (PBS) throughput on MI355X.
 
 Workload = BASELINE.json metric config: N=1024, k=1, n=630, l=3, logB=7 (configs[1]'s
-parameters) at batch 4096 per GPU.  A step = one batched PBS (one kernel launch) over the
-rank's 4096 resident LWE ciphertexts.  Multi-GPU = weak scaling: every rank bootstraps its
-own 4096-ciphertext shard; the device-format bootstrapping key is produced once on rank 0
-and broadcast over RCCL (xGMI); there is no collective in the data path.
+parameters) at the metric's batch of 4096.  A step = one batched PBS (one kernel launch per
+rank) over resident LWE ciphertexts.  Multi-GPU = the metric's whole-node batch of 4096 split
+into contiguous shards (strong scaling: 512 per GPU on 8 GPUs), with weak scaling (4096 per
+GPU) measured as a secondary row; the device-format bootstrapping key is produced once on
+rank 0 and broadcast over RCCL (xGMI); there is no collective in the data path.
 
 Usage: python bench.py [--gpus N --steps K --warmup W]
        (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
@@ -110,10 +111,13 @@ def parse():
                          "optB: the optimizer's B-bit row of v0_last_128 (backend.OPTIMIZER_SETS)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=4096, help="PBS per GPU per step (weak scaling)")
+    ap.add_argument("--batch", type=int, default=4096, help="PBS per GPU per step (weak scaling: --weak)")
     ap.add_argument("--global-batch", type=int, default=0,
                     help="strong scaling: this many PBS per step for the whole job, split over the ranks "
-                         "(e.g. the metric's whole-node batch 4096 = 512 per GPU on 8 GPUs)")
+                         "(default for cfg2: the metric's whole-node batch 4096, i.e. 512 per GPU on 8 GPUs)")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling as the main line: --batch PBS per GPU (cfg2 N>1 reports it as "
+                         "secondary.weak_scaling anyway)")
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="PBS in the bounded CPU-baseline sample (default: cfg2 4096 = one full batch, "
                          "cfg4 1024; ~10-20 s)")
@@ -146,6 +150,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # The metric is "PBS/sec (whole node) at N=1024 batch=4096": for cfg2 the job's batch is 4096
+    # however many GPUs share it (strong scaling, BASELINE.json); weak scaling (4096 per GPU) is
+    # measured as a secondary row on N > 1.
+    if args.global_batch == 0 and args.config == "cfg2" and not args.weak:
+        args.global_batch = 4096
     strong = args.global_batch > 0
     if strong:
         # contiguous shards of the job's batch (the first global % world ranks get one more)
@@ -239,6 +248,31 @@ def main():
         total_done, global_batch = int(t[0]), int(t[1])
     else:
         global_batch = args.batch
+
+    # ---- weak scaling (cfg2, N > 1): every rank its own full batch of 4096, same timing rule
+    weak_res = None
+    if strong and world > 1 and args.config == "cfg2" and not args.weak:
+        _, _, cts_w = shard_inputs(rank, 4096)
+        d_in_w = B.to_device(cts_w, dev)
+        d_out_w = torch.empty((4096, p.lwe_out_size), dtype=torch.int64, device=dev)
+        for _ in range(args.warmup):
+            B.pbs(p, fbsk, d_in_w, d_lut, out=d_out_w)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            B.pbs(p, fbsk, d_in_w, d_lut, out=d_out_w)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        weak_res = {"metric": f"PBS/sec (whole node), 4096 per GPU ({4096 * world} per step)",
+                    "value": round(4096 * world * args.steps / float(t[0]), 1), "unit": "PBS/s",
+                    "ms_per_step": round(float(t[0]) / args.steps * 1e3, 3), "batch_per_gpu": 4096,
+                    "scaling": "weak"}
+        del d_in_w, d_out_w
 
     # ---- secondary row: batched keyswitch kN -> n of this batch, after the PBS
     ks_res = None
@@ -486,7 +520,7 @@ def main():
                          "kernel_ms": round(kern_ms, 3), "bytes_per_pbs": bytes_per_pbs,
                          "dram": dram, "valu": valu},
             "cpu_baseline": cpu,
-            "secondary": {"keyswitch": ks_res, "sdfg_route": sdfg_res,
+            "secondary": {"keyswitch": ks_res, "sdfg_route": sdfg_res, "weak_scaling": weak_res,
                           "pcie_inclusive_pbs_per_s": None if e2e is None else round(e2e * world, 1)},
             "checks": {"decrypt_ok": f"{ok_all}/{global_batch}", "bitexact_rows": args.verify, "gather": gather_check,
                        "bitexact": bitexact},

@@ -117,6 +117,34 @@ int take_device_status(int gpu) {
   return -4;
 }
 
+// Stream-ordered form: the word is read on s after the work issued there (the runtime's slice and
+// shard streams), so concurrent calls on other streams are not waited for.  The word is per device:
+// a flag raised by a launch on another stream is reported by whichever call reads it first (the
+// outputs of that launch are wrong either way; the call that reads it aborts).
+int take_stream_status(int gpu, hipStream_t s, uint32_t* h) {
+  uint32_t* w;
+  {
+    std::lock_guard<std::mutex> g(g_status_mu);
+    w = (gpu >= 0 && gpu < STATUS_MAX_DEV) ? g_status[gpu] : nullptr;
+  }
+  if (!w) {  // no PBS kernel has run on this device: only the stream's own work to wait for
+    CHIP_CHECK(hipStreamSynchronize(s));
+    return 0;
+  }
+  CHIP_CHECK(hipMemcpyAsync(h, w, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  CHIP_CHECK(hipStreamSynchronize(s));
+  const uint32_t v = *h;
+  if (v == 0) return 0;
+  CHIP_CHECK(hipMemsetAsync(w, 0, sizeof(uint32_t), s));
+  CHIP_CHECK(hipStreamSynchronize(s));
+  if (v & DEV_STATUS_SYNC_TIMEOUT) {
+    set_error("device %d: a PBS wave synchronisation exceeded its spin bound; that launch's outputs are wrong",
+              gpu);
+    return -4;
+  }
+  set_error("device %d: status word 0x%x", gpu, v);
+  return -4;
+}
 
 // ---- general-format companion keys (pbs_needs_generic_key) ------------------------------
 // A primary device key in a hand-tuned kernel's format (N = 1024 / 2048) whose standard-domain

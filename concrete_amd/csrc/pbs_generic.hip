@@ -949,6 +949,229 @@ __global__ void __launch_bounds__(Big<M>::NT) gen_big_step_kernel(StepArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// N = 4096, k = 1: the whole blind rotation of a ciphertext in ONE workgroup and one launch, the
+// digit and slot spectra on chip (round 4).  The two-launch path above moves ~0.57 MB of X / Y
+// spectra and accumulator per ciphertext and CMUX step through HBM at N = 4096 (8x the
+// algorithmic bytes, profiles/r04_opt6_pmc.json); here only the key is streamed (from L2: every
+// CU walks the same GGSW at about the same time) and the LWE rows are read and written once.
+//
+// Mapping: 8 waves; wave w owns row j1 = w mod R of GLWE polynomial c = w / R of the accumulator
+// in registers (the four-step row order of gen_big_step_kernel: coefficient n = j1 + R J, lane
+// holds J = lane + 64 e and J + 512, 16 u64).  Per CMUX step:
+//   forward  the rotated difference X^{a} acc - acc through an LDS copy of both polynomials,
+//            decomposition, sub-digits; per (q, t) every wave transforms its row (fft512_fwd,
+//            column twiddle tau), one barrier, then thread p runs the R-point column DFT of
+//            position p for both polynomials: X[(r q) T + t][k1] = frequency k1 512 + p stays in
+//            the thread's registers (2 l T R complex);
+//   product  slot m of output polynomial c at the thread's R frequencies, Y = sum_{r,q,t} X G,
+//            key values read straight from L2 (coalesced: position p is the fastest index of the
+//            key, gen_convert_kernel perm);
+//   inverse  the R-point inverse column DFT in registers into the rows of E, one barrier, every
+//            wave the inverse row transform of its row, exact rounding and the 2^{m b} shift-add
+//            into its accumulator row.
+// The arithmetic is gen_big_step_kernel's (same transforms, twiddles, key and rounding), so the
+// certified bound and generic_pbs_ok hold unchanged; the tests compare bit for bit with the
+// oracle.  LDS: 2R rows of 576 complex (each wave's row doubles as its transpose scratch), the
+// fft512 tables and tau: 118 KB, one workgroup per CU.
+// ------------------------------------------------------------------------------------------
+struct FusedArgs {
+  uint64_t* out;
+  const uint64_t* out_idx;
+  const uint64_t* in;
+  const uint64_t* in_idx;
+  const uint64_t* luts;
+  const uint64_t* lut_idx;
+  const cplx* G;    // Fourier key [n][c][lim][r][q][M], four-step frequency order
+  const cplx* Tau;  // column twiddles [R][512]
+  unsigned long long* resid;
+  uint32_t count, n, base_log, bits;
+};
+
+template <int R, int LV, int T, int L>
+struct Fused {
+  static constexpr int M = R * 512, N = 2 * M;
+  static constexpr int NW = 2 * R, NT = 64 * NW;  // one wave per accumulator row
+  static constexpr int RS = 576;                  // row stride (complex): 512 + transpose pad
+  static constexpr int NX = 2 * LV * T;           // digit spectra per ciphertext and step
+  static constexpr int LDS_CPLX = NW * RS + FFT512_TABLE_ENTRIES + R * 512;
+  static_assert(NT == 512, "one column position per thread");
+  static_assert(LDS_CPLX * 16 <= 160 * 1024, "LDS");
+  static_assert(NW * RS * 16 >= 2 * N * 8, "the accumulator copy fits the rows");
+};
+
+template <int R, int LV, int T, int L, bool W32>
+__global__ void __launch_bounds__(512) gen_fused_kernel(FusedArgs a) {
+  using F = Fused<R, LV, T, L>;
+  constexpr int M = F::M, N = F::N, RS = F::RS, NX = F::NX;
+  constexpr int LOGR = R == 2 ? 1 : R == 4 ? 2 : 3, LOG2_2N = Geo<M>::LOG + 2;
+  using St = typename std::conditional<W32, uint32_t, uint64_t>::type;
+  using Dg = typename std::conditional<W32, int32_t, int64_t>::type;
+  __shared__ cplx lds[F::LDS_CPLX];
+  cplx* E = lds;
+  cplx* tab = lds + F::NW * RS;
+  cplx* tau = tab + FFT512_TABLE_ENTRIES;
+  build_fft512_tables(tab, threadIdx.x, F::NT);
+  for (int x = threadIdx.x; x < R * 512; x += F::NT) tau[x] = a.Tau[x];
+  const Fft512Tables TB = fft512_tables_at(tab);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c = w / R, j1 = w % R;
+  const int pos = threadIdx.x;  // column position of this thread
+  cplx* row = E + w * RS;       // the wave's row (and transpose scratch)
+  const uint32_t ct = blockIdx.x;
+  const uint64_t in_row = a.in_idx ? a.in_idx[ct] : ct;
+  const uint64_t* lwe = a.in + in_row * (uint64_t)(a.n + 1);
+  auto jcol = [&](int e) { return lane + 64 * (e & 7) + 512 * (e >> 3); };
+  uint64_t A[16];
+  {
+    // acc_c = LUT_c * X^{-ms(b)} (blind_rotate_assign: polynomial_wrapping_monic_monomial_div)
+    const uint64_t* lut = a.luts + (a.lut_idx ? a.lut_idx[ct] : 0ull) * (uint64_t)(2 * N) + (uint64_t)c * N;
+    const uint32_t bt = modswitch(lwe[a.n], LOG2_2N);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t src = ((uint32_t)(j1 + R * jcol(e)) + bt) & (2 * N - 1);
+      const uint64_t v = lut[src & (N - 1)];
+      A[e] = src < (uint32_t)N ? v : 0ull - v;
+    }
+  }
+  const int logB = (int)a.base_log, sb = (int)a.bits;
+  const int nrep = 64 - LV * logB;
+  const bool split = T > 1;
+  const St half = split ? (St)1 << (sb - 1) : (St)0, bmask = split ? ((St)1 << sb) - (St)1 : ~(St)0;
+  double max_resid = 0.0;
+  pair_barrier();  // tables, tau
+
+#pragma unroll 1
+  for (uint32_t i = 0; i < a.n; ++i) {
+    // ---- forward: X^{a_i} acc - acc through the LDS copy of both polynomials (row order)
+    const uint32_t at = modswitch(lwe[i], LOG2_2N);
+    uint64_t* accl = reinterpret_cast<uint64_t*>(E);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) accl[c * N + j1 * (N / R) + jcol(e)] = A[e];
+    pair_barrier();
+    St S[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t src = ((uint32_t)(j1 + R * jcol(e)) - at) & (2 * N - 1);
+      const uint32_t idx = src & (N - 1);
+      const uint64_t rv = accl[c * N + (idx & (R - 1)) * (N / R) + (idx >> LOGR)];
+      const uint64_t x = (src < (uint32_t)N ? rv : 0ull - rv) - A[e];
+      S[e] = (St)(nrep > 0 ? decomp_init(x, nrep) : x);
+    }
+    pair_barrier();  // the rows are free again
+    cplx X[NX][R];
+#pragma unroll
+    for (int q = 0; q < LV; ++q) {
+      Dg D[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        if constexpr (W32) D[e] = decomp_next_t<uint32_t>(S[e], logB);
+        else D[e] = decomp_next64(S[e], logB);
+      }
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        cplx v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          // balanced b-bit sub-digit, exact: D - s is a multiple of 2^b
+          const Dg s0 = (Dg)(((St)D[e] + half) & bmask) - (Dg)half;
+          const Dg s1 = (Dg)(((St)D[e + 8] + half) & bmask) - (Dg)half;
+          D[e] = (D[e] - s0) >> sb;
+          D[e + 8] = (D[e + 8] - s1) >> sb;
+          v[e] = {(double)s0, (double)s1};
+        }
+        fft512_fwd(v, row, TB, lane);
+        if (j1 != 0)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = cmul(v[e], tau[j1 * 512 + e * 64 + lane]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) row[e * 64 + lane] = v[e];
+        pair_barrier();
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          cplx u[R];
+#pragma unroll
+          for (int jj = 0; jj < R; ++jj) u[jj] = E[(r * R + jj) * RS + pos];
+          dft_col<R, false>(u);
+#pragma unroll
+          for (int k1 = 0; k1 < R; ++k1) X[(r * LV + q) * T + t][k1] = u[k1];
+        }
+        pair_barrier();
+      }
+    }
+
+    // ---- products and inverse transforms, slot by slot
+    const cplx* Gi = a.G + (uint64_t)i * (2 * L * 2 * LV) * M + pos;
+#pragma unroll 1
+    for (int m = 0; m < L; ++m) {
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) {
+        cplx y[R];
+#pragma unroll
+        for (int k1 = 0; k1 < R; ++k1) y[k1] = {0.0, 0.0};
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          const int lim = m - t;
+          if (lim < 0) continue;  // lim < L always (m < L)
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int q = 0; q < LV; ++q) {
+              const cplx* g = Gi + (uint64_t)(((cc * L + lim) * 2 + r) * LV + q) * M;
+#pragma unroll
+              for (int k1 = 0; k1 < R; ++k1) {
+                const cplx gv = g[k1 * 512], xv = X[(r * LV + q) * T + t][k1];
+                y[k1].re = __builtin_fma(xv.re, gv.re, __builtin_fma(-xv.im, gv.im, y[k1].re));
+                y[k1].im = __builtin_fma(xv.re, gv.im, __builtin_fma(xv.im, gv.re, y[k1].im));
+              }
+            }
+        }
+        dft_col<R, true>(y);
+#pragma unroll
+        for (int jj = 0; jj < R; ++jj) E[(cc * R + jj) * RS + pos] = y[jj];
+      }
+      pair_barrier();
+      cplx v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = row[e * 64 + lane];
+      wave_lds_fence();  // the row is read whole before the transform writes its scratch over it
+      if (j1 != 0)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = cmulc(v[e], tau[j1 * 512 + e * 64 + lane]);
+      cplx gi2[4];
+      inv_p2_stage_tw(gi2, TB, lane & 7);
+      fft512_inv_tw(v, row, TB, lane, gi2, 0);
+      // slot shifts stay below 64: the top limb is 64 - (L - 1) b bits wide (key_format)
+      const uint32_t sh = ((uint32_t)m * a.bits) & 63u;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const double tr = v[e].re + RND_MAGIC, ti = v[e].im + RND_MAGIC;
+        max_resid = fmax(max_resid, fmax(fabs(v[e].re - (tr - RND_MAGIC)), fabs(v[e].im - (ti - RND_MAGIC))));
+        A[e] += ((uint64_t)__double_as_longlong(tr) - RND_MAGIC_BITS) << sh;
+        A[e + 8] += ((uint64_t)__double_as_longlong(ti) - RND_MAGIC_BITS) << sh;
+      }
+      pair_barrier();  // the rows are written by the next slot's column DFTs
+    }
+  }
+
+  // sample extract (nth = 0): out[j] = -A_0[N - j] (j > 0), out[0] = A_0[0], out[N] = A_1[0]
+  const uint64_t orow = a.out_idx ? a.out_idx[ct] : ct;
+  uint64_t* o = a.out + orow * (uint64_t)(N + 1);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const uint32_t j = (uint32_t)(j1 + R * jcol(e));
+    if (c == 0)
+      o[(N - j) & (N - 1)] = j == 0 ? A[e] : 0ull - A[e];
+    else if (j == 0)
+      o[N] = A[e];
+  }
+  if (a.resid) {
+    for (int off = 32; off > 0; off >>= 1) max_resid = fmax(max_resid, __shfl_xor(max_resid, off));
+    if (lane == 0) atomicMax(a.resid, (unsigned long long)__double_as_longlong(max_resid));
+  }
+}
+
+
 // Y[ct][c][m][f] = sum over (r, q, t) with 0 <= m - t < L of X[ct][r][q][t][f] * G_i[c][m-t][r][q][f]
 struct MacArgs {
   const cplx* X;
@@ -1693,6 +1916,26 @@ static bool tile_dispatch(uint32_t N, uint32_t K1, uint32_t KL, uint32_t T, uint
   return false;
 }
 
+// k = 1, N = 4096 with an instance for (l, T, L): the one-launch gen_fused_kernel.  false: no instance
+// (or CONCRETE_HIP_GEN_FUSED=0, A/B runs): the two-launch path runs.
+static bool fused_dispatch(const FusedArgs& f, uint32_t k, uint32_t N, uint32_t level, uint32_t T, uint32_t L,
+                           hipStream_t st) {
+  static const bool on = !getenv("CONCRETE_HIP_GEN_FUSED") || atoi(getenv("CONCRETE_HIP_GEN_FUSED")) != 0;
+  if (!on || k != 1 || N != 4096 || !four_step(N)) return false;
+  const bool w32 = (uint64_t)level * f.base_log <= 31;
+#define GEN_FUSED(LVv, Tv, Lv)                                                                               \
+  if (level == LVv && T == Tv && L == Lv) {                                                                  \
+    if (w32)                                                                                                 \
+      hipLaunchKernelGGL((gen_fused_kernel<4, LVv, Tv, Lv, true>), dim3(f.count), dim3(512), 0, st, f);     \
+    else                                                                                                     \
+      hipLaunchKernelGGL((gen_fused_kernel<4, LVv, Tv, Lv, false>), dim3(f.count), dim3(512), 0, st, f);    \
+    return true;                                                                                             \
+  }
+  GEN_FUSED(1, 2, 5)
+#undef GEN_FUSED
+  return false;
+}
+
 }  // namespace gen
 
 uint64_t generic_scratch_bytes_per_sample(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
@@ -1730,6 +1973,18 @@ int pbs_generic_launch(const PbsArgs& a) {
   const uint32_t K1 = a.k + 1, M = a.N / 2, L = fmt.limbs, b = fmt.bits;
   const uint32_t T = (a.base_log + b - 1) / b;
   const Tables tb = tables_for(a.N);
+  {
+    const FusedArgs f{a.out, a.out_idx, a.in, a.in_idx, a.luts, a.lut_idx, reinterpret_cast<const cplx*>(a.fbsk),
+                      tb.Tau, a.resid, a.num_samples, a.n, a.base_log, b};
+    if (fused_dispatch(f, a.k, a.N, a.level, T, L, a.stream)) {
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) {
+        set_error("generic pbs (fused) launch failed: %s", hipGetErrorString(e));
+        return -1;
+      }
+      return 0;
+    }
+  }
   {
     const TileArgs t{a.out,   a.out_idx, a.in,    a.in_idx, a.luts,         a.lut_idx, reinterpret_cast<const cplx*>(a.fbsk),
                      tb.Wfull, tb.Z,     a.resid, a.num_samples, a.n, a.base_log, b};

@@ -161,8 +161,9 @@ void slot_release(SliceSlot& sl) {
   for (int i = 0; i < 4; ++i)
     if (sl.buf[i]) CHIP_CHECK(hipFree(sl.buf[i]));
   for (void* p : sl.retired) CHIP_CHECK(hipFree(p));
-  for (int i = 0; i < 5; ++i)
+  for (int i = 0; i < 4; ++i)
     if (sl.ev[i]) CHIP_CHECK(hipEventDestroy(sl.ev[i]));
+  if (sl.status_h) CHIP_CHECK(hipHostFree(sl.status_h));
   CHIP_CHECK(hipStreamDestroy(sl.s));
   sl = SliceSlot{};
 }
@@ -173,7 +174,24 @@ void slot_init(SliceSlot& sl, uint32_t gpu) {
   sl.gpu = gpu;
   CHIP_CHECK(hipSetDevice((int)gpu));
   CHIP_CHECK(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
-  for (int i = 0; i < 5; ++i) CHIP_CHECK(hipEventCreate(&sl.ev[i]));
+  for (int i = 0; i < 4; ++i) CHIP_CHECK(hipEventCreate(&sl.ev[i]));
+  CHIP_CHECK(hipHostMalloc((void**)&sl.status_h, sizeof(uint32_t), hipHostMallocDefault));
+}
+
+SlotSet* take_set(concrete_hip_keyset* ks) {
+  std::lock_guard<std::mutex> g(ks->call_m);
+  if (!ks->idle_sets.empty()) {
+    SlotSet* s = ks->idle_sets.back();
+    ks->idle_sets.pop_back();
+    return s;
+  }
+  ks->all_sets.push_back(new SlotSet());
+  return ks->all_sets.back();
+}
+
+void return_set(concrete_hip_keyset* ks, SlotSet* s) {
+  std::lock_guard<std::mutex> g(ks->call_m);
+  ks->idle_sets.push_back(s);
 }
 
 // grow-only device buffer i of the slot (the slot's stream is idle between calls).  hipFree
@@ -192,76 +210,74 @@ uint64_t* slot_buf(SliceSlot& sl, int i, uint64_t bytes) {
 }
 
 void mark(concrete_hip_keyset* ks, SliceSlot& sl, int i) {
+  // (timing is switched between calls; a racy read only decides whether an event is recorded)
   if (ks->timing) CHIP_CHECK(hipEventRecord(sl.ev[i], sl.s));
 }
 
 // Run body(slot, start, count) for every contiguous slice of the batch, one host thread per slice
-// when there are several, then check every device's status word (a PBS whose wave
-// synchronisation gave up produced wrong outputs: abort, as the reference's wrappers do).
+// when there are several, on a slot set of this call's own (concurrent calls on one keyset overlap),
+// then read every slice stream's status word on that stream (a PBS whose wave synchronisation gave
+// up produced wrong outputs: abort, as the reference's wrappers do).
 template <class F>
 void run_sliced(concrete_hip_keyset* ks, uint64_t num_samples, F&& body) {
-  std::lock_guard<std::mutex> call(ks->call_m);
   std::vector<uint32_t> devs;
   {
     std::lock_guard<std::mutex> g(ks->m);
     devs = ks->devices;
   }
   const uint64_t parts = std::max<uint64_t>(1, std::min<uint64_t>(devs.size(), num_samples));
-  if (ks->slots.size() < parts) ks->slots.resize(parts);
+  SlotSet* set = take_set(ks);
+  std::vector<SliceSlot>& slots = set->slots;
+  if (slots.size() < parts) slots.resize(parts);
   std::vector<uint64_t> start(parts), count(parts);
   for (uint64_t r = 0; r < parts; ++r) {
-    slot_init(ks->slots[r], devs[r]);
+    slot_init(slots[r], devs[r]);
     slice_of(num_samples, parts, r, start[r], count[r]);
   }
-  // timing base: one event per device, recorded on the device's first (idle) slot stream
-  int base_of[RT_MAX_DEV];
-  std::fill(base_of, base_of + RT_MAX_DEV, -1);
-  if (ks->timing)
-    for (uint64_t r = 0; r < parts; ++r) {
-      SliceSlot& sl = ks->slots[r];
-      if (base_of[sl.gpu] >= 0) continue;
-      base_of[sl.gpu] = (int)r;
-      CHIP_CHECK(hipSetDevice((int)sl.gpu));
-      CHIP_CHECK(hipEventRecord(sl.ev[4], sl.s));
-    }
+  bool timing;
+  {
+    std::lock_guard<std::mutex> g(ks->call_m);
+    timing = ks->timing;
+  }
+  auto slice = [&](uint64_t r) {
+    SliceSlot& sl = slots[r];
+    body(sl, start[r], count[r]);
+    if (take_stream_status((int)sl.gpu, sl.s, sl.status_h) != 0) rt_die("%s", concrete_hip_last_error());
+  };
   if (parts == 1) {
-    body(ks->slots[0], start[0], count[0]);
+    slice(0);
   } else {
     std::vector<std::thread> th;
     th.reserve(parts);
-    for (uint64_t r = 0; r < parts; ++r)
-      th.emplace_back([&, r] { body(ks->slots[r], start[r], count[r]); });
+    for (uint64_t r = 0; r < parts; ++r) th.emplace_back(slice, r);
     for (auto& t : th) t.join();
   }
   for (uint64_t r = 0; r < parts; ++r) {
-    SliceSlot& sl = ks->slots[r];
+    SliceSlot& sl = slots[r];
     if (sl.retired.empty()) continue;
     CHIP_CHECK(hipSetDevice((int)sl.gpu));
     for (void* p : sl.retired) CHIP_CHECK(hipFree(p));
     sl.retired.clear();
   }
-  bool seen[RT_MAX_DEV] = {};
-  for (uint64_t r = 0; r < parts; ++r) {
-    const uint32_t g = ks->slots[r].gpu;
-    if (seen[g]) continue;
-    seen[g] = true;
-    if (take_device_status((int)g) != 0) rt_die("%s", concrete_hip_last_error());
-  }
-  if (ks->timing) {
-    ks->timeline.assign(parts * 6, 0.0);
-    for (uint64_t r = 0; r < parts; ++r) {
-      SliceSlot& sl = ks->slots[r];
+  if (timing) {
+    std::vector<double> tl(parts * 6, 0.0);
+    std::lock_guard<std::mutex> g(ks->call_m);
+    for (uint64_t r = 0; r < parts && ks->timing; ++r) {
+      SliceSlot& sl = slots[r];
+      if (!ks->timing_base[sl.gpu]) continue;  // a device added after timing was enabled
       CHIP_CHECK(hipSetDevice((int)sl.gpu));
-      double* t = &ks->timeline[r * 6];
+      double* t = &tl[r * 6];
       t[0] = sl.gpu;
       for (int i = 0; i < 4; ++i) {
         float ms = 0.f;
-        CHIP_CHECK(hipEventElapsedTime(&ms, ks->slots[base_of[sl.gpu]].ev[4], sl.ev[i]));
+        CHIP_CHECK(hipEventElapsedTime(&ms, ks->timing_base[sl.gpu], sl.ev[i]));
         t[1 + i] = ms;
       }
       t[5] = (double)count[r];
     }
+    if (ks->timing) ks->timeline.insert(ks->timeline.end(), tl.begin(), tl.end());
   }
+  return_set(ks, set);
 }
 
 struct PbsCall {
@@ -407,7 +423,15 @@ void concrete_hip_keyset_destroy(concrete_hip_keyset* ks) {
     for (auto it = g_bound.begin(); it != g_bound.end();)
       it = it->second == ks ? g_bound.erase(it) : std::next(it);
   }
-  for (auto& sl : ks->slots) slot_release(sl);
+  for (SlotSet* set : ks->all_sets) {
+    for (auto& sl : set->slots) slot_release(sl);
+    delete set;
+  }
+  for (int d = 0; d < RT_MAX_DEV; ++d)
+    if (ks->timing_base[d]) {
+      CHIP_CHECK(hipSetDevice(d));
+      CHIP_CHECK(hipEventDestroy(ks->timing_base[d]));
+    }
   free_keys(ks);
   delete ks;
 }
@@ -473,7 +497,7 @@ int concrete_hip_keyset_set_devices(concrete_hip_keyset* ks, const uint32_t* dev
       set_error("keyset_set_devices: device %u not visible", devices[i]);
       return -3;
     }
-  std::lock_guard<std::mutex> call(ks->call_m);
+  // calls in flight keep the devices they started with (run_sliced copies the list)
   std::lock_guard<std::mutex> g(ks->m);
   ks->devices.assign(devices, devices + count);
   return 0;
@@ -481,9 +505,27 @@ int concrete_hip_keyset_set_devices(concrete_hip_keyset* ks, const uint32_t* dev
 
 void concrete_hip_keyset_set_timing(concrete_hip_keyset* ks, int enable) {
   if (!ks) return;
+  std::vector<uint32_t> devs;
+  {
+    std::lock_guard<std::mutex> g(ks->m);
+    devs = ks->devices;
+  }
   std::lock_guard<std::mutex> call(ks->call_m);
-  ks->timing = enable != 0;
   ks->timeline.clear();
+  ks->timing = false;
+  if (!enable) return;
+  // one base event per device, in the past of every later call: slices of different calls (and
+  // streams) share the time axis
+  int prev = 0;
+  CHIP_CHECK(hipGetDevice(&prev));
+  for (uint32_t d : devs) {
+    CHIP_CHECK(hipSetDevice((int)d));
+    if (!ks->timing_base[d]) CHIP_CHECK(hipEventCreate(&ks->timing_base[d]));
+    CHIP_CHECK(hipEventRecord(ks->timing_base[d], nullptr));
+    CHIP_CHECK(hipEventSynchronize(ks->timing_base[d]));
+  }
+  CHIP_CHECK(hipSetDevice(prev));
+  ks->timing = true;
 }
 
 uint32_t concrete_hip_keyset_timeline(concrete_hip_keyset* ks, double* out, uint32_t max_slices) {

@@ -136,10 +136,24 @@ struct SliceSlot {
   hipStream_t s = nullptr;
   void* buf[4] = {};      // in, out, luts (+ accumulators), lut indexes
   uint64_t cap[4] = {};   // bytes
-  hipEvent_t ev[5] = {};  // start, after H2D, after kernel, after D2H; ev[4] unused
+  hipEvent_t ev[4] = {};  // start, after H2D, after kernel, after D2H
   std::vector<void*> retired;  // outgrown buffers, freed once every slice thread has joined
   HostBuf stage_in, stage_out, stage_lut;  // page-locked staging of the caller's (pageable) memrefs
+  uint32_t* status_h = nullptr;  // page-locked landing word of the stream-ordered status read
 };
+
+// The slots of one call.  A keyset keeps a pool of them: concurrent calls on one keyset (several
+// RuntimeContexts sharing it) each take their own set, so they overlap instead of
+// queueing behind one lock (round 4; the reference runs one scheduler thread per device,
+// GPUDFG.cpp:852-895).
+struct SlotSet {
+  std::vector<SliceSlot> slots;
+};
+
+// Device status of the work issued so far on stream s (abi.hip): the status word is read on s itself
+// into h (page-locked) and s is synchronised — no device-wide synchronisation, so other streams'
+// calls keep running.  Returns 0, or -4 with the message set when a PBS wave synchronisation gave up.
+int take_stream_status(int gpu, hipStream_t s, uint32_t* h);
 
 }  // namespace chip
 
@@ -148,11 +162,12 @@ struct concrete_hip_keyset {
   std::vector<chip::BskEntry*> bsk;  // indexed by bsk_index
   std::vector<chip::KskEntry*> ksk;
   std::vector<uint32_t> devices{0};
-  // one memref call at a time uses the slots (a circuit's calls are sequential per context)
+  // call_m guards the pool and the timing state; it is held only to take or return a slot set
   std::mutex call_m;
-  std::vector<chip::SliceSlot> slots;
+  std::vector<chip::SlotSet*> idle_sets, all_sets;
   bool timing = false;
-  std::vector<double> timeline;  // 6 per slice of the last call (concrete_hip_keyset_timeline)
+  hipEvent_t timing_base[chip::RT_MAX_DEV] = {};  // recorded when timing was enabled, per device
+  std::vector<double> timeline;  // 6 per slice of every call since timing was enabled
 };
 
 namespace chip {

@@ -79,6 +79,7 @@ struct Slot {
   std::vector<void*> buf;
   std::vector<uint64_t> cap;
   std::vector<void*> retired;  // outgrown buffers, freed once every shard thread has joined
+  uint32_t* status_h = nullptr;  // page-locked landing word of the stream-ordered status read
 };
 
 // hipFree synchronises the whole device, so a buffer outgrown while other shards' kernels run on
@@ -97,6 +98,7 @@ void slot_free(Slot& sl) {
   for (void* p : sl.buf)
     if (p) CHIP_CHECK(hipFree(p));
   for (void* p : sl.retired) CHIP_CHECK(hipFree(p));
+  if (sl.status_h) CHIP_CHECK(hipHostFree(sl.status_h));
   CHIP_CHECK(hipStreamDestroy(sl.s));
   sl = Slot{};
 }
@@ -473,6 +475,7 @@ void execute(Dfg* g, Stream* target) {
       sl.gpu = g->devices[r];
       CHIP_CHECK(hipSetDevice((int)sl.gpu));
       CHIP_CHECK(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
+      CHIP_CHECK(hipHostMalloc((void**)&sl.status_h, sizeof(uint32_t), hipHostMallocDefault));
     }
     const uint64_t base = P.batch / parts, extra = P.batch % parts;
     shard[r].count = base + (r < extra ? 1 : 0);
@@ -488,6 +491,8 @@ void execute(Dfg* g, Stream* target) {
     const uint64_t chunk = std::max<uint64_t>(1, (uint64_t)(free_b / 2 / parts) / per_sample);
     for (uint64_t s0 = 0; s0 < shard[r].count; s0 += chunk)
       run_chunk(P, sl, shard[r].start + s0, std::min(chunk, shard[r].count - s0));
+    // the shard stream's own status read (no device-wide synchronisation)
+    if (take_stream_status((int)sl.gpu, sl.s, sl.status_h) != 0) rt_die("%s", concrete_hip_last_error());
   };
   if (parts == 1) {
     work(0);
@@ -497,13 +502,6 @@ void execute(Dfg* g, Stream* target) {
     for (auto& t : th) t.join();
   }
   for (uint64_t r = 0; r < parts; ++r) slot_free_retired(g->slots[r]);
-  bool seen[RT_MAX_DEV] = {};
-  for (uint64_t r = 0; r < parts; ++r) {
-    const uint32_t d = g->slots[r].gpu;
-    if (seen[d]) continue;
-    seen[d] = true;
-    if (take_device_status((int)d) != 0) rt_die("%s", concrete_hip_last_error());
-  }
   std::unordered_map<Stream*, uint64_t> memo;
   for (Stream* x : P.produced) {
     x->computed = true;

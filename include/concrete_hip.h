@@ -246,9 +246,11 @@ int concrete_hip_keyset_add_ksk(concrete_hip_keyset *ks, uint32_t ksk_index, con
 int concrete_hip_keyset_set_devices(concrete_hip_keyset *ks, const uint32_t *devices, uint32_t count);
 /* Diagnostics: record HIP events around every slice of the following calls ... */
 void concrete_hip_keyset_set_timing(concrete_hip_keyset *ks, int enable);
-/* ... and read them for the last call: 6 doubles per slice (device, then ms since the call's start
- * on that device: slice start, inputs copied (kernel issue), kernel done, outputs copied, then the
- * slice's sample count); returns the number of slices (copies at most max_slices). */
+/* ... and read them for every call since timing was enabled, in completion order: 6 doubles per
+ * slice (device, then ms since timing was enabled on that device: slice start, inputs copied
+ * (kernel issue), kernel done, outputs copied, then the slice's sample count); returns the number
+ * of slices (copies at most max_slices).  Concurrent calls on one keyset run on slot sets of their
+ * own, so their slices share this time axis (round 4). */
 uint32_t concrete_hip_keyset_timeline(concrete_hip_keyset *ks, double *out, uint32_t max_slices);
 
 /* The runtime's context pointer (mlir::concretelang::RuntimeContext *, context.h:42-154) is what

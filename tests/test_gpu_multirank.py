@@ -21,19 +21,23 @@ def _port():
 
 
 def test_bench_two_ranks():
+    """The driver's default multi-GPU line: the metric's whole-node batch of 4096 split over the
+    ranks (strong scaling), plus the weak-scaling secondary row (4096 per rank)."""
     env = dict(os.environ, CONCRETE_HIP_DIST_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "1", "--warmup", "1", "--batch", "256", "--no-cpu-baseline", "--no-ks",
-           "--verify", "4"]
+           "--gpus", "2", "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-ks", "--verify", "4"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 512
-    assert d["checks"]["decrypt_ok"] == "512/512"
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert d["config"]["global_batch"] == 4096 and d["config"]["batch_per_gpu"] == 2048
+    assert d["checks"]["decrypt_ok"] == "4096/4096"
     assert d["checks"]["bitexact"] is True
+    w = d["secondary"]["weak_scaling"]
+    assert w["batch_per_gpu"] == 4096 and w["value"] > 0
 
 
 def test_bench_eight_ranks_configs2_shape():
@@ -44,7 +48,7 @@ def test_bench_eight_ranks_configs2_shape():
     env = dict(os.environ, CONCRETE_HIP_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "8", "--steps", "1", "--warmup", "0", "--batch", "8192", "--no-cpu-baseline", "--no-ks",
+           "--gpus", "8", "--steps", "1", "--warmup", "0", "--weak", "--batch", "8192", "--no-cpu-baseline", "--no-ks",
            "--verify", "2", "--check-gather"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]

@@ -194,6 +194,66 @@ def test_slices_overlap_and_bit_exact(env):
     assert np.array_equal(got[rows], ref)
 
 
+def test_concurrent_calls_on_one_keyset_overlap(env):
+    """Two threads run memref_batched_bootstrap_lwe_cuda_u64 on ONE shared keyset (two runtime
+    contexts bound to it, as INTEGRATION.md §4 recommends): each call takes a slot set of its own and
+    reads the device status on its own stream, so the second call is issued while the first call's
+    kernel is still running (round 3 held one lock for the whole call and synchronised the device
+    after it).  HIP events on a common time base show the overlap; both results are bit-exact."""
+    import ctypes as C
+    import threading
+    B, R, O = env["B"], env["R"], env["O"]
+    p = B.CFG2  # full n: kernels of tens of ms
+    lwe_sk = B.binary_key(p.n, 81)
+    glwe_sk = B.binary_key(p.big_n, 82)
+    bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 83)
+    width = 3
+    table = np.array([1, 3, 5, 7, 0, 2, 4, 6], dtype=np.uint64)
+    tlu = B.expand_lut(table, p.N, width)
+    nb = 2048
+    rng = np.random.RandomState(84)
+    msgs = rng.randint(0, 1 << width, size=(2, nb))
+    cts = [B.lwe_encrypt(lwe_sk, [B.encode(m, width) for m in msgs[i]], p.n, B.secure_std(1, p.n), 85 + i)
+           for i in range(2)]
+    ks = R.Keyset([0])
+    ks.add_bsk(0, bsk, p)
+    ctx = [C.create_string_buffer(64) for _ in range(2)]  # two RuntimeContexts, one keyset
+    for c in ctx:
+        ks.bind(C.addressof(c))
+    for i in range(2):  # key conversion and both slot sets' buffers outside the recorded calls
+        R.batched_bootstrap_cuda(C.addressof(ctx[i]), p, cts[i], tlu)
+    outs = [None, None]
+    gate = threading.Barrier(2)
+
+    def call(i):
+        gate.wait()
+        outs[i] = R.batched_bootstrap_cuda(C.addressof(ctx[i]), p, cts[i], tlu)
+
+    for _ in range(2):  # warm both slot sets under concurrency too
+        th = [threading.Thread(target=call, args=(i,)) for i in range(2)]
+        [t.start() for t in th]
+        [t.join() for t in th]
+    ks.set_timing(True)
+    th = [threading.Thread(target=call, args=(i,)) for i in range(2)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    tl = ks.timeline()
+    ks.close()
+    assert tl.shape == (2, 6) and list(tl[:, 5]) == [nb, nb], tl
+    # columns: device, start, inputs copied (kernel issue), kernel done, outputs copied, count
+    first, second = (0, 1) if tl[0, 1] <= tl[1, 1] else (1, 0)
+    assert tl[second, 1] < tl[first, 3], f"the second call waited for the first call's kernel: {tl}"
+    for i in range(2):
+        dec = B.lwe_decrypt(glwe_sk, outs[i], p.big_n)
+        assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs[i]]
+    op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
+    rows = np.array([0, 777, nb - 1])
+    fcpu = O.bsk_to_fourier(op, bsk)
+    for i in range(2):
+        ref, _ = O.pbs_batch(op, cts[i][rows], B.trivial_glwe(p, tlu)[None, :], fbsk=fcpu)
+        assert np.array_equal(outs[i][rows], ref)
+
+
 def test_cuda_names_resolve_the_runtime_context(env):
     """memref_*_cuda_u64 under the reference's names take the circuit's RuntimeContext pointer:
     bound with concrete_hip_context_bind, or answered by a registered resolver."""

@@ -41,6 +41,8 @@ SIGNATURES = {
     "concrete_hip_last_error": (C.c_char_p, []),
     "concrete_hip_pbs_supported": (i32, [u32, u32, u32, u32]),
     "concrete_hip_keyswitch_supported": (i32, [u32, u32, u32, u32]),
+    "concrete_hip_server_keyset_level_order": (i32, [vp, i32, u32]),
+    "concrete_hip_server_keyset_secret_count": (u32, [vp]),
     "concrete_hip_bsk_limbs": (u32, [u32, u32, u32]),
     "concrete_hip_bsk_format": (C.c_int, [u32, u32, u32, C.POINTER(u32), C.POINTER(u32)]),
     "concrete_hip_generic_error_bound": (C.c_double, [u32, u32, u32, u32, C.c_double]),

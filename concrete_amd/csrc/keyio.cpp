@@ -24,12 +24,14 @@
 //
 // Parity: unpinned — the reference holds no serialized keyset; tests/test_keyio.py round-trips the
 // writer in concrete_amd/keys.py (single-segment, single-far and double-far layouts) and checks
-// malformed messages are refused.
+// malformed messages are refused.  The restated level orders of the standard layouts are checked
+// on read whenever the message carries the client secret keys (a Keyset): check_level_order.
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <exception>
 #include <initializer_list>
 #include <mutex>
@@ -47,8 +49,21 @@ struct concrete_hip_server_keyset {
   struct Key {
     concrete_hip_key_info info;
     std::vector<uint64_t> payload;  // concatenated blobs (u64 words)
+    // level order found when the key was last expanded against the client secret keys
+    // (CONCRETE_HIP_LEVEL_ORDER_*); mutable: expansion is a const read of the keyset
+    mutable int level_order = 0;
+  };
+  struct Secret {  // a client LweSecretKey (Keyset.client, concrete-protocol.capnp:139-145, 298-303)
+    uint32_t id = 0;
+    std::vector<uint64_t> words;  // lweDimension u64 words (binary keys: 0 / 1)
   };
   std::vector<Key> bsk, ksk;
+  std::vector<Secret> secrets;
+  const Secret* secret(uint32_t id, uint64_t dim) const {
+    for (const auto& x : secrets)
+      if (x.id == id && x.words.size() == dim) return &x;
+    return nullptr;
+  }
 };
 
 namespace {
@@ -475,6 +490,28 @@ bool read_keys(Reader& r, const Reader::List& list, bool is_bsk, std::vector<con
   return true;
 }
 
+// ClientKeyset.lweSecretKeys: LweSecretKey { info @0 (LweSecretKeyInfo: id u32 @0; ptr 0 params:
+// LweSecretKeyParams lweDimension u32 @0, integerPrecision u32 @4, keyType u16 @8), payload @1 }
+bool read_secrets(Reader& r, const Reader::List& list, std::vector<concrete_hip_server_keyset::Secret>& out) {
+  if (!list.present) return r.ok();
+  for (uint64_t i = 0; i < list.count; ++i) {
+    Reader::Struct key = r.list_struct(list, i);
+    if (!r.ok()) return false;
+    Reader::Struct info = r.ptr_struct(key, 0);
+    if (!info.present) continue;
+    concrete_hip_server_keyset::Secret sec;
+    sec.id = r.u32(info, 0);
+    Reader::Struct par = r.ptr_struct(info, 0);
+    const uint32_t dim = par.present ? r.u32(par, 0) : 0;
+    const uint32_t prec = par.present ? r.u32(par, 4) : 0;
+    uint64_t words = 0;
+    if (!read_payload(r, key, sec.words, words)) return false;
+    // only 64-bit secret keys of their declared dimension take part in the level-order check
+    if (prec == 64 && dim > 0 && words == dim) out.push_back(std::move(sec));
+  }
+  return r.ok();
+}
+
 int parse_impl(const uint64_t* words, uint64_t n_words, uint32_t root, concrete_hip_server_keyset** out);
 
 // no C++ exception crosses the C ABI: allocation failures (a 1 GB key on a short host) are errors
@@ -520,9 +557,16 @@ int parse_impl(const uint64_t* words, uint64_t n_words, uint32_t root, concrete_
   auto* ks = new concrete_hip_server_keyset();
   bool ok = true;
   switch (root) {
-    case CONCRETE_HIP_ROOT_KEYSET:
+    case CONCRETE_HIP_ROOT_KEYSET: {
+      // Keyset.client (secret keys: the level orders of the evaluation keys are checked against them)
+      Reader::Struct client = r.ptr_struct(top, 1);
+      if (client.present && !read_secrets(r, r.ptr_list(client, 0), ks->secrets)) {
+        ok = false;
+        break;
+      }
       top = r.ptr_struct(top, 0);  // Keyset.server
       if (!top.present) break;
+    }
       /* fallthrough */
     case CONCRETE_HIP_ROOT_SERVER_KEYSET:
       ok = read_keys(r, r.ptr_list(top, 0), true, ks->bsk) && read_keys(r, r.ptr_list(top, 1), false, ks->ksk);
@@ -551,12 +595,105 @@ int parse_impl(const uint64_t* words, uint64_t n_words, uint32_t root, concrete_
   return 0;
 }
 
+// ---- level order of an evaluation key, checked against the client secret keys ---------------
+// The standard layouts restate tfhe's storage orders (unpinned: no serialized keyset exists
+// offline): GGSW level position v of a bootstrap key encrypts s_i 2^(64 - logB (v + 1)) (keygen.cpp,
+// level 1 first); keyswitch row t of block i encrypts s_in[i] 2^(64 - logB (l - t)) (levels reversed,
+// keyswitch.rs:185-223).  When the keyset carries the client keys, one row per level of the first
+// mask position whose secret bit is 1 is decrypted: a key stored in the other order is re-ordered,
+// one that decrypts to neither is refused (a silent wrong order would bootstrap to garbage).
+// dist(a, b): |a - b| on the torus
+inline uint64_t tdist(uint64_t a, uint64_t b) {
+  const uint64_t d = a - b;
+  return (int64_t)d < 0 ? 0 - d : d;
+}
+// Classify per-level decryptions d[v] against the expected scales e[v] and their reversal.
+int classify_levels(const std::vector<uint64_t>& d, const std::vector<uint64_t>& e) {
+  const size_t l = e.size();
+  bool as_is = true, reversed = true;
+  for (size_t v = 0; v < l; ++v) {
+    const uint64_t de = tdist(d[v], e[v]), dr = tdist(d[v], e[l - 1 - v]);
+    // a level decrypts to its scale up to noise far below the gap between neighbouring scales
+    if (!(de < e[v] / 4)) as_is = false;
+    if (!(dr < e[l - 1 - v] / 4)) reversed = false;
+  }
+  if (as_is) return CONCRETE_HIP_LEVEL_ORDER_AS_EXPECTED;
+  if (reversed) return CONCRETE_HIP_LEVEL_ORDER_REVERSED;
+  return -1;
+}
+
+// key: standard-domain words; returns CONCRETE_HIP_LEVEL_ORDER_* or -1 (refuse)
+int check_level_order(const concrete_hip_server_keyset* ks, const concrete_hip_key_info& i, bool is_bsk,
+                      uint64_t* key) {
+  const uint32_t l = i.level_count, logB = i.base_log;
+  if (!ks || l < 2) return CONCRETE_HIP_LEVEL_ORDER_UNCHECKED;  // one level: nothing to order
+  const uint64_t n_out = is_bsk ? (uint64_t)i.glwe_dim * i.poly_size : i.output_lwe_dim;
+  const auto* s_in = ks->secret(i.input_id, i.input_lwe_dim);
+  const auto* s_out = ks->secret(i.output_id, n_out);
+  if (!s_in || !s_out) return CONCRETE_HIP_LEVEL_ORDER_UNCHECKED;
+  uint64_t pos = 0;
+  while (pos < i.input_lwe_dim && s_in->words[pos] != 1) ++pos;
+  if (pos == i.input_lwe_dim) return CONCRETE_HIP_LEVEL_ORDER_UNCHECKED;
+  std::vector<uint64_t> d(l), e(l);
+  const uint64_t* so = s_out->words.data();
+  if (is_bsk) {
+    // [n][l][k+1 rows][k+1 polys][N]: row k of level v, constant coefficient of B - sum_r A_r S_r
+    const uint64_t k = i.glwe_dim, N = i.poly_size, glwe = (k + 1) * N;
+    for (uint32_t v = 0; v < l; ++v) {
+      const uint64_t* ct = key + (((uint64_t)pos * l + v) * (k + 1) + k) * glwe;
+      uint64_t acc = ct[k * N];
+      for (uint64_t r = 0; r < k; ++r) {
+        const uint64_t* a = ct + r * N;
+        const uint64_t* sr = so + r * N;
+        acc -= a[0] * sr[0];
+        for (uint64_t j = 1; j < N; ++j) acc += a[j] * sr[N - j];  // negacyclic: X^N = -1
+      }
+      d[v] = acc;
+      e[v] = 1ull << (64 - logB * (v + 1));
+    }
+  } else {
+    // [n_in][l][n_out + 1]: row t decrypts to s_in[pos] 2^(64 - logB (l - t))
+    for (uint32_t t = 0; t < l; ++t) {
+      const uint64_t* ct = key + ((uint64_t)pos * l + t) * (n_out + 1);
+      uint64_t acc = ct[n_out];
+      for (uint64_t j = 0; j < n_out; ++j) acc -= ct[j] * so[j];
+      d[t] = acc;
+      e[t] = 1ull << (64 - logB * (l - t));
+    }
+  }
+  const int c = classify_levels(d, e);
+  if (c != CONCRETE_HIP_LEVEL_ORDER_REVERSED) return c;
+  // re-order: reverse the level blocks of every mask position
+  const uint64_t blk = is_bsk ? ((uint64_t)i.glwe_dim + 1) * ((uint64_t)i.glwe_dim + 1) * i.poly_size : n_out + 1;
+  for (uint64_t m = 0; m < i.input_lwe_dim; ++m)
+    for (uint32_t v = 0; v < l / 2; ++v)
+      std::swap_ranges(key + (m * l + v) * blk, key + (m * l + v + 1) * blk, key + (m * l + (l - 1 - v)) * blk);
+  return c;
+}
+
 std::mutex g_dec_mu;
 concrete_hip_bsk_decompressor g_bsk_dec = nullptr;
 concrete_hip_ksk_decompressor g_ksk_dec = nullptr;
 
-// Checks a key's parameters and payload size and writes its standard-domain form to dst.
-int expand(const concrete_hip_server_keyset::Key& k, bool is_bsk, uint64_t* dst, uint64_t dst_words) {
+int expand_raw(const concrete_hip_server_keyset::Key& k, bool is_bsk, uint64_t* dst, uint64_t dst_words);
+
+// Checks a key's parameters and payload size, writes its standard-domain form to dst, and checks
+// (and if needed fixes) its level order against the keyset's client secret keys.
+int expand(const concrete_hip_server_keyset* ks, const concrete_hip_server_keyset::Key& k, bool is_bsk, uint64_t* dst,
+           uint64_t dst_words) {
+  const int rc = expand_raw(k, is_bsk, dst, dst_words);
+  if (rc) return rc;
+  const int order = check_level_order(ks, k.info, is_bsk, dst);
+  if (order < 0) {
+    set_error("%s %u: no GGSW / keyswitch row decrypts to its level under the keyset's client keys, in either "
+              "level order", is_bsk ? "bootstrap key" : "keyswitch key", k.info.id);
+    return -3;
+  }
+  k.level_order = order;
+  return 0;
+}
+
+int expand_raw(const concrete_hip_server_keyset::Key& k, bool is_bsk, uint64_t* dst, uint64_t dst_words) {
   const concrete_hip_key_info& i = k.info;
   const char* what = is_bsk ? "bootstrap key" : "keyswitch key";
   if (i.integer_precision != 64 || i.modulus_kind != 0) {
@@ -635,7 +772,7 @@ static int add_server_keyset(concrete_hip_keyset* ks, const concrete_hip_server_
   for (uint32_t i = 0; i < sk->bsk.size(); ++i) {
     const concrete_hip_key_info& k = sk->bsk[i].info;
     buf.assign(k.key_words, 0);
-    int rc = expand(sk->bsk[i], true, buf.data(), buf.size());
+    int rc = expand(sk, sk->bsk[i], true, buf.data(), buf.size());
     if (rc) return rc;
     rc = concrete_hip_keyset_add_bsk(ks, i, buf.data(), k.input_lwe_dim, k.glwe_dim, k.level_count, k.base_log,
                                      k.poly_size);
@@ -644,7 +781,7 @@ static int add_server_keyset(concrete_hip_keyset* ks, const concrete_hip_server_
   for (uint32_t i = 0; i < sk->ksk.size(); ++i) {
     const concrete_hip_key_info& k = sk->ksk[i].info;
     buf.assign(k.key_words, 0);
-    int rc = expand(sk->ksk[i], false, buf.data(), buf.size());
+    int rc = expand(sk, sk->ksk[i], false, buf.data(), buf.size());
     if (rc) return rc;
     rc = concrete_hip_keyset_add_ksk(ks, i, buf.data(), k.level_count, k.base_log, k.input_lwe_dim,
                                      k.output_lwe_dim);
@@ -746,7 +883,7 @@ int concrete_hip_server_keyset_read_bsk(const concrete_hip_server_keyset* sk, ui
     set_error("server_keyset_read_bsk: bad argument or index %u", index);
     return -3;
   }
-  return expand(sk->bsk[index], true, dst, dst_words);
+  return expand(sk, sk->bsk[index], true, dst, dst_words);
 }
 
 int concrete_hip_server_keyset_read_ksk(const concrete_hip_server_keyset* sk, uint32_t index, uint64_t* dst,
@@ -755,7 +892,19 @@ int concrete_hip_server_keyset_read_ksk(const concrete_hip_server_keyset* sk, ui
     set_error("server_keyset_read_ksk: bad argument or index %u", index);
     return -3;
   }
-  return expand(sk->ksk[index], false, dst, dst_words);
+  return expand(sk, sk->ksk[index], false, dst, dst_words);
+}
+
+int concrete_hip_server_keyset_level_order(const concrete_hip_server_keyset* sk, int is_bsk, uint32_t index) {
+  if (!sk || index >= (is_bsk ? sk->bsk.size() : sk->ksk.size())) {
+    set_error("server_keyset_level_order: bad argument or index %u", index);
+    return -3;
+  }
+  return (is_bsk ? sk->bsk[index] : sk->ksk[index]).level_order;
+}
+
+uint32_t concrete_hip_server_keyset_secret_count(const concrete_hip_server_keyset* sk) {
+  return sk ? (uint32_t)sk->secrets.size() : 0;
 }
 
 void concrete_hip_set_seeded_key_decompressors(concrete_hip_bsk_decompressor bsk, concrete_hip_ksk_decompressor ksk) {

@@ -36,6 +36,12 @@ BSK_PARAMS_OFF = {"level_count": 0, "base_log": 4, "glwe_dim": 8, "poly_size": 1
 KSK_PARAMS_OFF = {"level_count": 0, "base_log": 4, "variance": 8, "integer_precision": 16, "key_type": 20,
                   "input_lwe_dim": 24, "output_lwe_dim": 28}
 INFO_WORDS, BSK_PARAMS_WORDS, KSK_PARAMS_WORDS = 2, 5, 4
+# LweSecretKeyInfo: id u32 @0 (1 data word, params pointer); LweSecretKeyParams: lweDimension u32 @0,
+# integerPrecision u32 @4, keyType u16 @8 (2 data words)
+SK_INFO_WORDS, SK_PARAMS_WORDS = 1, 2
+SK_PARAMS_OFF = {"lwe_dimension": 0, "integer_precision": 4, "key_type": 8}
+# concrete_hip_server_keyset_level_order
+LEVEL_ORDER = {0: "unchecked", 1: "as_expected", 2: "reversed"}
 
 
 class _CKeyInfo(C.Structure):
@@ -131,6 +137,17 @@ class ServerKeyset:
         out = np.zeros(self.keyswitch_keys[i].key_words, dtype=np.uint64)
         _native.check(self.lib.concrete_hip_server_keyset_read_ksk(self.h, i, out.ctypes.data, out.size), "read_ksk")
         return out
+
+    def level_order(self, kind: str, i: int) -> str:
+        """Level order found when key i ("bsk" / "ksk") was last read, checked against the client
+        secret keys of a Keyset message: "unchecked", "as_expected" or "reversed" (re-ordered)."""
+        rc = self.lib.concrete_hip_server_keyset_level_order(self.h, int(kind == "bsk"), i)
+        _native.check(rc if rc < 0 else 0, "server_keyset_level_order")
+        return LEVEL_ORDER[rc]
+
+    @property
+    def secret_count(self) -> int:
+        return self.lib.concrete_hip_server_keyset_secret_count(self.h)
 
     def add_to(self, keyset) -> None:
         """Register every key in a runtime.Keyset (bsk_index / ksk_index = list position)."""
@@ -292,10 +309,30 @@ def _write_key(m: _Message, key, info: KeyInfo, payload: np.ndarray, is_bsk: boo
     m.set_struct_ptr(key, 1, pl)
 
 
+def _write_secret(m: _Message, key, sk_id: int, words: np.ndarray, blob_words: int):
+    inf = m.new_struct(SK_INFO_WORDS, 1)
+    m.set_data(inf, 0, "I", sk_id)
+    par = m.new_struct(SK_PARAMS_WORDS, 0)
+    m.set_data(par, SK_PARAMS_OFF["lwe_dimension"], "I", int(words.size))
+    m.set_data(par, SK_PARAMS_OFF["integer_precision"], "I", 64)
+    m.set_data(par, SK_PARAMS_OFF["key_type"], "H", 0)
+    m.set_struct_ptr(inf, 0, par)
+    m.set_struct_ptr(key, 0, inf)
+    pl = m.new_struct(0, 1)
+    w = np.ascontiguousarray(words, dtype=np.uint64)
+    nblobs = max(1, -(-w.size // blob_words))
+    plist = m.new_ptr_list(nblobs)
+    for b in range(nblobs):
+        m.set_list_elem_ptr(plist, b, m.new_data(w[b * blob_words:(b + 1) * blob_words].astype("<u8").tobytes()))
+    m.set_list_ptr(pl, 0, plist)
+    m.set_struct_ptr(key, 1, pl)
+
+
 def serialize_server_keyset(bsks=(), ksks=(), *, root: str = "server", layout: str = "flat",
-                            blob_words: int = BLOB_WORDS) -> bytes:
+                            blob_words: int = BLOB_WORDS, secrets=()) -> bytes:
     """Wire form of a server keyset: bsks / ksks are lists of (KeyInfo, u64 payload).
-    root: "server" (ServerKeyset), "keyset" (Keyset with the server part), or "bootstrap_key" /
+    root: "server" (ServerKeyset), "keyset" (Keyset with the server part, and the client part's
+    LweSecretKeys when `secrets` lists (id, u64 words) pairs), or "bootstrap_key" /
     "keyswitch_key" (a single key message)."""
     m = _Message(layout)
     if root in ("bootstrap_key", "keyswitch_key"):
@@ -310,6 +347,13 @@ def serialize_server_keyset(bsks=(), ksks=(), *, root: str = "server", layout: s
         m.set_root(top)
         srv = m.new_struct(0, 3)
         m.set_struct_ptr(top, 0, srv)
+        if secrets:
+            client = m.new_struct(0, 1)
+            m.set_struct_ptr(top, 1, client)
+            lst, elems = m.new_struct_list(len(secrets), 0, 2)
+            m.set_list_ptr(client, 0, lst)
+            for el, (sk_id, words) in zip(elems, secrets):
+                _write_secret(m, el, sk_id, np.asarray(words), blob_words)
     else:
         srv = m.new_struct(0, 3)
         m.set_root(srv)

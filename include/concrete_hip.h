@@ -107,7 +107,8 @@ void cuda_negate_lwe_ciphertext_vector_64(void *stream, uint32_t gpu_index, void
  * Part 2: extensions (return 0 on success, < 0 on error; message via concrete_hip_last_error)
  * ------------------------------------------------------------------------------------------ */
 
-/* ABI version of this header (2: round 3 — context-resolved memref_*_cuda_u64, stream emulator). */
+/* ABI version of this header (2: round 3 — context-resolved memref_*_cuda_u64, stream emulator;
+ * 3: round 4 — keyswitch support query, key level-order check against client keys). */
 uint32_t concrete_hip_abi_version(void);
 /* thread-local message of the last failed concrete_hip_* call */
 const char *concrete_hip_last_error(void);
@@ -460,6 +461,18 @@ int concrete_hip_server_keyset_bsk_info(const concrete_hip_server_keyset *sk, ui
 int concrete_hip_server_keyset_ksk_info(const concrete_hip_server_keyset *sk, uint32_t index,
                                         concrete_hip_key_info *out);
 /* the standard-domain key (BSK [n][l][k+1][k+1][N], KSK [n_in][l][n_out+1]); dst holds >= key_words */
+/* Level order of evaluation key `index` (is_bsk: bootstrap, else keyswitch), found when it was last
+ * read (read_bsk / read_ksk / keyset_add_server_keyset) against the client secret keys a Keyset
+ * message carries: one GGSW / keyswitch row per level is decrypted.  A key stored in the reversed
+ * level order is re-ordered on read; one that decrypts in neither order is refused (round 4). */
+enum {
+  CONCRETE_HIP_LEVEL_ORDER_UNCHECKED = 0,   /* no client keys (ServerKeyset), one level, or not read yet */
+  CONCRETE_HIP_LEVEL_ORDER_AS_EXPECTED = 1, /* the order the standard layouts assume */
+  CONCRETE_HIP_LEVEL_ORDER_REVERSED = 2     /* stored reversed: re-ordered on read */
+};
+int concrete_hip_server_keyset_level_order(const concrete_hip_server_keyset *sk, int is_bsk, uint32_t index);
+/* client secret keys read from a Keyset message (0 for the other roots) */
+uint32_t concrete_hip_server_keyset_secret_count(const concrete_hip_server_keyset *sk);
 int concrete_hip_server_keyset_read_bsk(const concrete_hip_server_keyset *sk, uint32_t index, uint64_t *dst,
                                         uint64_t dst_words);
 int concrete_hip_server_keyset_read_ksk(const concrete_hip_server_keyset *sk, uint32_t index, uint64_t *dst,

@@ -399,3 +399,65 @@ def test_keyswitch_support_is_checked_before_expansion():
     assert lib.concrete_hip_keyswitch_supported(2, 4, 1024, 65535) == 1
     assert lib.concrete_hip_keyswitch_supported(2, 4, 1024, 65536) == 0
     assert lib.concrete_hip_keyswitch_supported(2, 4, 1024, 0xFFFFFFFF) == 0  # n_out + 1 wraps in u32
+
+
+# ---- (f) level orders, checked against the client secret keys of a Keyset message ---------------
+def _reverse_levels(key: np.ndarray, n: int, l: int) -> np.ndarray:
+    return key.reshape(n, l, -1)[:, ::-1, :].copy().ravel()
+
+
+def test_level_order_checked_against_client_keys():
+    """the GGSW level order (level 1 first, keygen.cpp) and the keyswitch key's
+    reversed levels are restated, not pinned.  A Keyset message carries the client secret keys, so
+    on read one row per level is decrypted: a key in the expected order passes, a level-reversed key
+    is detected and re-ordered, one that decrypts in neither order is refused, and a ServerKeyset
+    (no secret keys) stays unchecked."""
+    from dataclasses import dataclass
+
+    from concrete_amd import backend as B
+
+    @dataclass
+    class P:
+        n: int = 12
+        k: int = 2
+        N: int = 64
+        level: int = 3
+        base_log: int = 7
+        ks_level: int = 4
+        ks_base_log: int = 5
+
+        @property
+        def big_n(self):
+            return self.k * self.N
+
+        bsk_len = property(lambda s: s.n * s.level * (s.k + 1) ** 2 * s.N)
+        ksk_len = property(lambda s: s.big_n * s.ks_level * (s.n + 1))
+
+    p = P()
+    lwe_sk = B.binary_key(p.n, 31)
+    glwe_sk = B.binary_key(p.big_n, 32)
+    assert lwe_sk.any() and glwe_sk.any()
+    bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 33, std=2.0 ** -45)
+    ksk = B.ksk_generate(p, glwe_sk, lwe_sk, 34, std=2.0 ** -45)
+    bi = [K.bsk_info(p, id=i, input_id=0, output_id=1) for i in range(3)]
+    ki = [K.ksk_info(p, id=10 + i, input_id=1, output_id=0) for i in range(3)]
+    rng = np.random.default_rng(35)
+    junk_b = rng.integers(0, 2 ** 64, size=bsk.size, dtype=np.uint64)
+    junk_k = rng.integers(0, 2 ** 64, size=ksk.size, dtype=np.uint64)
+    bsks = [(bi[0], bsk), (bi[1], _reverse_levels(bsk, p.n, p.level)), (bi[2], junk_b)]
+    ksks = [(ki[0], ksk), (ki[1], _reverse_levels(ksk, p.big_n, p.ks_level)), (ki[2], junk_k)]
+    data = K.serialize_server_keyset(bsks, ksks, root="keyset", layout="mixed", secrets=[(0, lwe_sk), (1, glwe_sk)])
+    sk = K.ServerKeyset.deserialize(data, "keyset")
+    assert sk.secret_count == 2
+    assert sk.level_order("bsk", 0) == "unchecked"  # not read yet
+    assert np.array_equal(sk.bsk(0), bsk) and sk.level_order("bsk", 0) == "as_expected"
+    assert np.array_equal(sk.bsk(1), bsk) and sk.level_order("bsk", 1) == "reversed"
+    assert np.array_equal(sk.ksk(0), ksk) and sk.level_order("ksk", 0) == "as_expected"
+    assert np.array_equal(sk.ksk(1), ksk) and sk.level_order("ksk", 1) == "reversed"
+    for kind in ("bsk", "ksk"):
+        with pytest.raises(RuntimeError, match="in either level order"):
+            getattr(sk, kind)(2)
+    # the same keys in a ServerKeyset message: nothing to check against
+    srv = K.ServerKeyset.deserialize(K.serialize_server_keyset(bsks[:2], ksks[:2]))
+    assert srv.secret_count == 0
+    assert np.array_equal(srv.bsk(1), bsks[1][1]) and srv.level_order("bsk", 1) == "unchecked"

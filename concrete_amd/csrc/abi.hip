@@ -4,6 +4,7 @@
 // keep the reference conventions: void return, abort on failure, stream-ordered work.
 // The concrete_hip_* extensions return status codes for testability.
 #include <stdarg.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <mutex>
@@ -91,6 +92,25 @@ static uint32_t* status_word(int gpu) {
 }
 
 SyncGuard sync_guard(int gpu) { return SyncGuard{status_word(gpu), g_spin_limit.load(std::memory_order_relaxed)}; }
+
+void report_hip_state(FILE* f) {
+  int n = -1;
+  const hipError_t e = hipGetDeviceCount(&n);
+  int dev = -1;
+  (void)hipGetDevice(&dev);
+  fprintf(f, "concrete-hip: process %d: hipGetDeviceCount -> %s, %d device(s); current device %d", (int)getpid(),
+          hipGetErrorString(e), n, dev);
+  for (const char* v : {"HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL"})
+    if (const char* x = getenv(v)) fprintf(f, "; %s=%s", v, x);
+  fprintf(f, "\n");
+  fflush(f);
+}
+
+[[noreturn]] void hip_fatal(const char* expr, const char* file, int line, hipError_t e) {
+  fprintf(stderr, "concrete-hip: %s failed at %s:%d: %s\n", expr, file, line, hipGetErrorString(e));
+  report_hip_state(stderr);
+  abort();
+}
 
 int take_device_status(int gpu) {
   uint32_t* w;

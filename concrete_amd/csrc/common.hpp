@@ -12,12 +12,14 @@ namespace chip {
 #define CHIP_CHECK(expr)                                                                      \
   do {                                                                                        \
     hipError_t _e = (expr);                                                                   \
-    if (_e != hipSuccess) {                                                                   \
-      fprintf(stderr, "concrete-hip: %s failed at %s:%d: %s\n", #expr, __FILE__, __LINE__,    \
-              hipGetErrorString(_e));                                                         \
-      abort();                                                                                \
-    }                                                                                         \
+    if (_e != hipSuccess) ::chip::hip_fatal(#expr, __FILE__, __LINE__, _e);                   \
   } while (0)
+
+// abi.hip: prints the failed call, the HIP error, what hipGetDeviceCount reports now and the
+// device-visibility environment (the round-3 abort left no such record), flushes, aborts
+[[noreturn]] void hip_fatal(const char* expr, const char* file, int line, hipError_t e);
+// the same state report without aborting (rt_die)
+void report_hip_state(FILE* f);
 
 // Error state for the concrete_hip_* extension entry points (which return status codes).
 void set_error(const char* fmt, ...);

@@ -1920,8 +1920,8 @@ static bool tile_dispatch(uint32_t N, uint32_t K1, uint32_t KL, uint32_t T, uint
 // (or CONCRETE_HIP_GEN_FUSED=0, A/B runs): the two-launch path runs.
 static bool fused_dispatch(const FusedArgs& f, uint32_t k, uint32_t N, uint32_t level, uint32_t T, uint32_t L,
                            hipStream_t st) {
-  static const bool on = !getenv("CONCRETE_HIP_GEN_FUSED") || atoi(getenv("CONCRETE_HIP_GEN_FUSED")) != 0;
-  if (!on || k != 1 || N != 4096 || !four_step(N)) return false;
+  const char* fe = getenv("CONCRETE_HIP_GEN_FUSED");  // read per call (tests cover both paths)
+  if ((fe && atoi(fe) == 0) || k != 1 || N != 4096 || !four_step(N)) return false;
   const bool w32 = (uint64_t)level * f.base_log <= 31;
 #define GEN_FUSED(LVv, Tv, Lv)                                                                               \
   if (level == LVv && T == Tv && L == Lv) {                                                                  \

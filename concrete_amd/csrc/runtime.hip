@@ -42,6 +42,7 @@ void rt_die(const char* fmt, ...) {
   vfprintf(stderr, fmt, ap);
   fprintf(stderr, "\n");
   va_end(ap);
+  report_hip_state(stderr);
   abort();
 }
 

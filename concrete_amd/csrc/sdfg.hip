@@ -115,7 +115,7 @@ std::atomic<uint64_t> g_clock{0};
 
 std::vector<uint32_t> default_devices() {
   const int visible = concrete_hip_device_count();
-  if (visible <= 0) rt_die("stream_emulator_init: no GPUs available on system");
+  if (visible <= 0) rt_die("stream_emulator_init: no GPUs available on system (device count %d)", visible);
   std::vector<uint32_t> d;
   if (const char* e = getenv("CONCRETE_HIP_SDFG_DEVICES")) {
     for (const char* p = e; *p;) {

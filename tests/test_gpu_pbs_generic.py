@@ -95,10 +95,11 @@ def test_generic_pbs_bit_exact(B, oracle, torch_cuda, case):
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
 
 
-@pytest.mark.parametrize("ci", [0, 2, 3], ids=[CASES[i][0] for i in (0, 2, 3)])
+@pytest.mark.parametrize("ci", [0, 2, 3, 5], ids=[CASES[i][0] for i in (0, 2, 3, 5)])
 def test_generic_tile_many_workgroups(B, oracle, torch_cuda, ci):
     """The one-launch tile kernels over many workgroups (67 ciphertexts: not a multiple of any
-    tile size, so the last workgroup runs empty groups), bit-exact vs the exact oracle."""
+    tile size, so the last workgroup runs empty groups) and the one-launch N = 4096 kernel (a
+    workgroup per ciphertext), bit-exact vs the exact oracle."""
     case = CASES[ci][:3] + (4,) + CASES[ci][4:]
     p, glwe_sk, bsk, fbsk, cts, acc, table, msgs, got, resid = run_case(B, oracle, torch_cuda, case, 7500, batch=67)
     op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
@@ -170,7 +171,7 @@ def test_generic_legacy_step_kernel(B, oracle, torch_cuda):
     assert r.returncode == 0 and "legacy ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
-@pytest.mark.parametrize("streams", [1, 2, 3])
+@pytest.mark.parametrize("streams", [0, 1, 2, 3])
 @pytest.mark.parametrize("ci", [5, 7], ids=[CASES[i][0] for i in (5, 7)])
 def test_generic_chunked_two_streams(B, oracle, torch_cuda, ci, streams, monkeypatch):
     """The two-launch path over several chunks (CONCRETE_HIP_GEN_CHUNK=3 on 7 ciphertexts: 3
@@ -192,6 +193,9 @@ def test_generic_chunked_two_streams(B, oracle, torch_cuda, ci, streams, monkeyp
     out = torch_cuda.zeros((7, p.lwe_out_size), dtype=torch_cuda.int64, device=dev)
     monkeypatch.setenv("CONCRETE_HIP_GEN_CHUNK", "3")
     monkeypatch.setenv("CONCRETE_HIP_GEN_STREAMS", str(streams))
+    # N = 4096 has the one-launch kernel (gen_fused_kernel): streams = 0 runs it on the same index
+    # arrays, the others force the two-launch path this test is about
+    monkeypatch.setenv("CONCRETE_HIP_GEN_FUSED", "1" if streams == 0 else "0")
     B.pbs(p, fbsk, B.to_device(cts, dev), B.to_device(luts, dev), out=out, **d)
     torch_cuda.cuda.synchronize()
     op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)

@@ -18,6 +18,7 @@ step() {  # name timeout cmd...
   return 0
 }
 step child_init 240 python -u tools/microbench/child_first_init.py
+step unmap_stall 180 python -u tools/microbench/unmap_stall.py
 step generic 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_pbs_generic.py -k "N4096 or ln2 or index_arrays"
 step runtime 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_runtime.py tests/test_gpu_sdfg.py
 step bench_opt6 300 python -u bench.py --config opt6 --steps 3 --warmup 1 --no-cpu-baseline --no-ks

@@ -38,6 +38,10 @@
 #include "pbs.hpp"
 #include "companion.hpp"
 
+#ifndef MAC_CTS
+#define MAC_CTS 16  // ciphertexts per block (key values loaded once per tile)
+#endif
+
 namespace chip {
 
 // abi.hip: raise the device's default memory-pool release threshold once, so stream-ordered
@@ -80,7 +84,7 @@ double generic_error_bound(uint32_t k, uint32_t N, uint32_t level, uint32_t base
 // Levels up to 64 (l logB <= 64: the optimizer's rows reach l = 44 at logB = 1, v0_last_128).
 static bool generic_shape_ok(uint32_t k, uint32_t N, uint32_t level) {
   if (k < 1 || k > (uint32_t)GEN_MAX_K || level < 1 || level > 64) return false;
-  return N >= 256 && N <= 16384 && (N & (N - 1)) == 0;
+  return N >= 256 && N <= 65536 && (N & (N - 1)) == 0;
 }
 
 // Limb width b for (k, N, l): the widest b whose bound holds for digits of up to 2b bits
@@ -950,6 +954,476 @@ __global__ void __launch_bounds__(Big<M>::NT) gen_big_step_kernel(StepArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// N = 32768 / 65536 (the optimizer's 9- and 10-bit rows, v0_last_128): a polynomial spread over
+// S = N / 16384 workgroups (round 4).  The M-point spectrum (M = R x 512, R = 32 / 64 rows of the
+// four-step order) no longer fits one CU's LDS, so the R-point column DFT splits by row class:
+// with j1 = S a + h (h < S, a < 16) and f = k2 + 512 k1,
+//   Z_f = sum_h w_R^{h k1} G_h[k1 mod 16](k2),  G_h = DFT16_a( tau(S a + h, k2) FFT512_{S a + h}[k2] )
+// i.e. workgroup h of a polynomial runs the 16 rows of its class exactly as gen_big_step_kernel
+// runs an M' = 8192 polynomial (fft512 rows in registers, tau, one LDS exchange, DFT16 columns) and
+// writes G_h; the product kernel combines the S classes when it loads X (gen_mac_split_kernel), and
+// the inverse splits Y back the same way, H_h[k1'] = sum_u conj(w_R^{h (k1' + 16 u)}) Y[k1' + 16 u],
+// before workgroup h's inverse DFT16 and row transforms.  Every path through the transform still
+// has log2 M butterfly stages with at most log2 M inexact twiddle products, each a correctly rounded
+// table entry (tau, w_R) or fft512 / DFT16 constant, so generic_error_bound holds unchanged.  The
+// front half (rotation, decomposition, forward transforms) reads the rotated accumulator rows of
+// the other classes from HBM, so the back half and the front half are separate launches.
+// ------------------------------------------------------------------------------------------
+constexpr int SPLIT_ROWS = 16;  // rows per workgroup (the M' = 8192 four-step shape)
+
+struct SplitArgs {
+  uint64_t* acc;        // [chunk][K1][N] in the four-step row order (n at (n mod R) ROWLEN + n / R)
+  cplx* X;              // [chunk][K1 r][l q][T t][S h][16][512]: the column-class transforms G_h
+  const cplx* Y;        // [chunk][K1 c][L m][M], position p = k1 512 + pos (k1 < R)
+  const cplx* Tau;      // tau(j1, pos) [R][512], then the slot factors [R][8]
+  const cplx* WR;       // w_R^x = exp(-2 pi i x / R), x < R
+  const uint64_t* in;   // LWE inputs (rows of n + 1)
+  const uint64_t* in_idx;
+  const uint64_t* luts;
+  const uint64_t* lut_idx;
+  unsigned long long* resid;
+  uint32_t base, count, n, k, level, base_log, bits, limbs, subs;
+  uint32_t step;  // front: the mask position whose rotation is prepared
+};
+
+template <int S>
+struct Split {
+  static constexpr int R = SPLIT_ROWS * S, M = R * 512, N = 2 * M;
+  static constexpr int LOGR = S == 2 ? 5 : 6;
+  static constexpr int NT = 512, SPW = 2, RS = 576;  // 8 waves, two rows each
+  static constexpr int LDS_CPLX = SPLIT_ROWS * RS + FFT512_TABLE_ENTRIES + SPLIT_ROWS * 8;
+  static_assert(S == 2 || S == 4, "split");
+  static_assert(LDS_CPLX * 16 <= 160 * 1024, "LDS");
+};
+
+// acc = LUT * X^{-ms(b)}, row order (blind_rotate_assign: polynomial_wrapping_monic_monomial_div)
+template <int S>
+__global__ void __launch_bounds__(256) gen_split_init_kernel(SplitArgs a) {
+  using G = Split<S>;
+  constexpr int N = G::N, LOG2_2N = G::LOGR + 9 + 2;
+  const uint32_t K1 = a.k + 1;
+  const uint64_t total = (uint64_t)a.count * K1 * N;
+  for (uint64_t g = blockIdx.x * 256ull + threadIdx.x; g < total; g += (uint64_t)gridDim.x * 256) {
+    const uint32_t nn = (uint32_t)(g % N);
+    const uint64_t poly = g / N;
+    const uint32_t ct = (uint32_t)(poly / K1), c = (uint32_t)(poly % K1), s = a.base + ct;
+    const uint64_t row = a.in_idx ? a.in_idx[s] : s;
+    const uint32_t bt = modswitch(a.in[row * (uint64_t)(a.n + 1) + a.n], LOG2_2N);
+    const uint64_t* lut = a.luts + (a.lut_idx ? a.lut_idx[s] : 0ull) * (uint64_t)(K1 * N) + (uint64_t)c * N;
+    const uint32_t src = (nn + bt) & (2 * N - 1);
+    const uint64_t v = lut[src & (N - 1)];
+    a.acc[poly * N + (uint64_t)(nn & (G::R - 1)) * (N / G::R) + (nn >> G::LOGR)] = src < (uint32_t)N ? v : 0ull - v;
+  }
+}
+
+// The rows of class h of one polynomial: tables, tau factors (lane factor in registers, slot factor
+// in LDS, as gen_big_step_kernel at R = 16) and the global row of local row jl.
+template <int S>
+struct SplitRows {
+  cplx* E;
+  cplx* beta;
+  Fft512Tables T;
+  cplx tau_r[2];
+  int w, lane, h;
+  __device__ int jg(int sr) const { return S * (w * 2 + sr) + h; }
+  __device__ cplx tau(int sr, int e) const { return e == 0 ? tau_r[sr] : cmul(tau_r[sr], beta[(w * 2 + sr) * 8 + e]); }
+};
+
+template <int S>
+__device__ __forceinline__ SplitRows<S> split_rows_setup(cplx* lds, const SplitArgs& a, int h) {
+  using G = Split<S>;
+  SplitRows<S> q;
+  q.E = lds;
+  build_fft512_tables(lds + SPLIT_ROWS * G::RS, threadIdx.x, G::NT);
+  q.beta = lds + SPLIT_ROWS * G::RS + FFT512_TABLE_ENTRIES;
+  q.w = threadIdx.x >> 6, q.lane = threadIdx.x & 63, q.h = h;
+  for (int x = threadIdx.x; x < SPLIT_ROWS * 8; x += G::NT)
+    q.beta[x] = a.Tau[G::R * 512 + (S * (x >> 3) + h) * 8 + (x & 7)];
+  q.T = fft512_tables_at(lds + SPLIT_ROWS * G::RS);
+#pragma unroll
+  for (int sr = 0; sr < 2; ++sr) q.tau_r[sr] = a.Tau[q.jg(sr) * 512 + q.lane];
+  return q;
+}
+
+// front: X^{a_i} acc - acc from the accumulator in HBM, decomposition, sub-digits, the class-h
+// transforms of every digit polynomial -> X (G_h)
+template <int S, bool W32>
+__global__ void __launch_bounds__(512) gen_split_front_kernel(SplitArgs a) {
+  using G = Split<S>;
+  constexpr int N = G::N, R = G::R, RS = G::RS, LOG2_2N = G::LOGR + 9 + 2, ROWLEN = N / R;
+  using St = typename std::conditional<W32, uint32_t, uint64_t>::type;
+  using Dg = typename std::conditional<W32, int32_t, int64_t>::type;
+  __shared__ cplx lds[G::LDS_CPLX];
+  const uint32_t K1 = a.k + 1, h = blockIdx.x % S, poly = blockIdx.x / S, ct = poly / K1;
+  const SplitRows<S> q = split_rows_setup<S>(lds, a, (int)h);
+  const int lane = q.lane;
+  cplx* xch = q.E + q.w * 2 * RS;  // the wave's first row and its pad
+  const uint32_t s = a.base + ct;
+  const uint64_t row = a.in_idx ? a.in_idx[s] : s;
+  const uint32_t at = modswitch(a.in[row * (uint64_t)(a.n + 1) + a.step], LOG2_2N);
+  const uint64_t* acc = a.acc + (uint64_t)poly * N;
+  auto jcol = [&](int e) { return lane + 64 * (e & 7) + 512 * (e >> 3); };
+  const int nrep = 64 - (int)(a.level * a.base_log);
+  St Sx[2][16];
+#pragma unroll
+  for (int sr = 0; sr < 2; ++sr)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t nn = (uint32_t)(q.jg(sr) + R * jcol(e));
+      const uint32_t src = (nn - at) & (2 * N - 1), idx = src & (N - 1);
+      const uint64_t rv = acc[(uint64_t)(idx & (R - 1)) * ROWLEN + (idx >> G::LOGR)];
+      const uint64_t x = (src < (uint32_t)N ? rv : 0ull - rv) - acc[(uint64_t)q.jg(sr) * ROWLEN + jcol(e)];
+      Sx[sr][e] = (St)(nrep > 0 ? decomp_init(x, nrep) : x);
+    }
+  pair_barrier();  // fft512 tables, beta
+  cplx* Xc = a.X + (uint64_t)poly * a.level * a.subs * S * (SPLIT_ROWS * 512) + (uint64_t)h * SPLIT_ROWS * 512;
+  const int logB = (int)a.base_log, sb = (int)a.bits;
+  const bool split = a.subs > 1;
+  const St half = split ? (St)1 << (sb - 1) : (St)0, bmask = split ? ((St)1 << sb) - (St)1 : ~(St)0;
+#pragma unroll 1
+  for (uint32_t qq = 0; qq < a.level; ++qq) {
+    Dg D[2][16];
+#pragma unroll
+    for (int sr = 0; sr < 2; ++sr)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        if constexpr (W32) D[sr][e] = decomp_next_t<uint32_t>(Sx[sr][e], logB);
+        else D[sr][e] = decomp_next64(Sx[sr][e], logB);
+      }
+#pragma unroll 1
+    for (uint32_t t = 0; t < a.subs; ++t) {
+      cplx hold[8];  // the first row's spectrum, until the second row's transform is done
+#pragma unroll
+      for (int sr = 0; sr < 2; ++sr) {
+        cplx v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const Dg s0 = (Dg)(((St)D[sr][e] + half) & bmask) - (Dg)half;
+          const Dg s1 = (Dg)(((St)D[sr][e + 8] + half) & bmask) - (Dg)half;
+          D[sr][e] = (D[sr][e] - s0) >> sb;
+          D[sr][e + 8] = (D[sr][e + 8] - s1) >> sb;
+          v[e] = {(double)s0, (double)s1};
+        }
+        fft512_fwd(v, xch, q.T, lane);
+        if (q.jg(sr) != 0)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = cmul(v[e], q.tau(sr, e));
+        if (sr == 0) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) hold[e] = v[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) q.E[(q.w * 2 + 1) * RS + e * 64 + lane] = v[e];
+        }
+      }
+      wave_lds_fence();
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q.E[(q.w * 2) * RS + e * 64 + lane] = hold[e];
+      pair_barrier();
+      cplx* dst = Xc + ((uint64_t)qq * a.subs + t) * S * (SPLIT_ROWS * 512);
+      const int pos = threadIdx.x;
+      cplx u[SPLIT_ROWS];
+#pragma unroll
+      for (int jl = 0; jl < SPLIT_ROWS; ++jl) u[jl] = q.E[jl * RS + pos];
+      dft_col<SPLIT_ROWS, false>(u);
+#pragma unroll
+      for (int k1 = 0; k1 < SPLIT_ROWS; ++k1) dst[k1 * 512 + pos] = u[k1];
+      pair_barrier();
+    }
+  }
+}
+
+// back: acc += sum_m 2^{m b} round(iFFT(Y_m) conj(zeta^j)) for the rows of class h
+template <int S>
+__global__ void __launch_bounds__(512) gen_split_back_kernel(SplitArgs a) {
+  using G = Split<S>;
+  constexpr int N = G::N, R = G::R, RS = G::RS, M = G::M, ROWLEN = N / R;
+  __shared__ cplx lds[G::LDS_CPLX];
+  const uint32_t h = blockIdx.x % S, poly = blockIdx.x / S;
+  const SplitRows<S> q = split_rows_setup<S>(lds, a, (int)h);
+  const int lane = q.lane, pos = threadIdx.x;
+  cplx* xch = q.E + q.w * 2 * RS;
+  uint64_t* acc = a.acc + (uint64_t)poly * N;
+  auto jcol = [&](int e) { return lane + 64 * (e & 7) + 512 * (e >> 3); };
+  uint64_t A[2][16];
+#pragma unroll
+  for (int sr = 0; sr < 2; ++sr)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) A[sr][e] = acc[(uint64_t)q.jg(sr) * ROWLEN + jcol(e)];
+  // conj(w_R^{h (k1' + 16 u)}) for this class, k1' < 16, u < S
+  const cplx* Yc = a.Y + (uint64_t)poly * a.limbs * M + pos;
+  double max_resid = 0.0;
+  pair_barrier();  // fft512 tables, beta
+#pragma unroll 1
+  for (uint32_t m = 0; m < a.limbs; ++m) {
+    const cplx* Ym = Yc + (uint64_t)m * M;
+    cplx u[SPLIT_ROWS];
+#pragma unroll
+    for (int k1 = 0; k1 < SPLIT_ROWS; ++k1) {
+      cplx hsum = {0.0, 0.0};
+#pragma unroll
+      for (int uu = 0; uu < S; ++uu) {
+        const int kk = k1 + SPLIT_ROWS * uu;
+        const cplx y = Ym[(uint64_t)kk * 512];
+        const cplx w = a.WR[(h * kk) & (R - 1)];
+        hsum = cadd(hsum, cmulc(y, w));
+      }
+      u[k1] = hsum;
+    }
+    dft_col<SPLIT_ROWS, true>(u);
+#pragma unroll
+    for (int jl = 0; jl < SPLIT_ROWS; ++jl) q.E[jl * RS + pos] = u[jl];
+    pair_barrier();
+    const uint32_t sh = (m * a.bits) & 63u;
+#pragma unroll
+    for (int sr = 0; sr < 2; ++sr) {
+      // row 0 of the wave is read whole before its transform writes the scratch over it
+      cplx v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = q.E[(q.w * 2 + sr) * RS + e * 64 + lane];
+      wave_lds_fence();
+      if (q.jg(sr) != 0)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = cmulc(v[e], q.tau(sr, e));
+      cplx gi2[4];
+      inv_p2_stage_tw(gi2, q.T, lane & 7);
+      fft512_inv_tw(v, xch, q.T, lane, gi2, 0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const double tr = v[e].re + RND_MAGIC, ti = v[e].im + RND_MAGIC;
+        max_resid = fmax(max_resid, fmax(fabs(v[e].re - (tr - RND_MAGIC)), fabs(v[e].im - (ti - RND_MAGIC))));
+        A[sr][e] += ((uint64_t)__double_as_longlong(tr) - RND_MAGIC_BITS) << sh;
+        A[sr][e + 8] += ((uint64_t)__double_as_longlong(ti) - RND_MAGIC_BITS) << sh;
+      }
+    }
+    pair_barrier();
+  }
+#pragma unroll
+  for (int sr = 0; sr < 2; ++sr)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[(uint64_t)q.jg(sr) * ROWLEN + jcol(e)] = A[sr][e];
+  if (a.resid) {
+    for (int off = 32; off > 0; off >>= 1) max_resid = fmax(max_resid, __shfl_xor(max_resid, off));
+    if (lane == 0) atomicMax(a.resid, (unsigned long long)__double_as_longlong(max_resid));
+  }
+}
+
+// Y[ct][c][m][p] = sum over (r, q, t) with 0 <= m - t < L of X_p[r][q][t] G_i[c][m-t][r][q][p], with
+// X_p = sum_h w_R^{h k1} G_h[k1 mod 16][pos] combined on load (p = k1 512 + pos): one thread per
+// (position, output polynomial), the key values of the thread in registers across the tile
+struct MacSplitArgs {
+  const cplx* X;
+  cplx* Y;
+  const cplx* G;  // Fourier key [n][K1 c][L lim][K1 l rq][M]
+  const cplx* WR;
+  uint32_t count, k, level, limbs, subs, M, R;
+  uint32_t i;
+};
+
+template <int KL, int L, int T, int S>
+__global__ void __launch_bounds__(256) gen_mac_split_kernel(MacSplitArgs a) {
+  const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t c = blockIdx.y, K1 = a.k + 1;
+  const uint64_t M = a.M;
+  if (p >= M) return;
+  const uint32_t k1 = p >> 9, pos = p & 511, kl = k1 & (SPLIT_ROWS - 1);
+  cplx wr[S];
+#pragma unroll
+  for (int h = 0; h < S; ++h) wr[h] = a.WR[(h * k1) & (a.R - 1)];
+  cplx kv[L][KL];
+#pragma unroll
+  for (int lim = 0; lim < L; ++lim)
+#pragma unroll
+    for (int rq = 0; rq < KL; ++rq) kv[lim][rq] = a.G[((((uint64_t)a.i * K1 + c) * L + lim) * KL + rq) * M + p];
+  const uint32_t ct0 = blockIdx.z * MAC_CTS;
+  for (uint32_t ct = ct0; ct < ct0 + MAC_CTS && ct < a.count; ++ct) {
+    const cplx* Xct = a.X + (uint64_t)ct * KL * T * M + (uint64_t)kl * 512 + pos;
+    cplx xv[KL][T];
+#pragma unroll
+    for (int rq = 0; rq < KL; ++rq)
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const cplx* g = Xct + (uint64_t)(rq * T + t) * M;
+        cplx x = g[0];  // class 0: w_R^0 = 1
+#pragma unroll
+        for (int h = 1; h < S; ++h) {
+          const cplx gh = g[(uint64_t)h * SPLIT_ROWS * 512], w = wr[h];
+          x.re = __builtin_fma(gh.re, w.re, __builtin_fma(-gh.im, w.im, x.re));
+          x.im = __builtin_fma(gh.re, w.im, __builtin_fma(gh.im, w.re, x.im));
+        }
+        xv[rq][t] = x;
+      }
+    cplx* Yct = a.Y + ((uint64_t)ct * K1 + c) * L * M + p;
+#pragma unroll
+    for (int m = 0; m < L; ++m) {
+      cplx y = {0.0, 0.0};
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        if (m - t < 0 || m - t >= L) continue;
+#pragma unroll
+        for (int rq = 0; rq < KL; ++rq) {
+          const cplx xg = xv[rq][t], g = kv[m - t][rq];
+          y.re = __builtin_fma(xg.re, g.re, __builtin_fma(-xg.im, g.im, y.re));
+          y.im = __builtin_fma(xg.re, g.im, __builtin_fma(xg.im, g.re, y.im));
+        }
+      }
+      Yct[(uint64_t)m * M] = y;
+    }
+  }
+}
+
+// Any (k, l, T, L): one thread per (position, output polynomial, slot), the key values of
+// GEN_MAX_TERMS terms at a time in registers (as gen_mac_kernel), X combined on load.
+template <int S>
+__global__ void __launch_bounds__(256) gen_mac_split_generic_kernel(MacSplitArgs a) {
+  const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t K1 = a.k + 1, L = a.limbs, T = a.subs;
+  const uint32_t c = blockIdx.y / L, m = blockIdx.y % L;
+  const uint32_t terms = K1 * a.level * T;
+  const uint64_t M = a.M;
+  if (p >= M) return;
+  const uint32_t k1 = p >> 9, pos = p & 511, kl = k1 & (SPLIT_ROWS - 1);
+  cplx wr[S];
+#pragma unroll
+  for (int h = 0; h < S; ++h) wr[h] = a.WR[(h * k1) & (a.R - 1)];
+  const uint32_t ct0 = blockIdx.z * MAC_CTS;
+#pragma unroll 1
+  for (uint32_t x0 = 0; x0 < terms; x0 += GEN_MAX_TERMS) {
+    cplx kv[GEN_MAX_TERMS];
+#pragma unroll
+    for (int x = 0; x < GEN_MAX_TERMS; ++x) {
+      kv[x] = {0.0, 0.0};
+      const uint32_t xx = x0 + x;
+      if (xx < terms) {
+        const uint32_t t = xx % T, rq = xx / T;  // xx = (r l + q) T + t
+        if (m >= t && m - t < L) kv[x] = a.G[((((uint64_t)a.i * K1 + c) * L + (m - t)) * K1 * a.level + rq) * M + p];
+      }
+    }
+    for (uint32_t ct = ct0; ct < ct0 + MAC_CTS && ct < a.count; ++ct) {
+      const cplx* Xct = a.X + (uint64_t)ct * terms * M + (uint64_t)kl * 512 + pos;
+      cplx* Yp = a.Y + (((uint64_t)ct * K1 + c) * L + m) * M + p;
+      cplx y = x0 ? *Yp : cplx{0.0, 0.0};
+#pragma unroll
+      for (int x = 0; x < GEN_MAX_TERMS; ++x) {
+        if (x0 + x < terms) {
+          const cplx* g = Xct + (uint64_t)(x0 + x) * M;
+          cplx xv = g[0];
+#pragma unroll
+          for (int h = 1; h < S; ++h) xv = cadd(xv, cmul(g[(uint64_t)h * SPLIT_ROWS * 512], wr[h]));
+          y.re = __builtin_fma(xv.re, kv[x].re, __builtin_fma(-xv.im, kv[x].im, y.re));
+          y.im = __builtin_fma(xv.re, kv[x].im, __builtin_fma(xv.im, kv[x].re, y.im));
+        }
+      }
+      *Yp = y;
+    }
+  }
+}
+
+// Key conversion at N >= 32768: the class-h transforms of every limb of every standard polynomial
+// (the front kernel's transform with the limb as input) into scratch, then the combine and 1/M.
+struct SplitConvArgs {
+  cplx* Gs;             // [poly in batch][limb][S h][16][512]
+  const uint64_t* src;  // standard key, [i][v][r][c][N]
+  const cplx* Tau;
+  const cplx* WR;
+  cplx* dest;           // Fourier key [i][c][lim][r][q][M]
+  uint64_t poly0;       // first standard polynomial of this batch
+  uint32_t polys, k, level, bits, limbs;
+};
+
+template <int S>
+__global__ void __launch_bounds__(512) gen_split_convert_kernel(SplitConvArgs a) {
+  using G = Split<S>;
+  constexpr int N = G::N, R = G::R, RS = G::RS;
+  __shared__ cplx lds[G::LDS_CPLX];
+  const uint32_t h = blockIdx.x % S, item = blockIdx.x / S;  // item = (poly in batch, limb)
+  const uint32_t lim = item % a.limbs, pb = item / a.limbs;
+  SplitArgs t{};
+  t.Tau = a.Tau;
+  const SplitRows<S> q = split_rows_setup<S>(lds, t, (int)h);
+  const int lane = q.lane, pos = threadIdx.x;
+  cplx* xch = q.E + q.w * 2 * RS;
+  const uint64_t* g = a.src + (a.poly0 + pb) * (uint64_t)N;
+  auto jcol = [&](int e) { return lane + 64 * (e & 7) + 512 * (e >> 3); };
+  pair_barrier();  // fft512 tables, beta
+  cplx hold[8];
+#pragma unroll
+  for (int sr = 0; sr < 2; ++sr) {
+    cplx v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      // limb lim of the coefficient: balanced limbs as gen_convert_kernel (top limb in its own width)
+      int64_t sv[2];
+#pragma unroll
+      for (int z = 0; z < 2; ++z) {
+        uint64_t gv = g[(uint64_t)(q.jg(sr) + R * jcol(e + 8 * z))];
+        int64_t s0 = 0;
+        for (uint32_t j = 0; j <= lim; ++j) {
+          const uint32_t w = j + 1 < a.limbs ? a.bits : 64 - (a.limbs - 1) * a.bits;
+          const uint64_t half = 1ull << (w - 1), bmask = (1ull << w) - 1ull;
+          s0 = (int64_t)((gv + half) & bmask) - (int64_t)half;
+          gv = (gv - (uint64_t)s0) >> a.bits;
+        }
+        sv[z] = s0;
+      }
+      v[e] = {(double)sv[0], (double)sv[1]};
+    }
+    fft512_fwd(v, xch, q.T, lane);
+    if (q.jg(sr) != 0)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = cmul(v[e], q.tau(sr, e));
+    if (sr == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) hold[e] = v[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q.E[(q.w * 2 + 1) * RS + e * 64 + lane] = v[e];
+    }
+  }
+  wave_lds_fence();
+#pragma unroll
+  for (int e = 0; e < 8; ++e) q.E[(q.w * 2) * RS + e * 64 + lane] = hold[e];
+  pair_barrier();
+  cplx u[SPLIT_ROWS];
+#pragma unroll
+  for (int jl = 0; jl < SPLIT_ROWS; ++jl) u[jl] = q.E[jl * RS + pos];
+  dft_col<SPLIT_ROWS, false>(u);
+  cplx* dst = a.Gs + ((uint64_t)item * S + h) * SPLIT_ROWS * 512;
+#pragma unroll
+  for (int k1 = 0; k1 < SPLIT_ROWS; ++k1) dst[k1 * 512 + pos] = u[k1];
+}
+
+template <int S>
+__global__ void __launch_bounds__(256) gen_split_combine_kernel(SplitConvArgs a) {
+  using G = Split<S>;
+  constexpr int M = G::M, R = G::R;
+  const uint64_t total = (uint64_t)a.polys * a.limbs * M;
+  const uint32_t K1 = a.k + 1;
+  const double scale = 1.0 / (double)M;
+  for (uint64_t gi = blockIdx.x * 256ull + threadIdx.x; gi < total; gi += (uint64_t)gridDim.x * 256) {
+    const uint32_t p = (uint32_t)(gi % M);
+    const uint64_t item = gi / M;
+    const uint32_t lim = (uint32_t)(item % a.limbs);
+    const uint64_t pb = item / a.limbs;
+    const uint32_t k1 = p >> 9, pos = p & 511, kl = k1 & (SPLIT_ROWS - 1);
+    const cplx* gs = a.Gs + (item * S) * SPLIT_ROWS * 512 + (uint64_t)kl * 512 + pos;
+    cplx x = gs[0];
+#pragma unroll
+    for (int h = 1; h < S; ++h) x = cadd(x, cmul(gs[(uint64_t)h * SPLIT_ROWS * 512], a.WR[(h * k1) & (R - 1)]));
+    // standard polynomial index -> Fourier key slot (gen_convert_kernel)
+    uint64_t sp = a.poly0 + pb;
+    const uint32_t c = (uint32_t)(sp % K1);
+    sp /= K1;
+    const uint32_t r = (uint32_t)(sp % K1);
+    sp /= K1;
+    const uint32_t v = (uint32_t)(sp % a.level);
+    const uint64_t i = sp / a.level;
+    const uint32_t qq = a.level - 1 - v;
+    a.dest[((((i * K1 + c) * a.limbs + lim) * K1 + r) * a.level + qq) * (uint64_t)M + p] = {x.re * scale, x.im * scale};
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // N = 4096, k = 1: the whole blind rotation of a ciphertext in ONE workgroup and one launch, the
 // digit and slot spectra on chip (round 4).  The two-launch path above moves ~0.57 MB of X / Y
 // spectra and accumulator per ciphertext and CMUX step through HBM at N = 4096 (8x the
@@ -1180,9 +1654,6 @@ struct MacArgs {
   uint32_t count, k, level, limbs, subs, M;
   uint32_t i;  // GGSW index (LWE mask position)
 };
-#ifndef MAC_CTS
-#define MAC_CTS 16  // ciphertexts per block (key values loaded once per tile)
-#endif
 
 // Any number of terms: the key values of GEN_MAX_TERMS terms at a time in registers, the slot
 // sum carried through Y between the chunks (each thread re-reads only what it wrote).
@@ -1783,6 +2254,7 @@ struct Tables {
   cplx* Whi = nullptr;  // e^{-2 pi i j TW_LO/M}, j < max(1, M/TW_LO)
   cplx* Z = nullptr;    // zeta^j, j < M
   cplx* Tau = nullptr;  // four-step column twiddles tau(j1, k2(pos)) [R][512] (M >= 1024)
+  cplx* WR = nullptr;   // w_R^x = exp(-2 pi i x / R), x < R (N >= 32768: the column-class combine)
 };
 
 // Whether N runs on the four-step step kernel (and its keys are converted to the four-step
@@ -1837,6 +2309,10 @@ static Tables tables_for(uint32_t N) {
       }
     CHIP_CHECK(hipMalloc((void**)&t.Tau, tau.size() * sizeof(cplx)));
     CHIP_CHECK(hipMemcpy(t.Tau, tau.data(), tau.size() * sizeof(cplx), hipMemcpyHostToDevice));
+    std::vector<cplx> wr(R);
+    for (uint32_t x = 0; x < R; ++x) wr[x] = ex(-2.0L * PI * (long double)x / (long double)R);
+    CHIP_CHECK(hipMalloc((void**)&t.WR, R * sizeof(cplx)));
+    CHIP_CHECK(hipMemcpy(t.WR, wr.data(), R * sizeof(cplx), hipMemcpyHostToDevice));
   }
   cache[{dev, N}] = t;
   return t;
@@ -1936,6 +2412,107 @@ static bool fused_dispatch(const FusedArgs& f, uint32_t k, uint32_t N, uint32_t 
   return false;
 }
 
+// N >= 32768: the split path (S = N / 16384 workgroups per polynomial), one stream, chunks of
+// <= 2 GB of scratch run one after another: init, then per CMUX step the product, the back half
+// and the next step's front half.
+template <int S>
+static void launch_split_mac(const MacSplitArgs& m, uint32_t KL, uint32_t cnt, hipStream_t st) {
+  const dim3 g1((m.M + 255) / 256, m.k + 1, (cnt + MAC_CTS - 1) / MAC_CTS);
+  if (KL == 4 && m.limbs == 7 && m.subs == 2) {
+    hipLaunchKernelGGL((gen_mac_split_kernel<4, 7, 2, S>), g1, dim3(256), 0, st, m);
+    return;
+  }
+  const dim3 g2((m.M + 255) / 256, (m.k + 1) * m.limbs, (cnt + MAC_CTS - 1) / MAC_CTS);
+  hipLaunchKernelGGL((gen_mac_split_generic_kernel<S>), g2, dim3(256), 0, st, m);
+}
+
+template <int S>
+static void launch_split_front(const SplitArgs& s, uint32_t K1, hipStream_t st) {
+  const dim3 grid(s.count * K1 * S);
+  if ((uint64_t)s.level * s.base_log <= 31)
+    hipLaunchKernelGGL((gen_split_front_kernel<S, true>), grid, dim3(512), 0, st, s);
+  else
+    hipLaunchKernelGGL((gen_split_front_kernel<S, false>), grid, dim3(512), 0, st, s);
+}
+
+template <int S>
+static int pbs_split_launch(const PbsArgs& a, const KeyFormat& fmt, const Tables& tb, uint32_t T) {
+  using G = Split<S>;
+  const uint32_t K1 = a.k + 1, M = G::M, L = fmt.limbs;
+  const uint64_t per_ct = generic_scratch_bytes_per_sample(a.k, a.N, a.level, a.base_log);
+  const char* be = getenv("CONCRETE_HIP_GEN_BUDGET_MB");
+  const uint64_t budget = be && atoi(be) > 0 ? (uint64_t)atoi(be) << 20 : 2ull << 30;
+  const char* ce = getenv("CONCRETE_HIP_GEN_CHUNK");
+  const uint64_t cap = ce && atoi(ce) > 0 ? (uint64_t)atoi(ce) : 65536;
+  const uint32_t chunk = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(a.num_samples, cap),
+                                                      std::max<uint64_t>(1, budget / per_ct));
+  void* scratch = nullptr;
+  keep_pool_memory();
+  CHIP_CHECK(hipMallocAsync(&scratch, per_ct * chunk, a.stream));
+  hipStream_t st = a.stream;
+  for (uint32_t base = 0; base < a.num_samples; base += chunk) {
+    const uint32_t cnt = std::min(chunk, a.num_samples - base);
+    cplx* X = reinterpret_cast<cplx*>(scratch);
+    cplx* Y = X + (uint64_t)chunk * K1 * a.level * T * M;
+    uint64_t* acc = reinterpret_cast<uint64_t*>(Y + (uint64_t)chunk * K1 * L * M);
+    SplitArgs sa{acc, X, Y, tb.Tau, tb.WR, a.in, a.in_idx, a.luts, a.lut_idx, a.resid,
+                 base, cnt, a.n, a.k, a.level, a.base_log, fmt.bits, L, T, 0};
+    MacSplitArgs ma{X, Y, reinterpret_cast<const cplx*>(a.fbsk), tb.WR, cnt, a.k, a.level, L, T, M, G::R, 0};
+    const uint64_t elems = (uint64_t)cnt * K1 * a.N;
+    hipLaunchKernelGGL((gen_split_init_kernel<S>), dim3((uint32_t)std::min<uint64_t>((elems + 255) / 256, 65535)),
+                       dim3(256), 0, st, sa);
+    launch_split_front<S>(sa, K1, st);
+    for (uint32_t i = 0; i < a.n; ++i) {
+      ma.i = i;
+      launch_split_mac<S>(ma, K1 * a.level, cnt, st);
+      hipLaunchKernelGGL((gen_split_back_kernel<S>), dim3(cnt * K1 * S), dim3(512), 0, st, sa);
+      if (i + 1 < a.n) {
+        sa.step = i + 1;
+        launch_split_front<S>(sa, K1, st);
+      }
+    }
+    const uint64_t total = ((uint64_t)a.k * a.N + 1) * cnt;
+    const uint32_t eb = (uint32_t)std::min<uint64_t>((total + 255) / 256, 65535);
+    hipLaunchKernelGGL(gen_extract_kernel, dim3(eb), dim3(256), 0, st, a.out, a.out_idx, acc, base, cnt, a.k, a.N,
+                       (uint32_t)G::LOGR);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      set_error("generic pbs (split) launch failed: %s", hipGetErrorString(e));
+      CHIP_CHECK(hipFreeAsync(scratch, a.stream));
+      return -1;
+    }
+  }
+  CHIP_CHECK(hipFreeAsync(scratch, a.stream));
+  return 0;
+}
+
+template <int S>
+static int convert_split_launch(const ConvertArgs& a, const KeyFormat& fmt, const Tables& tb) {
+  using G = Split<S>;
+  const uint64_t polys = (uint64_t)a.n * a.level * (a.k + 1) * (a.k + 1);
+  const uint64_t per_poly = (uint64_t)fmt.limbs * G::M * sizeof(cplx);
+  const uint32_t batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(polys, (1ull << 30) / per_poly));
+  void* scratch = nullptr;
+  keep_pool_memory();
+  CHIP_CHECK(hipMallocAsync(&scratch, per_poly * batch, a.stream));
+  for (uint64_t p0 = 0; p0 < polys; p0 += batch) {
+    const uint32_t nb = (uint32_t)std::min<uint64_t>(batch, polys - p0);
+    SplitConvArgs c{reinterpret_cast<cplx*>(scratch), a.src_dev, tb.Tau, tb.WR, reinterpret_cast<cplx*>(a.dest), p0,
+                    nb, a.k, a.level, fmt.bits, fmt.limbs};
+    hipLaunchKernelGGL((gen_split_convert_kernel<S>), dim3(nb * fmt.limbs * S), dim3(512), 0, a.stream, c);
+    const uint64_t total = (uint64_t)nb * fmt.limbs * G::M;
+    hipLaunchKernelGGL((gen_split_combine_kernel<S>), dim3((uint32_t)std::min<uint64_t>((total + 255) / 256, 65535)),
+                       dim3(256), 0, a.stream, c);
+  }
+  CHIP_CHECK(hipFreeAsync(scratch, a.stream));
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("generic convert (split) launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
 }  // namespace gen
 
 uint64_t generic_scratch_bytes_per_sample(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
@@ -1973,6 +2550,8 @@ int pbs_generic_launch(const PbsArgs& a) {
   const uint32_t K1 = a.k + 1, M = a.N / 2, L = fmt.limbs, b = fmt.bits;
   const uint32_t T = (a.base_log + b - 1) / b;
   const Tables tb = tables_for(a.N);
+  if (a.N == 32768) return pbs_split_launch<2>(a, fmt, tb, T);
+  if (a.N == 65536) return pbs_split_launch<4>(a, fmt, tb, T);
   {
     const FusedArgs f{a.out, a.out_idx, a.in, a.in_idx, a.luts, a.lut_idx, reinterpret_cast<const cplx*>(a.fbsk),
                       tb.Tau, a.resid, a.num_samples, a.n, a.base_log, b};
@@ -2103,6 +2682,8 @@ int convert_bsk_generic_launch(const ConvertArgs& a) {
   const Tables tb = tables_for(a.N);
   const uint64_t blocks = (uint64_t)a.n * a.level * (a.k + 1) * (a.k + 1);
   if (blocks == 0) return 0;
+  if (a.N == 32768) return convert_split_launch<2>(a, fmt, tb);
+  if (a.N == 65536) return convert_split_launch<4>(a, fmt, tb);
   cplx* G = reinterpret_cast<cplx*>(a.dest);
 #define GEN_CONV(MM)                                                                                        \
   hipLaunchKernelGGL(gen_convert_kernel<MM>, dim3((uint32_t)blocks), dim3(Geo<MM>::THREADS), 0, a.stream, G, \

@@ -17,10 +17,10 @@
 
 int main(void) {
   CHECK(concrete_hip_abi_version() == 3);
-  /* cfg2 and cfg4 (BASELINE.json) are supported, N = 32768 is not */
+  /* cfg2 and cfg4 (BASELINE.json) are supported, N = 2^17 is not (up to 2^16 since round 4) */
   CHECK(concrete_hip_pbs_supported(1, 1024, 3, 7) == 1);
   CHECK(concrete_hip_pbs_supported(1, 2048, 1, 23) == 1);
-  CHECK(concrete_hip_pbs_supported(1, 32768, 1, 7) == 0);
+  CHECK(concrete_hip_pbs_supported(1, 131072, 1, 7) == 0);
   uint32_t limbs = 0, bits = 0;
   CHECK(concrete_hip_bsk_format(1, 1024, 3, &limbs, &bits) == 1 && limbs == 3);
   /* n (k+1)^2 l x 3 limbs x N/2 complex f64 */
@@ -29,7 +29,7 @@ int main(void) {
    * (-2, with a message): the dummy host pointers below are never dereferenced */
   static uint64_t dummy[4];
   CHECK(concrete_hip_pbs(NULL, 0, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 630, 1, 1024, 7, 3, 4, NULL) == -1);
-  CHECK(concrete_hip_pbs(NULL, 0, dummy, NULL, dummy, NULL, dummy, NULL, dummy, 630, 1, 32768, 7, 3, 4, NULL) == -2);
+  CHECK(concrete_hip_pbs(NULL, 0, dummy, NULL, dummy, NULL, dummy, NULL, dummy, 630, 1, 131072, 7, 3, 4, NULL) == -2);
   CHECK(strstr(concrete_hip_last_error(), "unsupported") != NULL);
   /* an empty batch is a no-op */
   CHECK(concrete_hip_pbs(NULL, 0, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 630, 1, 1024, 7, 3, 0, NULL) == 0);

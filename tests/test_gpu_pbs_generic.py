@@ -47,6 +47,10 @@ CASES = [
     ("k1_N4096_l3_wide_state", 1, 4096, 4, 3, 12, 3),
     ("k1_N8192_l2_wide_state", 1, 8192, 3, 2, 17, 4),
     ("k1_N16384_l3_wide_state", 1, 16384, 2, 3, 11, 3),
+    # N = 2^15 / 2^16 (the 9- and 10-bit rows, v0_last_128:243 / :264): a polynomial spread over
+    # S = 2 / 4 workgroups (gen_split_*_kernel), the key converted the same way
+    ("9bit_k1_N32768", 1, 32768, 2, 2, 15, 9),
+    ("10bit_k1_N65536", 1, 65536, 2, 2, 14, 10),
 ]
 
 
@@ -206,7 +210,7 @@ def test_generic_chunked_two_streams(B, oracle, torch_cuda, ci, streams, monkeyp
 
 def test_generic_outside_exact_range_refused(B):
     """Sets whose certified bound would exceed the gate are refused, not rounded wrongly."""
-    assert not B.pbs_supported(B.PbsParams(n=8, k=1, N=32768, level=2, base_log=15))
+    assert not B.pbs_supported(B.PbsParams(n=8, k=1, N=131072, level=2, base_log=15))
     assert not B.pbs_supported(B.PbsParams(n=8, k=1, N=4096, level=1, base_log=40))
 
 
@@ -343,6 +347,8 @@ LN2_CASES = [
     ("7bit_ln2_20", 1, 8192, 3, 42, 1, 7, 898, 18, 1),
     ("8bit_ln2_17", 1, 16384, 2, 14, 3, 8, 1007, 11, 2),
     ("8bit_ln2_18", 1, 16384, 2, 41, 1, 8, 985, 21, 1),
+    ("9bit_ln2_16", 1, 32768, 1, 41, 1, 9, 1059, 23, 1),
+    ("10bit_ln2_13", 1, 65536, 1, 20, 2, 10, 1095, 12, 2),
 ]
 
 

@@ -36,7 +36,7 @@ def test_abi_version_and_queries():
     assert L.concrete_hip_pbs_supported(1, 1024, 1, 23) == 1
     assert L.concrete_hip_pbs_supported(1, 1024, 2, 33) == 0  # l * logB > 64
     assert L.concrete_hip_pbs_supported(2, 1024, 3, 7) == 1  # k = 2: the general path
-    assert L.concrete_hip_pbs_supported(1, 32768, 1, 7) == 0
+    assert L.concrete_hip_pbs_supported(1, 131072, 1, 7) == 0  # N up to 2^16
     assert L.concrete_hip_bsk_limbs(1024, 3, 7) == 3
     p = B.CFG2
     # n * l * (k+1)^2 * LIMBS * N/2 complex f64
@@ -47,7 +47,7 @@ def test_abi_version_and_queries():
 def test_status_codes_without_device():
     L = _native.lib()
     # unsupported parameters are rejected before any device call
-    rc = L.concrete_hip_pbs(None, 0, 1, None, 1, None, 1, None, 1, 630, 1, 32768, 7, 3, 4, None)
+    rc = L.concrete_hip_pbs(None, 0, 1, None, 1, None, 1, None, 1, 630, 1, 131072, 7, 3, 4, None)
     assert rc == -2 and b"unsupported" in L.concrete_hip_last_error()
     rc = L.concrete_hip_pbs(None, 0, None, None, None, None, None, None, None, 630, 1, 1024, 7, 3, 4, None)
     assert rc == -1
@@ -106,7 +106,8 @@ def test_key_formats_and_exact_range():
     assert L.concrete_hip_pbs_supported(1, 2048, 1, 25) == 1  # past the cfg4 kernel: the general path
     # the general-format key of the hand-tuned shapes (wide digits): its own limbs
     assert L.concrete_hip_generic_bsk_size_bytes(10, 1, 1, 2048) > 0
-    assert L.concrete_hip_generic_bsk_size_bytes(10, 1, 1, 32768) == 0
+    assert L.concrete_hip_generic_bsk_size_bytes(10, 1, 1, 32768) > 0  # N = 2^15: the split path (round 4)
+    assert L.concrete_hip_generic_bsk_size_bytes(10, 1, 1, 131072) == 0
     for k, N, l, logB in [(5, 256, 1, 15), (6, 256, 1, 18), (3, 512, 1, 18), (2, 1024, 1, 23), (1, 4096, 1, 22),
                           (1, 8192, 1, 22), (1, 16384, 2, 15), (1, 2048, 2, 10)]:
         kind, limbs, bits = fmt(k, N, l)
@@ -114,8 +115,10 @@ def test_key_formats_and_exact_range():
         assert L.concrete_hip_pbs_supported(k, N, l, logB) == 1, (k, N, l, logB)
         assert 0 < L.concrete_hip_generic_error_bound(k, N, l, logB, 0.0) < 0.25
         assert L.concrete_hip_fourier_bsk_size_bytes(10, k, l, N) == 10 * l * (k + 1) ** 2 * limbs * (N // 2) * 16
-    assert fmt(1, 32768, 2)[0] == 0
-    assert L.concrete_hip_pbs_supported(1, 32768, 2, 15) == 0
+    assert fmt(1, 32768, 2)[0] == 3 and fmt(1, 65536, 2)[0] == 3
+    assert L.concrete_hip_pbs_supported(1, 32768, 2, 15) == 1  # v0_last_128 9-bit row
+    assert L.concrete_hip_pbs_supported(1, 65536, 2, 14) == 1  # 10-bit row
+    assert fmt(1, 131072, 2)[0] == 0
     assert L.concrete_hip_pbs_supported(1, 4096, 1, 40) == 0
 
 
@@ -135,7 +138,7 @@ def test_optimizer_table_coverage():
     """Every row of the optimizer's reference table (tests/golden/v0_last_128_rows.json, from
     v0-parameters/ref/v0_last_128 by tests/golden/make_v0_rows.py) from 1 to 8 bits, at every log
     norm2, has a PBS (k, N, br_l, br_b) and a keyswitch (ks_l, ks_b, kN -> n) the backend runs
-    exactly; the 9- and 10-bit rows (N = 2^15, 2^16) are refused, as DESIGN.md states."""
+    exactly, and so does every 9- and 10-bit row (N = 2^15, 2^16: the split path, round 4)."""
     import json
 
     L = _native.lib()
@@ -147,5 +150,5 @@ def test_optimizer_table_coverage():
     assert len(small) == 204
     assert [r for r in small if not runs(r)] == []
     big = [r for r in rows if r["bits"] > 8]
-    assert all(r["N"] >= 32768 for r in big)
-    assert [r for r in big if L.concrete_hip_keyswitch_supported(r["ks_l"], r["ks_b"], r["k"] * r["N"], r["n"]) != 1] == []
+    assert len(big) == 31 and all(r["N"] >= 32768 for r in big)
+    assert [r for r in big if not runs(r)] == []

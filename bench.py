@@ -106,7 +106,7 @@ def host_cpus():
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=("cfg2", "cfg4") + tuple(f"opt{b}" for b in range(1, 9)), default="cfg2",
+    ap.add_argument("--config", choices=("cfg2", "cfg4") + tuple(f"opt{b}" for b in range(1, 11)), default="cfg2",
                     help="cfg2: N=1024 n=630 l=3 logB=7 (the metric's config); cfg4: N=2048 n=742 l=1 logB=23; "
                          "optB: the optimizer's B-bit row of v0_last_128 (backend.OPTIMIZER_SETS)")
     ap.add_argument("--steps", type=int, default=5)

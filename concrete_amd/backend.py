@@ -75,6 +75,8 @@ OPTIMIZER_SETS = {
     6: PbsParams(n=880, k=1, N=4096, level=1, base_log=22, ks_level=4, ks_base_log=4),
     7: PbsParams(n=915, k=1, N=8192, level=1, base_log=22, ks_level=6, ks_base_log=3),
     8: PbsParams(n=1006, k=1, N=16384, level=2, base_log=15, ks_level=5, ks_base_log=4),
+    9: PbsParams(n=1039, k=1, N=32768, level=2, base_log=15, ks_level=7, ks_base_log=3),
+    10: PbsParams(n=1136, k=1, N=65536, level=2, base_log=14, ks_level=6, ks_base_log=4),
 }
 
 

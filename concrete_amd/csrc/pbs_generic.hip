@@ -1474,6 +1474,9 @@ struct Fused {
   static_assert(NW * RS * 16 >= 2 * N * 8, "the accumulator copy fits the rows");
 };
 
+#ifndef FUSED_PF
+#define FUSED_PF 1
+#endif
 template <int R, int LV, int T, int L, bool W32>
 __global__ void __launch_bounds__(512) gen_fused_kernel(FusedArgs a) {
   using F = Fused<R, LV, T, L>;
@@ -1576,6 +1579,19 @@ __global__ void __launch_bounds__(512) gen_fused_kernel(FusedArgs a) {
 
     // ---- products and inverse transforms, slot by slot
     const cplx* Gi = a.G + (uint64_t)i * (2 * L * 2 * LV) * M + pos;
+    // FUSED_PF: the first output polynomial's t = 0 key values of slot m + 1 (lim = m + 1, q = 0)
+    // are loaded while slot m's inverse transforms run, so their L2 latency hides behind them
+    cplx kp[FUSED_PF ? 2 : 1][R];
+    auto load_kp = [&](int lim) {
+      if constexpr (FUSED_PF) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+          for (int k1 = 0; k1 < R; ++k1) kp[r][k1] = Gi[(uint64_t)((lim * 2 + r) * LV) * M + k1 * 512];
+        __builtin_amdgcn_sched_barrier(0);  // issued here, not sunk to their use
+      }
+    };
+    load_kp(0);
 #pragma unroll 1
     for (int m = 0; m < L; ++m) {
 #pragma unroll
@@ -1592,9 +1608,10 @@ __global__ void __launch_bounds__(512) gen_fused_kernel(FusedArgs a) {
 #pragma unroll
             for (int q = 0; q < LV; ++q) {
               const cplx* g = Gi + (uint64_t)(((cc * L + lim) * 2 + r) * LV + q) * M;
+              const bool pre = FUSED_PF && cc == 0 && t == 0 && q == 0;
 #pragma unroll
               for (int k1 = 0; k1 < R; ++k1) {
-                const cplx gv = g[k1 * 512], xv = X[(r * LV + q) * T + t][k1];
+                const cplx gv = pre ? kp[FUSED_PF ? r : 0][k1] : g[k1 * 512], xv = X[(r * LV + q) * T + t][k1];
                 y[k1].re = __builtin_fma(xv.re, gv.re, __builtin_fma(-xv.im, gv.im, y[k1].re));
                 y[k1].im = __builtin_fma(xv.re, gv.im, __builtin_fma(xv.im, gv.re, y[k1].im));
               }
@@ -1604,6 +1621,7 @@ __global__ void __launch_bounds__(512) gen_fused_kernel(FusedArgs a) {
 #pragma unroll
         for (int jj = 0; jj < R; ++jj) E[(cc * R + jj) * RS + pos] = y[jj];
       }
+      if (m + 1 < L) load_kp(m + 1);
       pair_barrier();
       cplx v[8];
 #pragma unroll

@@ -22,4 +22,8 @@ step generic_all 900 python -u -m pytest -v --timeout 300 --timeout-method threa
 step opt6_pf 300 python -u bench.py --config opt6 --steps 3 --warmup 1 --no-cpu-baseline --no-ks --no-e2e
 step opt6_nopf 300 env CONCRETE_HIP_LIB=$GRAFT_REPO_ROOT/variants/libconcrete_hip_nopf.so python -u bench.py --config opt6 --steps 3 --warmup 1 --no-cpu-baseline --no-ks --no-e2e
 step opt9 600 python -u bench.py --config opt9 --steps 1 --warmup 0 --batch 1024 --no-cpu-baseline --no-ks --no-e2e --verify 0
+# N = 8192 one-launch kernel (spilling; CONCRETE_HIP_GEN_FUSED8=1): parity, then opt7 A/B
+step fused8_test 600 env CONCRETE_HIP_GEN_FUSED8=1 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_pbs_generic.py -k "7bit_k1_N8192"
+step opt7_fused8 300 env CONCRETE_HIP_GEN_FUSED8=1 python -u bench.py --config opt7 --steps 2 --warmup 1 --no-cpu-baseline --no-ks --no-e2e
+step opt7_base 300 python -u bench.py --config opt7 --steps 2 --warmup 1 --no-cpu-baseline --no-ks --no-e2e
 echo "pass C done"

@@ -1450,7 +1450,6 @@ __global__ void __launch_bounds__(256) gen_split_combine_kernel(SplitConvArgs a)
 // fft512 tables and tau: 118 KB, one workgroup per CU.
 // ------------------------------------------------------------------------------------------
 struct FusedArgs {
-  uint64_t* acc;  // N = 8192: per-ciphertext accumulator rows [count][2][N] (gen_fused8_kernel)
   uint64_t* out;
   const uint64_t* out_idx;
   const uint64_t* in;
@@ -1664,215 +1663,6 @@ __global__ void __launch_bounds__(512) gen_fused_kernel(FusedArgs a) {
   }
 }
 
-
-// ------------------------------------------------------------------------------------------
-// N = 8192, k = 1 in one launch (round 4): as gen_fused_kernel, one ciphertext per workgroup and
-// the digit spectra in registers (X: 2 l T spectra x 8 frequencies per thread), but an M = 4096
-// polynomial has 8 rows, so the workgroup's 8 waves take one polynomial at a time (wave w = row
-// w), and the accumulator (128 KB) does not stay in registers next to X: each wave reads its row
-// from a per-ciphertext accumulator in HBM (L2 / MALL) before the rotation and before each output
-// polynomial's inverse, and writes it back after the inverse.  Per CMUX step that is 384 KB of
-// accumulator traffic per ciphertext against the two-launch path's ~3 MB of X / Y / accumulator.
-// X is 128 KB per ciphertext: the last spectrum lives in LDS (XL = 1), the others in registers, and
-// tau(j1, e 64 + lane) is the lane factor alpha = tau(j1, lane) times the slot factor
-// beta(j1, e) from LDS (as gen_big_step_kernel at R = 16: within 3u of tau).
-// LDS: 8 rows of 576 complex (one polynomial; also the rotation's copy), fft512 tables, beta
-// (8 x 8), one spectrum (8 x 512): 153 KB.
-// ------------------------------------------------------------------------------------------
-template <int LV, int T, int L, bool W32>
-__global__ void __launch_bounds__(512) gen_fused8_kernel(FusedArgs a) {
-  constexpr int R = 8, M = R * 512, N = 2 * M, RS = 576, NX = 2 * LV * T, LOGR = 3, LOG2_2N = 15;
-  constexpr int XL = 1, NXR = NX - XL;  // spectra in LDS / in registers
-  constexpr int ROWLEN = N / R;
-  using St = typename std::conditional<W32, uint32_t, uint64_t>::type;
-  using Dg = typename std::conditional<W32, int32_t, int64_t>::type;
-  static_assert(R * RS * 16 >= N * 8, "the rotation copy fits the rows");
-  __shared__ cplx lds[R * RS + FFT512_TABLE_ENTRIES + R * 8 + XL * M];
-  cplx* E = lds;
-  cplx* tab = lds + R * RS;
-  cplx* beta = tab + FFT512_TABLE_ENTRIES;
-  cplx* Xl = beta + R * 8;  // [XL][k1 512 + pos]
-  build_fft512_tables(tab, threadIdx.x, 512);
-  for (int x = threadIdx.x; x < R * 8; x += 512) beta[x] = a.Tau[R * 512 + x];
-  const Fft512Tables TB = fft512_tables_at(tab);
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int j1 = w;             // the wave's row of the polynomial in hand
-  const cplx alpha = a.Tau[j1 * 512 + lane];
-  auto tau = [&](int e) { return e == 0 ? alpha : cmul(alpha, beta[j1 * 8 + e]); };
-  const int pos = threadIdx.x;  // column position of this thread
-  cplx* row = E + w * RS;
-  const uint32_t ct = blockIdx.x;
-  const uint64_t in_row = a.in_idx ? a.in_idx[ct] : ct;
-  const uint64_t* lwe = a.in + in_row * (uint64_t)(a.n + 1);
-  uint64_t* accg = a.acc + (uint64_t)ct * 2 * N;  // [c][row order]
-  auto jcol = [&](int e) { return lane + 64 * (e & 7) + 512 * (e >> 3); };
-  {
-    // acc_c = LUT_c * X^{-ms(b)}, each wave its row of both polynomials
-    const uint32_t bt = modswitch(lwe[a.n], LOG2_2N);
-#pragma unroll 1
-    for (int c = 0; c < 2; ++c) {
-      const uint64_t* lut = a.luts + (a.lut_idx ? a.lut_idx[ct] : 0ull) * (uint64_t)(2 * N) + (uint64_t)c * N;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const uint32_t src = ((uint32_t)(j1 + R * jcol(e)) + bt) & (2 * N - 1);
-        const uint64_t v = lut[src & (N - 1)];
-        accg[(uint64_t)c * N + j1 * ROWLEN + jcol(e)] = src < (uint32_t)N ? v : 0ull - v;
-      }
-    }
-  }
-  const int logB = (int)a.base_log, sb = (int)a.bits;
-  const int nrep = 64 - LV * logB;
-  const bool split = T > 1;
-  const St half = split ? (St)1 << (sb - 1) : (St)0, bmask = split ? ((St)1 << sb) - (St)1 : ~(St)0;
-  double max_resid = 0.0;
-  __syncthreads();  // tables, beta, the initial accumulator rows (global stores, read back below)
-
-#pragma unroll 1
-  for (uint32_t i = 0; i < a.n; ++i) {
-    const uint32_t at = modswitch(lwe[i], LOG2_2N);
-    cplx X[NXR][R];
-    // ---- forward, one polynomial at a time
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      uint64_t A[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) A[e] = accg[(uint64_t)c * N + j1 * ROWLEN + jcol(e)];
-      uint64_t* accl = reinterpret_cast<uint64_t*>(E);
-#pragma unroll
-      for (int e = 0; e < 16; ++e) accl[j1 * ROWLEN + jcol(e)] = A[e];
-      pair_barrier();
-      St S[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const uint32_t src = ((uint32_t)(j1 + R * jcol(e)) - at) & (2 * N - 1);
-        const uint32_t idx = src & (N - 1);
-        const uint64_t rv = accl[(idx & (R - 1)) * ROWLEN + (idx >> LOGR)];
-        const uint64_t x = (src < (uint32_t)N ? rv : 0ull - rv) - A[e];
-        S[e] = (St)(nrep > 0 ? decomp_init(x, nrep) : x);
-      }
-      pair_barrier();  // the rows are free again
-#pragma unroll
-      for (int q = 0; q < LV; ++q) {
-        Dg D[16];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          if constexpr (W32) D[e] = decomp_next_t<uint32_t>(S[e], logB);
-          else D[e] = decomp_next64(S[e], logB);
-        }
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-          cplx v[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const Dg s0 = (Dg)(((St)D[e] + half) & bmask) - (Dg)half;
-            const Dg s1 = (Dg)(((St)D[e + 8] + half) & bmask) - (Dg)half;
-            D[e] = (D[e] - s0) >> sb;
-            D[e + 8] = (D[e + 8] - s1) >> sb;
-            v[e] = {(double)s0, (double)s1};
-          }
-          fft512_fwd(v, row, TB, lane);
-          if (j1 != 0)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = cmul(v[e], tau(e));
-#pragma unroll
-          for (int e = 0; e < 8; ++e) row[e * 64 + lane] = v[e];
-          pair_barrier();
-          cplx u[R];
-#pragma unroll
-          for (int jj = 0; jj < R; ++jj) u[jj] = E[jj * RS + pos];
-          dft_col<R, false>(u);
-          const int x = (c * LV + q) * T + t;
-#pragma unroll
-          for (int k1 = 0; k1 < R; ++k1) {
-            if (x < NXR) X[x < NXR ? x : 0][k1] = u[k1];
-            else Xl[(x - NXR) * M + k1 * 512 + pos] = u[k1];
-          }
-          pair_barrier();
-        }
-      }
-    }
-    // ---- products and inverse transforms, one output polynomial at a time
-    const cplx* Gi = a.G + (uint64_t)i * (2 * L * 2 * LV) * M + pos;
-#pragma unroll 1
-    for (int cc = 0; cc < 2; ++cc) {
-      uint64_t A[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) A[e] = accg[(uint64_t)cc * N + j1 * ROWLEN + jcol(e)];
-#pragma unroll 1
-      for (int m = 0; m < L; ++m) {
-        cplx y[R];
-#pragma unroll
-        for (int k1 = 0; k1 < R; ++k1) y[k1] = {0.0, 0.0};
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-          const int lim = m - t;
-          if (lim < 0) continue;
-#pragma unroll
-          for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int q = 0; q < LV; ++q) {
-              const cplx* g = Gi + (uint64_t)(((cc * L + lim) * 2 + r) * LV + q) * M;
-              const int x = (r * LV + q) * T + t;
-#pragma unroll
-              for (int k1 = 0; k1 < R; ++k1) {
-                const cplx gv = g[k1 * 512];
-                const cplx xv = x < NXR ? X[x < NXR ? x : 0][k1] : Xl[(x - NXR) * M + k1 * 512 + pos];
-                y[k1].re = __builtin_fma(xv.re, gv.re, __builtin_fma(-xv.im, gv.im, y[k1].re));
-                y[k1].im = __builtin_fma(xv.re, gv.im, __builtin_fma(xv.im, gv.re, y[k1].im));
-              }
-              // one term's key values in flight at a time (X already fills half the registers)
-              __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        dft_col<R, true>(y);
-#pragma unroll
-        for (int jj = 0; jj < R; ++jj) E[jj * RS + pos] = y[jj];
-        pair_barrier();
-        cplx v[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = row[e * 64 + lane];
-        wave_lds_fence();  // the row is read whole before the transform writes its scratch over it
-        if (j1 != 0)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = cmulc(v[e], tau(e));
-        cplx gi2[4];
-        inv_p2_stage_tw(gi2, TB, lane & 7);
-        fft512_inv_tw(v, row, TB, lane, gi2, 0);
-        const uint32_t sh = ((uint32_t)m * a.bits) & 63u;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const double tr = v[e].re + RND_MAGIC, ti = v[e].im + RND_MAGIC;
-          max_resid = fmax(max_resid, fmax(fabs(v[e].re - (tr - RND_MAGIC)), fabs(v[e].im - (ti - RND_MAGIC))));
-          A[e] += ((uint64_t)__double_as_longlong(tr) - RND_MAGIC_BITS) << sh;
-          A[e + 8] += ((uint64_t)__double_as_longlong(ti) - RND_MAGIC_BITS) << sh;
-        }
-        pair_barrier();
-      }
-      // the wave's own row: read back only by this wave (the rotation goes through LDS)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) accg[(uint64_t)cc * N + j1 * ROWLEN + jcol(e)] = A[e];
-    }
-  }
-
-  // sample extract (nth = 0): out[j] = -A_0[N - j] (j > 0), out[0] = A_0[0], out[N] = A_1[0]
-  const uint64_t orow = a.out_idx ? a.out_idx[ct] : ct;
-  uint64_t* o = a.out + orow * (uint64_t)(N + 1);
-#pragma unroll 1
-  for (int c = 0; c < 2; ++c)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const uint32_t j = (uint32_t)(j1 + R * jcol(e));
-      const uint64_t v = accg[(uint64_t)c * N + j1 * ROWLEN + jcol(e)];
-      if (c == 0)
-        o[(N - j) & (N - 1)] = j == 0 ? v : 0ull - v;
-      else if (j == 0)
-        o[N] = v;
-    }
-  if (a.resid) {
-    for (int off = 32; off > 0; off >>= 1) max_resid = fmax(max_resid, __shfl_xor(max_resid, off));
-    if (lane == 0) atomicMax(a.resid, (unsigned long long)__double_as_longlong(max_resid));
-  }
-}
 
 // Y[ct][c][m][f] = sum over (r, q, t) with 0 <= m - t < L of X[ct][r][q][t][f] * G_i[c][m-t][r][q][f]
 struct MacArgs {
@@ -2627,22 +2417,6 @@ static bool fused_dispatch(const FusedArgs& f, uint32_t k, uint32_t N, uint32_t 
   const char* fe = getenv("CONCRETE_HIP_GEN_FUSED");  // read per call (tests cover both paths)
   if ((fe && atoi(fe) == 0) || k != 1 || !four_step(N)) return false;
   const bool w32 = (uint64_t)level * f.base_log <= 31;
-  if (N == 8192) {
-    // (CONCRETE_HIP_GEN_FUSED8=1: under evaluation — X does not fit the registers next to the
-    // transforms, the kernel spills; off by default)
-    const char* f8 = getenv("CONCRETE_HIP_GEN_FUSED8");
-    if (!(f8 && atoi(f8) == 1) || !(level == 1 && T == 2 && L == 6)) return false;
-    // the accumulator rows of every ciphertext (2 N u64 each), stream-ordered scratch
-    FusedArgs g = f;
-    keep_pool_memory();
-    CHIP_CHECK(hipMallocAsync((void**)&g.acc, (uint64_t)f.count * 2 * N * 8, st));
-    if (w32)
-      hipLaunchKernelGGL((gen_fused8_kernel<1, 2, 6, true>), dim3(f.count), dim3(512), 0, st, g);
-    else
-      hipLaunchKernelGGL((gen_fused8_kernel<1, 2, 6, false>), dim3(f.count), dim3(512), 0, st, g);
-    CHIP_CHECK(hipFreeAsync(g.acc, st));
-    return true;
-  }
   if (N != 4096) return false;
 #define GEN_FUSED(LVv, Tv, Lv)                                                                               \
   if (level == LVv && T == Tv && L == Lv) {                                                                  \
@@ -2798,8 +2572,8 @@ int pbs_generic_launch(const PbsArgs& a) {
   if (a.N == 32768) return pbs_split_launch<2>(a, fmt, tb, T);
   if (a.N == 65536) return pbs_split_launch<4>(a, fmt, tb, T);
   {
-    const FusedArgs f{nullptr, a.out, a.out_idx, a.in, a.in_idx, a.luts, a.lut_idx,
-                      reinterpret_cast<const cplx*>(a.fbsk), tb.Tau, a.resid, a.num_samples, a.n, a.base_log, b};
+    const FusedArgs f{a.out, a.out_idx, a.in, a.in_idx, a.luts, a.lut_idx, reinterpret_cast<const cplx*>(a.fbsk),
+                      tb.Tau, a.resid, a.num_samples, a.n, a.base_log, b};
     if (fused_dispatch(f, a.k, a.N, a.level, T, L, a.stream)) {
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) {

@@ -213,6 +213,30 @@ __global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__
 }
 #endif
 
+// N = 1024, k = 2, l = 1 (pbs1024k2.hip).  Block = (i, limb, col, row), in the order of the output
+// layout [n][limb][col][row][512]: limb `limb` of key polynomial (row, col), folded, twisted and
+// transformed like the k = 1 key.
+__global__ void __launch_bounds__(256) convert_bsk1024k2_kernel(cplx* __restrict__ dest,
+                                                               const uint64_t* __restrict__ src,
+                                                               const ddc* __restrict__ zeta_t,
+                                                               const ddc* __restrict__ tw_t) {
+  constexpr int M = 512, LOGM = 9, N = 1024;
+  __shared__ ddc buf[M];
+  const uint64_t blk = blockIdx.x;
+  const uint32_t row = (uint32_t)(blk % 3), col = (uint32_t)((blk / 3) % 3);
+  const uint32_t limb = (uint32_t)((blk / 9) % K2_LIMBS);
+  const uint64_t i = blk / (9 * K2_LIMBS);
+  const uint64_t* g = src + ((i * 3 + row) * 3 + col) * N;  // [n][l = 1][row][col][N]
+  for (int j = threadIdx.x; j < M; j += blockDim.x) {
+    ddc z{dd_from(limb_value<K2_LIMBS>(g[j], limb)), dd_from(limb_value<K2_LIMBS>(g[j + M], limb))};
+    z = ddc_mul(z, zeta_t[j]);
+    const int r = (int)(__builtin_bitreverse32((uint32_t)j) >> (32 - LOGM));
+    buf[r] = z;
+  }
+  __syncthreads();
+  dd_fft_scatter<M>(buf, tw_t, [&](int e) { return dest + blk * M + e; });
+}
+
 template <int N, int K, int L, int LIMBS>
 static int launch_convert(const ConvertArgs& a, const ddc* zeta, const ddc* tw) {
   const uint64_t blocks = (uint64_t)a.n * L * (K + 1) * (K + 1) * LIMBS;
@@ -267,7 +291,8 @@ int convert_bsk_launch(const ConvertArgs& a) {
   if (key_format(a.k, a.N, a.level).kind == KeyKind::GENERIC) return convert_bsk_generic_launch(a);
   const bool n1024 = a.N == 1024 && a.k == 1 && a.limbs == 3 && a.level >= 1 && a.level <= 3;
   const bool n2048 = a.N == 2048 && a.k == 1 && a.limbs == (uint32_t)PBS2_LIMBS && a.level == 1;
-  if (!n1024 && !n2048) {
+  const bool k2 = a.N == 1024 && a.k == 2 && a.limbs == (uint32_t)K2_LIMBS && a.level == 1;
+  if (!n1024 && !n2048 && !k2) {
     set_error("unsupported BSK conversion parameters: N=%u k=%u level=%u limbs=%u", a.N, a.k, a.level, a.limbs);
     return -2;
   }
@@ -289,6 +314,15 @@ int convert_bsk_launch(const ConvertArgs& a) {
     const uint64_t blocks = (uint64_t)a.n * PBS2_LIMBS * 4 * (P2_PM ? 1 : 2);
     hipLaunchKernelGGL((convert_bsk2048_kernel<PBS2_LIMBS>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
                        reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, ds);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      set_error("convert launch failed: %s", hipGetErrorString(e));
+      rc = -1;
+    }
+  } else if (k2) {
+    const uint64_t blocks = (uint64_t)a.n * K2_LIMBS * 9;
+    hipLaunchKernelGGL(convert_bsk1024k2_kernel, dim3((uint32_t)blocks), dim3(256), 0, a.stream,
+                       reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       set_error("convert launch failed: %s", hipGetErrorString(e));

@@ -42,11 +42,27 @@ constexpr size_t pbs2048_lds_bytes() {
          4 * PBS2_CTS * 4;  // + per-wave sync counters
 }
 
+// N = 1024, k = 2, l = 1 kernel geometry (pbs1024k2.hip): three waves per ciphertext (one per GLWE
+// polynomial), K2_CTS ciphertexts per workgroup, a ring of 24 KB key groups (one limb and one output
+// column: the three row spectra).  Key: 4 balanced 16-bit limbs, digits split as in pbs2048.hip.
+constexpr int K2_CTS = 2;
+constexpr int K2_RING_SLOTS = 3;
+constexpr int K2_LIMBS = 4;
+constexpr int K2_SUBS = 2;
+constexpr int K2_SUB_BITS = 16;
+constexpr int K2_MAX_LOGB = 24;  // certified bound < 1/2 (oracle/pyoracle.py:gpu1024k2_error_bound)
+constexpr size_t pbs1024k2_lds_bytes() {
+  return PBS1024_TABLE_BYTES + 3 * K2_CTS * PBS1024_XCH_SLOTS * 16 + (size_t)K2_RING_SLOTS * 3 * 512 * 16 +
+         3 * K2_CTS * 4;  // + per-wave sync counters
+}
+
 // Device key formats.  N1024 / N2048: the hand-tuned kernels' layouts (pbs.hip, pbs2048.hip);
 // GENERIC: pbs_generic.hip, L balanced limbs of `bits` bits for any k <= GEN_MAX_K and
 // N = 256 .. 16384.  The format depends on (k, N, l) only: the runtime's key conversion call
 // carries no base_log (context.h:106-109).
-enum class KeyKind { NONE, N1024, N2048, GENERIC };
+// K2N1024: pbs1024k2.hip (k = 2, N = 1024, l = 1).  The values are the ABI's format codes
+// (concrete_hip_bsk_format).
+enum class KeyKind { NONE, N1024, N2048, GENERIC, K2N1024 };
 struct KeyFormat {
   KeyKind kind;
   uint32_t limbs, bits;
@@ -81,6 +97,7 @@ inline bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_
     // one level whose digit splits into d_lo + 2^16 d_hi (pbs2048.hip)
     case KeyKind::N2048: return base_log >= 1 && base_log <= PBS2_MAX_LOGB;
     case KeyKind::GENERIC: return generic_pbs_ok(k, N, level, base_log);
+    case KeyKind::K2N1024: return base_log >= 1 && base_log <= K2_MAX_LOGB;
     default: return false;
   }
 }
@@ -89,11 +106,13 @@ inline bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_
 //   N1024:   [n][col][limb][row*l + q][512] complex f64
 //   N2048:   [n][limb][col][row][parity][512] complex f64 (pbs2048.hip)
 //   GENERIC: [n][col][limb][row][q][N/2] complex f64 (pbs_generic.hip)
+//   K2N1024: [n][limb][col][row][512] complex f64 (pbs1024k2.hip)
 inline uint64_t fourier_bsk_bytes(uint32_t n, uint32_t k, uint32_t level, uint32_t N) {
   const KeyFormat f = key_format(k, N, level);
   switch (f.kind) {
     case KeyKind::N2048: return (uint64_t)n * f.limbs * (k + 1) * (k + 1) * 2 * 512 * 16ull * level;
     case KeyKind::N1024:
+    case KeyKind::K2N1024:
     case KeyKind::GENERIC: return (uint64_t)n * level * (k + 1) * (k + 1) * f.limbs * (N / 2) * 16ull;
     default: return 0;
   }
@@ -116,6 +135,7 @@ struct PbsArgs {
 int pbs_launch(const PbsArgs& a);
 int pbs2048_launch(const PbsArgs& a);         // pbs2048.hip
 int pbs_generic_launch(const PbsArgs& a);     // pbs_generic.hip
+int pbs1024k2_launch(const PbsArgs& a);       // pbs1024k2.hip
 
 struct ConvertArgs {
   hipStream_t stream;

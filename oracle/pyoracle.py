@@ -131,6 +131,30 @@ def gpu2048_error_bound(fbsk_gpu: np.ndarray, logB: int = 23) -> float:
     return float(main + 4.0 * u * max_out)
 
 
+def gpu1024k2_error_bound(fbsk_gpu: np.ndarray, logB: int = 23) -> float:
+    """Certified bound on |x - round(x)| for the GPU's k = 2, N = 1024, l = 1 scheme
+    (concrete_amd/csrc/pbs1024k2.hip): the N = 1024 products of pbs.hip
+    (512-point folded, twisted transforms, log M = 9, correctly rounded tables: mu = u) on the
+    digit split of pbs2048.hip, d = d_lo + 2^16 d_hi (|d_lo| <= 2^15, |d_hi| <= 2^(logB-17) + 1)
+    against 16-bit key limbs: output slot m is the sum of d_lo g_m + d_hi g_{m-1} over the three
+    rows, 6 N = 1024 products.  fbsk_gpu: the device key (f64 view; spectra scaled by 1/512)."""
+    u = 2.0 ** -53
+    logM = 9.0
+    mu = u
+    eta = mu + 4.0 * u / (1.0 - 4.0 * u) * (np.sqrt(2.0) + mu)
+    gamma = logM * eta / (1.0 - logM * eta)
+    f = np.asarray(fbsk_gpu, dtype=np.float64).reshape(-1, 2)
+    maxG = float(np.max(np.hypot(f[:, 0], f[:, 1]))) * 512.0
+    dlo = 2.0 ** 15
+    dhi = 2.0 ** max(logB - 17, 0) + 1.0
+    dsum = 3.0 * (dlo + dhi)                    # sum over the 6 products of max |digit|
+    # forward transform, key rounding, pointwise product and inverse of each product, plus the
+    # accumulation additions: (4 gamma + 5 u), as for the N = 2048 products
+    main = np.sqrt(1024.0) * dsum * maxG * (4.0 * gamma + 5.0 * u) * 1.0001
+    max_out = 1024.0 * dsum * 2.0 ** 15
+    return float(main + 4.0 * u * max_out)
+
+
 def generic_error_bound(k: int, N: int, l: int, logB: int, bits: int, fbsk_gpu=None) -> float:
     """Certified bound on |x - round(x)| for the GPU's general path (concrete_amd/csrc/
     pbs_generic.hip:generic_error_bound): R = (k+1) l T products per slot of a

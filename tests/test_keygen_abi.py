@@ -108,7 +108,13 @@ def test_key_formats_and_exact_range():
     assert L.concrete_hip_generic_bsk_size_bytes(10, 1, 1, 2048) > 0
     assert L.concrete_hip_generic_bsk_size_bytes(10, 1, 1, 32768) > 0  # N = 2^15: the split path (round 4)
     assert L.concrete_hip_generic_bsk_size_bytes(10, 1, 1, 131072) == 0
-    for k, N, l, logB in [(5, 256, 1, 15), (6, 256, 1, 18), (3, 512, 1, 18), (2, 1024, 1, 23), (1, 4096, 1, 22),
+    # the optimizer's 4-bit rows (k = 2, N = 1024, l = 1): their own kernel (pbs1024k2.hip, round 4),
+    # 4 limbs of 16 bits, the digit split on the limb grid as at N = 2048
+    assert fmt(2, 1024, 1) == (4, 4, 16)
+    assert L.concrete_hip_fourier_bsk_size_bytes(801, 2, 1, 1024) == 801 * 4 * 9 * 512 * 16
+    assert L.concrete_hip_pbs_supported(2, 1024, 1, 24) == 1
+    assert L.concrete_hip_generic_error_bound(2, 1024, 1, 23, 0.0) == -1.0
+    for k, N, l, logB in [(5, 256, 1, 15), (6, 256, 1, 18), (3, 512, 1, 18), (2, 1024, 2, 15), (1, 4096, 1, 22),
                           (1, 8192, 1, 22), (1, 16384, 2, 15), (1, 2048, 2, 10)]:
         kind, limbs, bits = fmt(k, N, l)
         assert kind == 3 and limbs * bits >= 64, (k, N, l)

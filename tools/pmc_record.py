@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from bench import kernel_source_hash  # noqa: E402
 
-KERNEL = {"cfg2": "pbs1024", "cfg4": "pbs2048"}
+KERNEL = {"cfg2": "pbs1024_pair", "cfg4": "pbs2048", "opt4": "pbs1024k2"}
 # the general path (optB configs) runs several launches per PBS call (pbs_generic.hip): the record
 # sums every gen_* dispatch of the process's single call (tools/pmc.sh: --steps 1 --warmup 0 --no-e2e),
 # except the once-per-key conversion

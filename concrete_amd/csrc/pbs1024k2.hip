@@ -39,13 +39,47 @@ constexpr uint64_t K2_MAGIC_ALL =
     RND_MAGIC_BITS + (RND_MAGIC_BITS << 16) + (RND_MAGIC_BITS << 32) + (RND_MAGIC_BITS << 48);
 
 // first frequency slot of wave v's share (v = 0, 1, 2; SB(3) = 8)
-__device__ __forceinline__ int k2_slot_base(int v) { return v == 0 ? 0 : (v == 1 ? 3 : 5); }
+#ifndef K2_SB1
+#define K2_SB1 3
+#endif
+#ifndef K2_SB2
+#define K2_SB2 5
+#endif
+#ifndef K2_ASM_DMA
+#define K2_ASM_DMA 0
+#endif
+// Diagnostic builds only (timing; wrong results): K2D_NOBAR (no key-window barriers), K2D_NOMAC
+// (no key MAC FMAs), K2D_NOINV / K2D_NOFWD (no inverse / forward transforms), K2D_NOTRI (no
+// three-wave syncs).
+#ifndef K2D_NOBAR
+#define K2D_NOBAR 0
+#endif
+#ifndef K2D_NOMAC
+#define K2D_NOMAC 0
+#endif
+#ifndef K2D_NOINV
+#define K2D_NOINV 0
+#endif
+#ifndef K2D_NOFWD
+#define K2D_NOFWD 0
+#endif
+#ifndef K2D_NOTRI
+#define K2D_NOTRI 0
+#endif
+#ifndef K2D_NOROT
+#define K2D_NOROT 0
+#endif
+#ifndef K2D_NOXRD
+#define K2D_NOXRD 0
+#endif
+__device__ __forceinline__ int k2_slot_base(int v) { return v == 0 ? 0 : (v == 1 ? K2_SB1 : K2_SB2); }
 
 // Synchronisation of the three waves of one ciphertext (never the other ciphertext of the
 // workgroup): each wave publishes how many sync points it has passed and waits until its two
 // partners have reached the same count.  LDS traffic is drained, the key DMA is not.
 __device__ __forceinline__ void tri_sync(uint32_t* flags, int ctl, int v, uint32_t& cnt, const SyncGuard& guard) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (K2D_NOTRI) return;
   ++cnt;
   __hip_atomic_store(&flags[ctl * 3 + v], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   spin_until_ge(&flags[ctl * 3 + (v == 2 ? 0 : v + 1)], cnt, guard);
@@ -60,6 +94,7 @@ __device__ __forceinline__ void tri_signal(uint32_t* flags, int ctl, int v, uint
   __hip_atomic_store(&flags[ctl * 3 + v], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void tri_wait(uint32_t* flags, int ctl, int v, uint32_t cnt, const SyncGuard& guard) {
+  if (K2D_NOTRI) return;
   spin_until_ge(&flags[ctl * 3 + (v == 2 ? 0 : v + 1)], cnt, guard);
   spin_until_ge(&flags[ctl * 3 + (v == 0 ? 2 : v - 1)], cnt, guard);
   asm volatile("" ::: "memory");
@@ -97,7 +132,12 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
   const int ctl = w / 3;  // ciphertext within the workgroup
   const int v = w - 3 * ctl;  // own polynomial
   const int sb = k2_slot_base(v);
-  const int ns = v == 1 ? 2 : 3;  // slots of my share
+  // slots of my share; every share has at least 2 (K2_SB1, K2_SB2), so only slot 2 is conditional
+  const int ns = (v == 2 ? 8 : k2_slot_base(v + 1)) - sb;
+  static_assert(K2_SB1 >= 2 && K2_SB2 - K2_SB1 >= 2 && 8 - K2_SB2 >= 2 && K2_SB1 <= 3 && K2_SB2 - K2_SB1 <= 3 &&
+                    8 - K2_SB2 <= 3,
+                "slot shares of 2 or 3");
+  auto has = [&](int jj) __attribute__((always_inline)) { return jj < 2 || ns > 2; };
   const uint32_t s = blockIdx.x * K2_CTS + ctl;
   const bool active = s < num_samples;
   cplx* xch = xch_all + w * XS;
@@ -113,9 +153,19 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
     const char* src = reinterpret_cast<const char*>(key_step + r * GROUP);
     cplx* dst = ring_w + (r % RS) * GROUP;
 #pragma unroll
-    for (int j = 0; j < GLDS; ++j)
+    for (int j = 0; j < GLDS; ++j) {
+#if K2_ASM_DMA
+      const cplx* gp = reinterpret_cast<const cplx*>(src + j * 1024 + lane_b);
+      const uint32_t m0 = (uint32_t)(uintptr_t)(lds_ptr_t)(dst + j * 64);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(gp), "s"(m0) : "m0", "memory");
+#pragma clang diagnostic pop
+#else
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const cplx*>(src + j * 1024 + lane_b),
                                        (lds_ptr_t)(dst + j * 64), 16, 0, 0);
+#endif
+    }
   };
   if (n > 0) {
 #pragma unroll
@@ -165,7 +215,7 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
       wave_lds_fence();
       uint64_t rv[16];
 #pragma unroll
-      for (int m = 0; m < 16; ++m) rv[m] = xch64[(uint32_t)(lane + 64 * m - (int)at) & (N - 1)];
+      for (int m = 0; m < 16; ++m) rv[m] = K2D_NOROT ? A[m] ^ at : xch64[(uint32_t)(lane + 64 * m - (int)at) & (N - 1)];
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
@@ -198,9 +248,10 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
         fwd_p3_tw(tw3, T, lane);
         // the sub-0 exchange's "everyone has read my spectrum" wait, right before this
         // transform's first LDS write (the partners signalled right after their reads)
-        fft512_fwd_tw(vv8, xch, lane, tw2, tw3, 0, [&]() __attribute__((always_inline)) {
-          if (sub > 0) tri_wait(tflags, ctl, v, tcnt, guard);
-        });
+        if (!K2D_NOFWD)
+          fft512_fwd_tw(vv8, xch, lane, tw2, tw3, 0, [&]() __attribute__((always_inline)) {
+            if (sub > 0) tri_wait(tflags, ctl, v, tcnt, guard);
+          });
 #pragma unroll
         for (int k2 = 0; k2 < 8; ++k2) xch[k2 * 64 + lane] = vv8[k2];
       }
@@ -212,7 +263,7 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
         for (int row = 0; row < K1; ++row)
 #pragma unroll
           for (int jj = 0; jj < MS; ++jj)
-            if (jj < ns) X[row][sub][jj] = ctx[row * XS + (sb + jj) * 64 + lane];
+            if (has(jj)) X[row][sub][jj] = ctx[(K2D_NOXRD ? v : row) * XS + (sb + jj) * 64 + lane];
 #pragma unroll
         for (int row = 0; row < K1; ++row)
 #pragma unroll
@@ -244,7 +295,7 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
         // group r landed for this wave's pieces (the next DIST - 1 may stay in flight) ...
         if (r + DIST - 1 < NGRP || !last_step) wait_vmcnt<GLDS * (DIST - 1)>();
         else wait_vmcnt<0>();
-        pair_barrier();  // ... for every wave; everyone is done with group r - 1
+        if (!K2D_NOBAR) pair_barrier();  // ... for every wave; everyone is done with group r - 1
         // refill the slot of group r - 1 with group r + DIST (RS = DIST + 1)
         if (r + DIST < NGRP) issue_group(key_step, r + DIST);
         else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
@@ -254,7 +305,7 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
             for (int row = 0; row < K1; ++row)
 #pragma unroll
               for (int jj = 0; jj < MS; ++jj)
-                if (jj < ns) X[row][K2_SUBS - 1][jj] = ctx[row * XS + (sb + jj) * 64 + lane];
+                if (has(jj)) X[row][K2_SUBS - 1][jj] = ctx[(K2D_NOXRD ? v : row) * XS + (sb + jj) * 64 + lane];
           }
         }
         cplx Ya[MS];
@@ -266,10 +317,10 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
           cplx g[MS];
 #pragma unroll
           for (int jj = 0; jj < MS; ++jj)
-            if (jj < ns) g[jj] = G[row * 512 + jj * 64];
+            if (has(jj)) g[jj] = G[row * 512 + jj * 64];
 #pragma unroll
-          for (int jj = 0; jj < MS; ++jj) {
-            if (jj < ns) {
+          for (int jj = 0; jj < (K2D_NOMAC ? 0 : MS); ++jj) {
+            if (has(jj)) {
               const cplx x0 = X[row][0][jj];
               Ya[jj].re = __builtin_fma(x0.re, g[jj].re, __builtin_fma(-x0.im, g[jj].im, Ya[jj].re));
               Ya[jj].im = __builtin_fma(x0.re, g[jj].im, __builtin_fma(x0.im, g[jj].re, Ya[jj].im));
@@ -286,7 +337,7 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
         // each wave only ever touches its own slots of a partner's scratch.
 #pragma unroll
         for (int jj = 0; jj < MS; ++jj)
-          if (jj < ns) ctx[cc * XS + (sb + jj) * 64 + lane] = Ya[jj];
+          if (has(jj)) ctx[cc * XS + (sb + jj) * 64 + lane] = Ya[jj];
 #pragma unroll
         for (int jj = 0; jj < MS; ++jj) {
           pin(Ya[jj]);
@@ -306,7 +357,7 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
       {
         cplx gi2[4];
         inv_p2_stage_tw(gi2, T, lane & 7);
-        fft512_inv_tw(V, xch, T, lane, gi2, 0);
+        if (!K2D_NOINV) fft512_inv_tw(V, xch, T, lane, gi2, 0);
       }
 #pragma unroll
       for (int m = 0; m < 8; ++m) {

@@ -576,6 +576,16 @@ static int launch_pair(const PbsArgs& a) {
   const uint32_t cus = device_cus();
   const int P = forced == 1 || forced == 2 || forced == 4 ? forced
                 : a.num_samples <= cus ? 1 : a.num_samples <= 2 * cus ? 2 : 4;
+  // <= 1 ciphertext per CU at l = 3: four waves per ciphertext (pbs1024_quad.hip), +7 % at B = 256
+  // (at 2 per CU, B = 512, it measured 0.9x the pair kernel: DESIGN.md §4.1).  CONCRETE_HIP_PBS_QUAD=0
+  // keeps the pair kernel, =1 / =2 forces it with that many ciphertexts per workgroup (read per
+  // call: tests, A/B).
+  if (L == 3 && P <= 2 && !getenv("CONCRETE_HIP_PBS_STAMPS")) {
+    const char* qe = getenv("CONCRETE_HIP_PBS_QUAD");
+    const int q = qe ? atoi(qe) : -1;
+    if (q == 1 || q == 2) return pbs1024_quad_launch(a, q);
+    if (q != 0 && P == 1) return pbs1024_quad_launch(a, 1);
+  }
   if (P == 1) return launch_pair_p<1, L>(a);
   if (P == 2) return launch_pair_p<2, L>(a);
   return launch_pair_p<4, L>(a);

@@ -20,6 +20,12 @@ constexpr size_t pbs1024_pair_lds_bytes(int level, int pairs = PBS_PAIRS) {
          2 * (size_t)pairs * 4;  // + pair-sync counters
 }
 
+// Small batches at l = 3 (pbs1024_quad.hip): four waves per ciphertext, CTS = 1 or 2 ciphertexts per
+// workgroup; the pair kernel's ring and tables, one transpose scratch per wave, two counter sets.
+constexpr size_t pbs1024_quad_lds_bytes(int cts) {
+  return PBS1024_TABLE_BYTES + 4 * (size_t)cts * PBS1024_XCH_SLOTS * 16 + 3 * 3 * 512 * 16 + 2 * 4 * (size_t)cts * 4;
+}
+
 // N = 2048 kernel geometry (pbs2048.hip): four waves per ciphertext (one per even/odd half of
 // each GLWE polynomial), PBS2_CTS ciphertexts per workgroup, a ring of 16 KB key groups.
 constexpr int PBS2_CTS = 2;
@@ -134,6 +140,7 @@ struct PbsArgs {
 
 int pbs_launch(const PbsArgs& a);
 int pbs2048_launch(const PbsArgs& a);         // pbs2048.hip
+int pbs1024_quad_launch(const PbsArgs& a, int cts);  // pbs1024_quad.hip (cts = 1 or 2)
 int pbs_generic_launch(const PbsArgs& a);     // pbs_generic.hip
 int pbs1024k2_launch(const PbsArgs& a);       // pbs1024k2.hip
 

@@ -503,14 +503,18 @@ def test_keyswitch_key_byte_cache_and_fallback(B, oracle, torch_cuda, monkeypatc
     assert np.array_equal(B.to_host(out), ref)
 
 
-@pytest.mark.parametrize("pairs", [1, 2, 4])
+@pytest.mark.parametrize("pairs,quad", [(1, -1), (2, -1), (1, 0), (2, 0), (4, -1), (1, 2), (2, 1)])
 @pytest.mark.parametrize("level,base_log", [(1, 11), (2, 6), (3, 7)])
-def test_pbs_pairs_per_workgroup(B, oracle, torch_cuda, monkeypatch, pairs, level, base_log):
+def test_pbs_pairs_per_workgroup(B, oracle, torch_cuda, monkeypatch, pairs, quad, level, base_log):
     """The N = 1024 kernel at 1, 2 and 4 ciphertexts per workgroup (the small-batch forms that keep
     every CU busy at <= 2 x CUs ciphertexts, pbs.hip launch_pair; CONCRETE_HIP_PBS_PAIRS forces
-    one): ragged batches, permuted index arrays, per-sample LUTs — bit-exact vs the oracle with the
-    measured rounding residual below the certified bound."""
+    one).  At l = 3 and 1 per workgroup the four-wave kernel runs by default (pbs1024_quad.hip;
+    quad -1: the default, 1 / 2: forced with that many ciphertexts per workgroup, 0: the pair
+    kernel): ragged batches, permuted index arrays, per-sample LUTs — bit-exact
+    vs the oracle with the measured rounding residual below the certified bound."""
     monkeypatch.setenv("CONCRETE_HIP_PBS_PAIRS", str(pairs))
+    if quad >= 0:
+        monkeypatch.setenv("CONCRETE_HIP_PBS_QUAD", str(quad))
     p = replace(B.CFG2, n=12, level=level, base_log=base_log)
     S = Setup(B, oracle, torch_cuda, p, 5100 + 10 * level + pairs)
     width = 2

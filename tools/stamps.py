@@ -12,7 +12,8 @@ fbsk = B.convert_bsk(p, bsk, "cuda:0")
 rng = np.random.RandomState(0)
 cts = B.lwe_encrypt(lwe_sk, [B.encode(m, 3) for m in rng.randint(0, 8, nb)], p.n, B.secure_std(1, p.n), 5)
 acc = B.trivial_glwe(p, B.expand_lut(np.arange(8, dtype=np.uint64), p.N, 3))
-nw = 2 * ((nb + 3) // 4) * 4  # pair kernel: two waves per ciphertext, 4 pairs per workgroup
+P = int(os.environ.get("CONCRETE_HIP_PBS_PAIRS", "4"))
+nw = 2 * ((nb + P - 1) // P) * P  # pair kernel: two waves per ciphertext, P pairs per workgroup
 NS = 10  # kernel_util.hpp NSTAMP
 buf = torch.zeros(nw * NS, dtype=torch.int64, device="cuda:0")
 d_in, d_lut = B.to_device(cts, "cuda:0"), B.to_device(acc[None, :], "cuda:0")

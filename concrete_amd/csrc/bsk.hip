@@ -237,6 +237,37 @@ __global__ void __launch_bounds__(256) convert_bsk1024k2_kernel(cplx* __restrict
   dd_fft_scatter<M>(buf, tw_t, [&](int e) { return dest + blk * M + e; });
 }
 
+// N = 512, k = 3 / N = 256, k = 5, l = 1 (pbs_small.hip).  Block = (i, limb, col, row) in the order of
+// the output layout [n][limb][col][row][N/2]: limb `limb` of key polynomial (row, col), folded,
+// twisted by zeta_2N^j and transformed (M = N / 2 points), scaled 1 / (512 P) with P = 1024 / N (the
+// kernel's unnormalised unzip and zip), element e = (slot, lane) at frequency fft512_freq(lane, slot).
+template <int N, int K1>
+__global__ void __launch_bounds__(256) convert_bsk_small_kernel(cplx* __restrict__ dest,
+                                                               const uint64_t* __restrict__ src,
+                                                               const ddc* __restrict__ zeta_t,
+                                                               const ddc* __restrict__ tw_t) {
+  constexpr int M = N / 2, LOGM = N == 512 ? 8 : 7, P = 1024 / N;
+  __shared__ ddc buf[M];
+  const uint64_t blk = blockIdx.x;
+  const uint32_t row = (uint32_t)(blk % K1), col = (uint32_t)((blk / K1) % K1);
+  const uint32_t limb = (uint32_t)((blk / (K1 * K1)) % SM_LIMBS);
+  const uint64_t i = blk / (K1 * K1 * SM_LIMBS);
+  const uint64_t* g = src + ((i * K1 + row) * K1 + col) * N;  // [n][l = 1][row][col][N]
+  for (int j = threadIdx.x; j < M; j += blockDim.x) {
+    ddc z{dd_from(limb_value<SM_LIMBS>(g[j], limb)), dd_from(limb_value<SM_LIMBS>(g[j + M], limb))};
+    z = ddc_mul(z, zeta_t[j]);
+    const int r = (int)(__builtin_bitreverse32((uint32_t)j) >> (32 - LOGM));
+    buf[r] = z;
+  }
+  __syncthreads();
+  dd_fft<M>(buf, tw_t);
+  const double scale = 1.0 / (512.0 * P);
+  for (int e = threadIdx.x; e < M; e += blockDim.x) {
+    const ddc x = buf[fft512_freq(e & 63, e >> 6)];
+    dest[blk * M + e] = {(x.re.hi + x.re.lo) * scale, (x.im.hi + x.im.lo) * scale};
+  }
+}
+
 template <int N, int K, int L, int LIMBS>
 static int launch_convert(const ConvertArgs& a, const ddc* zeta, const ddc* tw) {
   const uint64_t blocks = (uint64_t)a.n * L * (K + 1) * (K + 1) * LIMBS;
@@ -292,12 +323,13 @@ int convert_bsk_launch(const ConvertArgs& a) {
   const bool n1024 = a.N == 1024 && a.k == 1 && a.limbs == 3 && a.level >= 1 && a.level <= 3;
   const bool n2048 = a.N == 2048 && a.k == 1 && a.limbs == (uint32_t)PBS2_LIMBS && a.level == 1;
   const bool k2 = a.N == 1024 && a.k == 2 && a.limbs == (uint32_t)K2_LIMBS && a.level == 1;
-  if (!n1024 && !n2048 && !k2) {
+  const bool small = pbs_small_shape(a.k, a.N, a.level) && a.limbs == (uint32_t)SM_LIMBS;
+  if (!n1024 && !n2048 && !k2 && !small) {
     set_error("unsupported BSK conversion parameters: N=%u k=%u level=%u limbs=%u", a.N, a.k, a.level, a.limbs);
     return -2;
   }
   std::vector<ddc> zeta, tw;
-  make_tables(1024, zeta, tw);  // both paths transform N = 1024 negacyclic polynomials
+  make_tables(small ? a.N : 1024, zeta, tw);  // the others transform N = 1024 negacyclic polynomials
   ddc *dz = nullptr, *dt = nullptr;
   keep_pool_memory();
   CHIP_CHECK(hipMallocAsync((void**)&dz, zeta.size() * sizeof(ddc), a.stream));
@@ -314,6 +346,19 @@ int convert_bsk_launch(const ConvertArgs& a) {
     const uint64_t blocks = (uint64_t)a.n * PBS2_LIMBS * 4 * (P2_PM ? 1 : 2);
     hipLaunchKernelGGL((convert_bsk2048_kernel<PBS2_LIMBS>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
                        reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, ds);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      set_error("convert launch failed: %s", hipGetErrorString(e));
+      rc = -1;
+    }
+  } else if (small) {
+    const uint64_t blocks = (uint64_t)a.n * SM_LIMBS * (a.k + 1) * (a.k + 1);
+    if (a.N == 512)
+      hipLaunchKernelGGL((convert_bsk_small_kernel<512, 4>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
+                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt);
+    else
+      hipLaunchKernelGGL((convert_bsk_small_kernel<256, 6>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
+                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       set_error("convert launch failed: %s", hipGetErrorString(e));

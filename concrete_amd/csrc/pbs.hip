@@ -596,6 +596,7 @@ int pbs_launch(const PbsArgs& a) {
   if (kind == KeyKind::GENERIC) return pbs_generic_launch(a);
   if (kind == KeyKind::N2048) return pbs2048_launch(a);
   if (kind == KeyKind::K2N1024) return pbs1024k2_launch(a);
+  if (kind == KeyKind::SMALL) return pbs_small_launch(a);
   if (kind == KeyKind::N1024 && a.limbs == 3) {
     switch (a.level) {
       case 1: return launch_pair<1>(a);

@@ -62,13 +62,33 @@ constexpr size_t pbs1024k2_lds_bytes() {
          3 * K2_CTS * 4;  // + per-wave sync counters
 }
 
+// N = 512, k = 3 and N = 256, k = 5, l = 1 (pbs_small.hip): P = 1024 / N polynomials per register
+// fft512, two waves per ciphertext, SM_CTS ciphertexts per workgroup, a ring of key groups (one limb
+// and one output column: the k + 1 row spectra).  Key: 4 balanced 16-bit limbs, scaled 1 / (512 P).
+constexpr int SM_CTS = 4;
+constexpr int SM_LIMBS = 4;
+constexpr int SM_SUB_BITS = 16;
+// largest digit: the certified bound (oracle/pyoracle.py:gpu_small_error_bound) is ~0.28 at N = 512,
+// k = 3 for any logB <= 24 and ~0.16 at N = 256, k = 5, logB <= 15 (one sub-digit, the table's
+// rows) on random keys of opt3 / opt1 size; wider digits run on the general path's companion key
+inline uint32_t pbs_small_max_logb(uint32_t N) { return N == 512 ? 24u : 15u; }
+constexpr int SM_RING_SLOTS = 4;
+constexpr size_t pbs_small_lds_bytes(int N, int K1) {
+  return PBS1024_TABLE_BYTES + 2 * SM_CTS * PBS1024_XCH_SLOTS * 16 + (size_t)SM_RING_SLOTS * K1 * (N / 2) * 16 +
+         2 * SM_CTS * 4;
+}
+inline bool pbs_small_shape(uint32_t k, uint32_t N, uint32_t level) {
+  return level == 1 && ((N == 512 && k == 3) || (N == 256 && k == 5));
+}
+
 // Device key formats.  N1024 / N2048: the hand-tuned kernels' layouts (pbs.hip, pbs2048.hip);
 // GENERIC: pbs_generic.hip, L balanced limbs of `bits` bits for any k <= GEN_MAX_K and
 // N = 256 .. 16384.  The format depends on (k, N, l) only: the runtime's key conversion call
 // carries no base_log (context.h:106-109).
-// K2N1024: pbs1024k2.hip (k = 2, N = 1024, l = 1).  The values are the ABI's format codes
+// K2N1024: pbs1024k2.hip (k = 2, N = 1024, l = 1); SMALL: pbs_small.hip (N = 512, k = 3 and N = 256,
+// k = 5, l = 1).  The values are the ABI's format codes
 // (concrete_hip_bsk_format).
-enum class KeyKind { NONE, N1024, N2048, GENERIC, K2N1024 };
+enum class KeyKind { NONE, N1024, N2048, GENERIC, K2N1024, SMALL };
 struct KeyFormat {
   KeyKind kind;
   uint32_t limbs, bits;
@@ -104,6 +124,7 @@ inline bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_
     case KeyKind::N2048: return base_log >= 1 && base_log <= PBS2_MAX_LOGB;
     case KeyKind::GENERIC: return generic_pbs_ok(k, N, level, base_log);
     case KeyKind::K2N1024: return base_log >= 1 && base_log <= K2_MAX_LOGB;
+    case KeyKind::SMALL: return base_log >= 1 && base_log <= pbs_small_max_logb(N);
     default: return false;
   }
 }
@@ -113,12 +134,14 @@ inline bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_
 //   N2048:   [n][limb][col][row][parity][512] complex f64 (pbs2048.hip)
 //   GENERIC: [n][col][limb][row][q][N/2] complex f64 (pbs_generic.hip)
 //   K2N1024: [n][limb][col][row][512] complex f64 (pbs1024k2.hip)
+//   SMALL:   [n][limb][col][row][N/2] complex f64 (pbs_small.hip)
 inline uint64_t fourier_bsk_bytes(uint32_t n, uint32_t k, uint32_t level, uint32_t N) {
   const KeyFormat f = key_format(k, N, level);
   switch (f.kind) {
     case KeyKind::N2048: return (uint64_t)n * f.limbs * (k + 1) * (k + 1) * 2 * 512 * 16ull * level;
     case KeyKind::N1024:
     case KeyKind::K2N1024:
+    case KeyKind::SMALL:
     case KeyKind::GENERIC: return (uint64_t)n * level * (k + 1) * (k + 1) * f.limbs * (N / 2) * 16ull;
     default: return 0;
   }
@@ -143,6 +166,7 @@ int pbs2048_launch(const PbsArgs& a);         // pbs2048.hip
 int pbs1024_quad_launch(const PbsArgs& a, int cts);  // pbs1024_quad.hip (cts = 1 or 2)
 int pbs_generic_launch(const PbsArgs& a);     // pbs_generic.hip
 int pbs1024k2_launch(const PbsArgs& a);       // pbs1024k2.hip
+int pbs_small_launch(const PbsArgs& a);       // pbs_small.hip
 
 struct ConvertArgs {
   hipStream_t stream;

@@ -1,0 +1,251 @@
+"""GPU parity tests of the small-ring kernel (concrete_amd/csrc/pbs_small.hip): N = 512, k = 3 and
+N = 256, k = 5, l = 1 — the optimizer's 3- and 1-bit rows (v0_last_128: opt3 n = 722 logB = 18,
+opt1 n = 592 logB = 15; bench.py --config opt3 / opt1) — vs the CPU oracle.
+
+Bit-exact u64 equality with the oracle's pure-integer Karatsuba product on the same keys and
+inputs, the measured rounding residual below the scheme's certified bound
+(oracle/pyoracle.py:gpu_small_error_bound, itself < 1/2), decrypt(out) == LUT[m], the device key
+layout against numpy transforms, both digit forms at N = 512 (one sub-digit at logB <= 15, two
+above), ragged batches (four ciphertexts per workgroup; at k = 5 the second wave of each
+ciphertext carries two empty polynomial slots), index arrays and mapped LUTs, edge inputs.
+"""
+from dataclasses import replace
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = {"N512_k3": 3, "N256_k5": 1}  # optimizer row (bits) per shape
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def B():
+    from concrete_amd import backend
+    return backend
+
+
+class Setup:
+    def __init__(self, B, oracle, torch, p, seed):
+        self.p = p
+        self.op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
+        self.lwe_sk = B.binary_key(p.n, seed)
+        self.glwe_sk = B.binary_key(p.big_n, seed + 1)
+        self.bsk = B.bsk_generate(p, self.lwe_sk, self.glwe_sk, seed + 2)
+        self.fbsk = B.convert_bsk(p, self.bsk, "cuda:0")
+        torch.cuda.synchronize()
+
+
+_cache = {}
+
+
+def small_setup(B, oracle, torch, shape, n=None, base_log=None, seed=9000):
+    key = (shape, n, base_log, seed)
+    if key not in _cache:
+        p = B.OPTIMIZER_SETS[SHAPES[shape]]
+        p = replace(p, n=n if n is not None else p.n, base_log=base_log if base_log is not None else p.base_log)
+        _cache[key] = Setup(B, oracle, torch, p, seed)
+    return _cache[key]
+
+
+def encrypt(B, S, msgs, width, seed, std=None):
+    std = B.secure_std(1, S.p.n) if std is None else std
+    return B.lwe_encrypt(S.lwe_sk, [B.encode(m, width) for m in msgs], S.p.n, std, seed)
+
+
+def lut_acc(B, S, table, width):
+    return B.trivial_glwe(S.p, B.expand_lut(np.array(table, dtype=np.uint64), S.p.N, width))
+
+
+def run_gpu(B, S, cts, luts, torch, lut_idx=None, in_idx=None, out_idx=None, resid=False):
+    dev = "cuda:0"
+    args = {}
+    n_s = cts.shape[0] if in_idx is None else len(in_idx)
+    for name, a in (("lut_idx", lut_idx), ("in_idx", in_idx), ("out_idx", out_idx)):
+        if a is not None:
+            args[name] = B.to_device(np.asarray(a, dtype=np.uint64), dev)
+    out = torch.zeros((n_s, S.p.lwe_out_size), dtype=torch.int64, device=dev)
+    r = torch.zeros(1, dtype=torch.int64, device=dev) if resid else None
+    B.pbs(S.p, S.fbsk, B.to_device(cts, dev), B.to_device(np.atleast_2d(luts), dev), out=out, num_samples=n_s,
+          resid=r, **args)
+    torch.cuda.synchronize()
+    res = B.to_host(out)
+    if resid:
+        return res, float(np.array([r.item()], dtype=np.int64).view(np.float64)[0])
+    return res
+
+
+def run_oracle(oracle, S, cts, luts, lut_idx=None, in_idx=None, out_idx=None):
+    out, _ = oracle.pbs_batch(S.op, cts, np.atleast_2d(luts), bsk=S.bsk, mode=oracle.MODE_KARATSUBA,
+                              lut_idx=lut_idx, in_idx=in_idx, out_idx=out_idx)
+    return out
+
+
+def bound(B, oracle, S):
+    return oracle.gpu_small_error_bound(B.to_host(S.fbsk).view(np.float64), S.p.N, S.p.k, S.p.base_log)
+
+
+def signed_limb(x, limb, limbs=4):
+    rem = x.astype(np.uint64).copy()
+    w = 64 // limbs
+    val = None
+    for _ in range(limb + 1):
+        vv = (rem & np.uint64((1 << w) - 1)).astype(np.int64)
+        sgn = np.where(vv >= (1 << (w - 1)), vv - (1 << w), vv)
+        val = sgn
+        rem = (rem - sgn.astype(np.uint64)) >> np.uint64(w)
+    return val.astype(np.float64)
+
+
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_key_format_and_layout(B, oracle, torch_cuda, shape):
+    """Device key [n][limb][col][row][slot][lane] == the 16-bit limb of key polynomial (row, col),
+    folded (g_t + i g_{t+N/2}), twisted by zeta_2N^t and transformed (N/2 points), at frequency
+    fft512_freq(lane, slot), divided by 512 P (P = 1024 / N).  (numpy's FFT is not correctly
+    rounded: tolerance 1e-13.)"""
+    S = small_setup(B, oracle, torch_cuda, shape, n=6)
+    p = S.p
+    N, K1, M, P = p.N, p.k + 1, p.N // 2, 1024 // p.N
+    assert B.bsk_format(p) == (5, 4, 16)
+    assert B.fourier_bsk_bytes(p) == p.n * 4 * K1 * K1 * M * 16
+    got = B.to_host(S.fbsk).view(np.float64).reshape(p.n, 4, K1, K1, M // 64, 64, 2)
+    bsk = S.bsk.reshape(p.n, 1, K1, K1, N)
+    lane = np.arange(64)
+    slot = np.arange(M // 64)
+    K = (lane[None, :] >> 3) + 8 * (lane[None, :] & 7) + 64 * slot[:, None]
+    tw = np.exp(1j * np.pi * np.arange(M) / N)
+    worst = 0.0
+    for i in (0, p.n - 1):
+        for li in range(4):
+            for col in range(K1):
+                for row in range(K1):
+                    lv = signed_limb(bsk[i, 0, row, col], li)
+                    ref = np.fft.fft((lv[:M] + 1j * lv[M:]) * tw)[K] / (512.0 * P)
+                    gg = got[i, li, col, row]
+                    worst = max(worst, np.max(np.abs(gg[..., 0] + 1j * gg[..., 1] - ref)) / np.max(np.abs(ref)))
+    assert worst < 1e-13, worst
+
+
+@pytest.mark.parametrize("batch", [1, 3, 4, 9])
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_bit_exact_small(B, oracle, torch_cuda, shape, batch):
+    """Ragged batches: 1, 3 and 9 leave ciphertext slots of the last workgroup empty."""
+    S = small_setup(B, oracle, torch_cuda, shape, n=14)
+    width = 3
+    rng = np.random.RandomState(batch)
+    table = rng.randint(0, 8, size=8)
+    msgs = rng.randint(0, 8, size=batch)
+    cts = encrypt(B, S, msgs, width, 10 + batch, std=2.0 ** -30)
+    acc = lut_acc(B, S, table, width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    assert np.array_equal(got, run_oracle(oracle, S, cts, acc))
+    assert resid < bound(B, oracle, S) < 0.5
+    dec = B.lwe_decrypt(S.glwe_sk, got, S.p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+
+
+@pytest.mark.parametrize("shape,logB", [("N512_k3", 6), ("N512_k3", 15), ("N512_k3", 16), ("N512_k3", 24),
+                                        ("N256_k5", 4), ("N256_k5", 12)])
+def test_digit_forms(B, oracle, torch_cuda, shape, logB):
+    """N = 512: one sub-digit up to logB = 15, the split d = d_lo + 2^16 d_hi from 16 (|d_hi| = 1 at
+    the tie) to the largest accepted 24; N = 256: one sub-digit (its gate is logB <= 15)."""
+    S = small_setup(B, oracle, torch_cuda, shape, n=10, base_log=logB, seed=9100 + logB)
+    width = 2
+    rng = np.random.RandomState(logB)
+    msgs = rng.randint(0, 4, size=6)
+    cts = encrypt(B, S, msgs, width, 50 + logB, std=2.0 ** -30)
+    acc = lut_acc(B, S, rng.randint(0, 4, size=4), width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    assert np.array_equal(got, run_oracle(oracle, S, cts, acc))
+    assert resid < bound(B, oracle, S) < 0.5
+
+
+def test_n256_wide_digits_run_on_the_general_path(B, oracle, torch_cuda):
+    """N = 256, k = 5 past the kernel's gate (logB = 18): through a keyset (memref route) the call
+    runs on the general path's companion key, built from the keyset's standard key; bit-exact."""
+    from concrete_amd import runtime as R
+    p = replace(B.OPTIMIZER_SETS[1], n=8, base_log=18)
+    assert B.pbs_supported(p)
+    lwe_sk = B.binary_key(p.n, 9300)
+    glwe_sk = B.binary_key(p.big_n, 9301)
+    bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 9302)
+    width = 2
+    rng = np.random.RandomState(18)
+    table = rng.randint(0, 4, size=4).astype(np.uint64)
+    tlu = B.expand_lut(table, p.N, width)
+    msgs = rng.randint(0, 4, size=5)
+    cts = B.lwe_encrypt(lwe_sk, [B.encode(m, width) for m in msgs], p.n, 2.0 ** -30, 77)
+    op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
+    ref, _ = oracle.pbs_batch(op, cts, B.trivial_glwe(p, tlu)[None, :], bsk=bsk, mode=oracle.MODE_KARATSUBA)
+    ks = R.Keyset([0])
+    try:
+        ks.add_bsk(0, bsk, p)
+        got = R.batched_bootstrap(ks, p, cts, tlu)
+    finally:
+        ks.close()
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_index_arrays_and_mapped_luts(B, oracle, torch_cuda, shape):
+    S = small_setup(B, oracle, torch_cuda, shape, n=14)
+    width = 2
+    nb = 7
+    rng = np.random.RandomState(9)
+    msgs = rng.randint(0, 4, size=nb)
+    cts = encrypt(B, S, msgs, width, 41, std=2.0 ** -30)
+    luts = np.stack([lut_acc(B, S, rng.randint(0, 4, size=4), width) for _ in range(nb)])
+    lut_idx = rng.permutation(nb).astype(np.uint64)
+    in_idx = rng.permutation(nb).astype(np.uint64)
+    out_idx = rng.permutation(nb).astype(np.uint64)
+    got = run_gpu(B, S, cts, luts, torch_cuda, lut_idx=lut_idx, in_idx=in_idx, out_idx=out_idx)
+    ref = run_oracle(oracle, S, cts, luts, lut_idx=lut_idx, in_idx=in_idx, out_idx=out_idx)
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_edge_inputs(B, oracle, torch_cuda, shape):
+    S = small_setup(B, oracle, torch_cuda, shape, n=14)
+    p = S.p
+    width = 2
+    rng = np.random.RandomState(5)
+    cts = encrypt(B, S, rng.randint(0, 4, size=8), width, 31, std=2.0 ** -30)
+    cts[0, : p.n // 2] = 0
+    cts[1, :] = 0
+    cts[2, :] = np.uint64(0xFFFFFFFFFFFFFFFF)
+    cts[3, : p.n] = np.uint64(1)
+    cts[4, : p.n] = np.uint64((1 << 54) - 1)
+    cts[5, p.n] = np.uint64(0xFFFFFFFFFFFFFFFF - 5)
+    cts[6, : p.n] = np.uint64(1 << 63)
+    cts[7, : p.n] = np.uint64(3 << 53)
+    acc = lut_acc(B, S, [3, 1, 0, 2], width)
+    got = run_gpu(B, S, cts, acc, torch_cuda)
+    assert np.array_equal(got, run_oracle(oracle, S, cts, acc))
+
+
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_full_row_bit_exact_and_bound(B, oracle, torch_cuda, shape):
+    """The full optimizer row (opt3: n = 722; opt1: n = 592): 512 samples decrypted, 3 bit-exact
+    vs the exact oracle, the measured residual under the certified bound (< 1/2)."""
+    S = small_setup(B, oracle, torch_cuda, shape)
+    width = SHAPES[shape]
+    rng = np.random.RandomState(3)
+    table = rng.randint(0, 1 << width, size=1 << width)
+    nb = 512
+    msgs = rng.randint(0, 1 << width, size=nb)
+    cts = encrypt(B, S, msgs, width, 77)
+    acc = lut_acc(B, S, table, width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    b = bound(B, oracle, S)
+    assert resid < b < 0.5, (resid, b)
+    dec = B.lwe_decrypt(S.glwe_sk, got, S.p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+    pick = np.array([0, 1, nb - 1])
+    assert np.array_equal(got[pick], run_oracle(oracle, S, cts[pick], acc))

@@ -36,7 +36,8 @@ KERNEL_HEADERS = ("concrete_amd/csrc/pbs.hpp", "concrete_amd/csrc/fft512.hpp", "
                   "concrete_amd/csrc/common.hpp")
 KERNEL_SOURCES = {"cfg2": ("concrete_amd/csrc/pbs.hip",) + KERNEL_HEADERS,
                   "cfg4": ("concrete_amd/csrc/pbs2048.hip",) + KERNEL_HEADERS,
-                  "opt4": ("concrete_amd/csrc/pbs1024k2.hip",) + KERNEL_HEADERS}
+                  "opt4": ("concrete_amd/csrc/pbs1024k2.hip",) + KERNEL_HEADERS,
+                  **{c: ("concrete_amd/csrc/pbs_small.hip",) + KERNEL_HEADERS for c in ("opt1", "opt2", "opt3")}}
 
 
 def kernel_source_hash(config: str = "cfg2") -> str:

@@ -72,9 +72,14 @@ constexpr int SM_SUB_BITS = 16;
 // k = 3 for any logB <= 24 and ~0.16 at N = 256, k = 5, logB <= 15 (one sub-digit, the table's
 // rows) on random keys of opt3 / opt1 size; wider digits run on the general path's companion key
 inline uint32_t pbs_small_max_logb(uint32_t N) { return N == 512 ? 24u : 15u; }
-constexpr int SM_RING_SLOTS = 4;
+// key group = one limb and SM_GC(N) output columns (K1 row spectra each); SM_RS(N) ring slots
+#ifndef SM_GC256
+#define SM_GC256 2
+#endif
+constexpr int sm_gc(int N) { return N == 256 ? SM_GC256 : 1; }
+constexpr int sm_rs(int N) { return N == 256 ? (SM_GC256 == 2 ? 3 : 4) : 4; }
 constexpr size_t pbs_small_lds_bytes(int N, int K1) {
-  return PBS1024_TABLE_BYTES + 2 * SM_CTS * PBS1024_XCH_SLOTS * 16 + (size_t)SM_RING_SLOTS * K1 * (N / 2) * 16 +
+  return PBS1024_TABLE_BYTES + 2 * SM_CTS * PBS1024_XCH_SLOTS * 16 + (size_t)sm_rs(N) * sm_gc(N) * K1 * (N / 2) * 16 +
          2 * SM_CTS * 4;
 }
 inline bool pbs_small_shape(uint32_t k, uint32_t N, uint32_t level) {

@@ -29,6 +29,21 @@
 #include "kernel_util.hpp"
 #include "pbs.hpp"
 
+// Diagnostic builds only (timing; wrong results): SMD_NOMAC / SMD_NOINV / SMD_NOFWD drop the key
+// products / inverse transforms / forward transforms, SMD_NOZIP the unzip and zip.
+#ifndef SMD_NOMAC
+#define SMD_NOMAC 0
+#endif
+#ifndef SMD_NOINV
+#define SMD_NOINV 0
+#endif
+#ifndef SMD_NOFWD
+#define SMD_NOFWD 0
+#endif
+#ifndef SMD_NOZIP
+#define SMD_NOZIP 0
+#endif
+
 namespace chip {
 
 namespace {
@@ -93,10 +108,13 @@ pbs_small_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
   constexpr int MS = SL / W;                // key-product slots per wave
   constexpr int NW = W * SM_CTS;
   constexpr int LOG2_2N = N == 512 ? 10 : 9;
-  constexpr int GROUP = K1 * M;             // (limb, column): the K1 row spectra
-  constexpr int NGRP = SM_LIMBS * K1;
+  constexpr int GC = sm_gc(N);              // output columns per key group
+  constexpr int GROUP = GC * K1 * M;        // (limb, GC columns): their K1 row spectra each
+  constexpr int NCG = K1 / GC;              // column groups per limb
+  static_assert(K1 % GC == 0, "column groups");
+  constexpr int NGRP = SM_LIMBS * NCG;
   constexpr int PER_I = NGRP * GROUP;
-  constexpr int RS = SM_RING_SLOTS, DIST = SM_RING_SLOTS - 1;
+  constexpr int RS = sm_rs(N), DIST = RS - 1;
   constexpr int PB = (GROUP * 16) % (NW * 1024) == 0 ? 16 : 4;  // LDS-DMA bytes per lane
   constexpr int GLDS = GROUP * 16 / (64 * PB) / NW;              // DMA instructions per wave per group
   constexpr int XS = (int)PBS1024_XCH_SLOTS;
@@ -234,18 +252,20 @@ pbs_small_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
         cplx tw2[4], tw3[4];
         fwd_p2_tw(tw2, T, lane >> 3);
         fwd_p3_tw(tw3, T, lane);
-        fft512_fwd_tw(vv, xch, lane, tw2, tw3, 0, [&]() __attribute__((always_inline)) {
-          if (sub > 0) sm_wait(sflags, ctl, v, scnt, guard);
-        });
+        if (!SMD_NOFWD)
+          fft512_fwd_tw(vv, xch, lane, tw2, tw3, 0, [&]() __attribute__((always_inline)) {
+            if (sub > 0) sm_wait(sflags, ctl, v, scnt, guard);
+          });
         // unzip: E_p = conj(tz_p) sum_q w_P^{-pq} Z[slot sl + q SL]
 #pragma unroll
         for (int sl = 0; sl < SL; ++sl) {
           cplx y[P];
 #pragma unroll
           for (int q = 0; q < P; ++q) y[q] = vv[sl + q * SL];
-          dftp<P>(y, true);
+          if (!SMD_NOZIP) dftp<P>(y, true);
 #pragma unroll
-          for (int p = 0; p < P; ++p) xch[(p * SL + sl) * 64 + lane] = p == 0 ? y[0] : cmulc(y[p], tz[p][sl]);
+          for (int p = 0; p < P; ++p)
+            xch[(p * SL + sl) * 64 + lane] = p == 0 || SMD_NOZIP ? y[p] : cmulc(y[p], tz[p][sl]);
         }
       }
       // the last sub-digit's spectra are published by the first key window's barrier
@@ -279,8 +299,9 @@ pbs_small_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
 #pragma unroll
         for (int js = 0; js < MS; ++js) Yn[cc][js] = {0.0, 0.0};
 #pragma unroll
-      for (int cc = 0; cc < K1; ++cc) {
-        const int r = li * K1 + cc;
+      for (int cg = 0; cg < NCG; ++cg) {
+        const int r = li * NCG + cg;
+        static_assert(DIST <= 3, "vmcnt tail cases");
         if (r + DIST - 1 < NGRP || !last_step) wait_vmcnt<GLDS * (DIST - 1)>();
         else if (r + 1 == NGRP) wait_vmcnt<0>();
         else if (r + 2 == NGRP) wait_vmcnt<GLDS>();
@@ -289,7 +310,7 @@ pbs_small_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
         if (r + DIST < NGRP) issue_group(key_step, r + DIST);
         else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
         if constexpr (li == 0) {
-          if (cc == 0) {
+          if (cg == 0) {
 #pragma unroll
             for (int row = 0; row < K1; ++row)
 #pragma unroll
@@ -297,17 +318,20 @@ pbs_small_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
                 X[row][SUBS - 1][js] = ctx[(row / P) * XS + ((row % P) * SL + sv + js) * 64 + lane];
           }
         }
+#pragma unroll
+      for (int c2 = 0; c2 < GC; ++c2) {
+        const int cc = cg * GC + c2;
         cplx Ya[MS];
 #pragma unroll
         for (int js = 0; js < MS; ++js) Ya[js] = Yc[cc][js];
-        const cplx* G = ring + (r % RS) * GROUP + sv * 64 + lane;
+        const cplx* G = ring + (r % RS) * GROUP + c2 * K1 * M + sv * 64 + lane;
 #pragma unroll
         for (int row = 0; row < K1; ++row) {
           cplx g[MS];
 #pragma unroll
           for (int js = 0; js < MS; ++js) g[js] = G[row * M + js * 64];
 #pragma unroll
-          for (int js = 0; js < MS; ++js) {
+          for (int js = 0; js < (SMD_NOMAC ? 0 : MS); ++js) {
             const cplx x0 = X[row][0][js];
             Ya[js].re = __builtin_fma(x0.re, g[js].re, __builtin_fma(-x0.im, g[js].im, Ya[js].re));
             Ya[js].im = __builtin_fma(x0.re, g[js].im, __builtin_fma(x0.im, g[js].re, Ya[js].im));
@@ -328,6 +352,7 @@ pbs_small_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
           if constexpr (HI) pin(Yn[cc][js]);
         }
       }
+      }
       if constexpr (HI) {
 #pragma unroll
         for (int cc = 0; cc < K1; ++cc)
@@ -343,16 +368,16 @@ pbs_small_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
         for (int p = 0; p < P; ++p) {
           // an empty polynomial slot of the last wave has no mailbox writer: zero
           const cplx e = v * P + p < K1 ? xch[(p * SL + sl) * 64 + lane] : cplx{0.0, 0.0};
-          y[p] = p == 0 ? e : cmul(e, tz[p][sl]);
+          y[p] = p == 0 || SMD_NOZIP ? e : cmul(e, tz[p][sl]);
         }
-        dftp<P>(y, false);
+        if (!SMD_NOZIP) dftp<P>(y, false);
 #pragma unroll
         for (int q = 0; q < P; ++q) V[sl + q * SL] = y[q];
       }
       {
         cplx gi2[4];
         inv_p2_stage_tw(gi2, T, lane & 7);
-        fft512_inv_tw(V, xch, T, lane, gi2, 0);
+        if (!SMD_NOINV) fft512_inv_tw(V, xch, T, lane, gi2, 0);
       }
 #pragma unroll
       for (int m = 0; m < 8; ++m) {

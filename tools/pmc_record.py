@@ -21,7 +21,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from bench import kernel_source_hash  # noqa: E402
 
-KERNEL = {"cfg2": "pbs1024_pair", "cfg4": "pbs2048", "opt4": "pbs1024k2"}
+KERNEL = {"cfg2": "pbs1024_pair", "cfg4": "pbs2048", "opt4": "pbs1024k2", "opt1": "pbs_small", "opt2": "pbs_small",
+          "opt3": "pbs_small"}
 # the general path (optB configs) runs several launches per PBS call (pbs_generic.hip): the record
 # sums every gen_* dispatch of the process's single call (tools/pmc.sh: --steps 1 --warmup 0 --no-e2e),
 # except the once-per-key conversion
@@ -31,7 +32,7 @@ GENERIC_SKIP = ("gen_convert",)
 
 def collect(src, kname):
     vals = {}
-    generic = kname.startswith("opt")
+    generic = kname.startswith("opt")  # a config without a kernel of its own: the general path
     for f in glob.glob(f"{src}/**/run_counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
             name = row.get("Kernel_Name", "")

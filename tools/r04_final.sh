@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4 closing evidence on the final sources.  Usage: tools/r04_final.sh TAG PART
 #   a: the whole GPU suite, smoke(), the default bench line, kernel-trace stats + PMC records of
-#      cfg2 / cfg4 / opt4
+#      cfg2 / cfg4 / opt4 / opt1 / opt3
 #   b: kernel-trace stats + PMC records of opt6 / opt7, bench lines of every config
 #   c: kernel-trace stats + PMC record of opt8 (long PMC passes)
 TAG=${1:-r04f}
@@ -40,6 +40,8 @@ a)
   prof cfg2 abde
   prof cfg4 abde
   prof opt4 abde
+  prof opt1 bde
+  prof opt3 bde
   ;;
 b)
   prof opt6 bde

@@ -51,7 +51,11 @@ b)
   done
   ;;
 c)
-  prof opt8 bde 600
+  # one stream: under --pmc the profiler serialises dispatches, and the chunked two-launch path's
+  # cross-stream event waits made a pass run > 600 s (r04f); the bytes and instructions of one
+  # call do not depend on the stream count
+  export CONCRETE_HIP_GEN_STREAMS=1
+  prof opt8 bde 500
   ;;
 esac
 echo "part $PART done"

@@ -587,3 +587,23 @@ def test_keyswitch_mfma_four_wave_kernel(B, oracle, torch_cuda, monkeypatch, ks_
     sel = rows[: min(len(rows), 64)]
     exp = oracle.keyswitch_batch(op, cts[in_idx[sel].astype(np.int64)], ksk)
     assert np.array_equal(B.to_host(out2)[sel], exp)
+
+
+@pytest.mark.parametrize("cts_per_wg", [1, 2])
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_pbs_quad_tiny_n(B, oracle, torch_cuda, monkeypatch, cts_per_wg, n):
+    """The four-wave kernel (pbs1024_quad.hip) over blind rotations of 1-3 steps: its key ring's
+    prologue and tail, the per-step delta exchange; bit-exact vs the oracle."""
+    monkeypatch.setenv("CONCRETE_HIP_PBS_QUAD", str(cts_per_wg))
+    p = replace(B.CFG2, n=n)
+    S = Setup(B, oracle, torch_cuda, p, 5300 + 10 * n + cts_per_wg)
+    width = 2
+    rng = np.random.RandomState(n)
+    msgs = rng.randint(0, 4, size=5)
+    cts = encrypt(B, S, msgs, width, 71 + n, std=2.0 ** -25)
+    acc = lut_acc(B, S, rng.randint(0, 4, size=4), width)
+    dev = "cuda:0"
+    out = B.pbs(p, S.fbsk, B.to_device(cts, dev), B.to_device(acc[None, :], dev))
+    torch_cuda.cuda.synchronize()
+    ref, _ = oracle.pbs_batch(S.op, cts, acc[None, :], fbsk=S.fbsk_cpu)
+    assert np.array_equal(B.to_host(out), ref)

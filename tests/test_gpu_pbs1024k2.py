@@ -28,9 +28,6 @@ def B():
     return backend
 
 
-OPT4 = None  # set from backend.OPTIMIZER_SETS[4] in the fixtures
-
-
 class Setup:
     def __init__(self, B, oracle, torch, p, seed):
         self.p = p
@@ -208,3 +205,17 @@ def test_opt4_full_bit_exact_and_bound(B, oracle, opt4, torch_cuda):
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
     pick = np.array([0, 1, 2, nb - 1])
     assert np.array_equal(got[pick], run_oracle(oracle, opt4, cts[pick], acc))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_tiny_n(B, oracle, torch_cuda, n):
+    """Blind rotations of 1-3 steps: the key ring's prologue and tail (the last step issues no
+    further groups and waits for fewer in flight) meet within one or two steps."""
+    S = Setup(B, oracle, torch_cuda, replace(B.OPTIMIZER_SETS[4], n=n), 8400 + n)
+    width = 3
+    rng = np.random.RandomState(n)
+    msgs = rng.randint(0, 8, size=5)
+    cts = encrypt(B, S, msgs, width, 60 + n, std=2.0 ** -30)
+    acc = lut_acc(B, S, rng.randint(0, 8, size=8), width)
+    got = run_gpu(B, S, cts, acc, torch_cuda)
+    assert np.array_equal(got, run_oracle(oracle, S, cts, acc))

@@ -249,3 +249,18 @@ def test_full_row_bit_exact_and_bound(B, oracle, torch_cuda, shape):
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
     pick = np.array([0, 1, nb - 1])
     assert np.array_equal(got[pick], run_oracle(oracle, S, cts[pick], acc))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_tiny_n(B, oracle, torch_cuda, shape, n):
+    """Blind rotations of 1-3 steps: the key ring's prologue (DIST groups in flight) and its tail
+    meet within one or two steps."""
+    S = small_setup(B, oracle, torch_cuda, shape, n=n, seed=9400 + n)
+    width = 2
+    rng = np.random.RandomState(n)
+    msgs = rng.randint(0, 4, size=5)
+    cts = encrypt(B, S, msgs, width, 60 + n, std=2.0 ** -30)
+    acc = lut_acc(B, S, rng.randint(0, 4, size=4), width)
+    got = run_gpu(B, S, cts, acc, torch_cuda)
+    assert np.array_equal(got, run_oracle(oracle, S, cts, acc))

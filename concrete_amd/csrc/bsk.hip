@@ -237,7 +237,7 @@ __global__ void __launch_bounds__(256) convert_bsk1024k2_kernel(cplx* __restrict
   dd_fft_scatter<M>(buf, tw_t, [&](int e) { return dest + blk * M + e; });
 }
 
-// N = 512, k = 3 / N = 256, k = 5, l = 1 (pbs_small.hip).  Block = (i, limb, col, row) in the order of
+// N = 512, k = 3 / N = 256, k = 5, 6, l = 1 (pbs_small.hip).  Block = (i, limb, col, row) in the order of
 // the output layout [n][limb][col][row][N/2]: limb `limb` of key polynomial (row, col), folded,
 // twisted by zeta_2N^j and transformed (M = N / 2 points), scaled 1 / (512 P) with P = 1024 / N (the
 // kernel's unnormalised unzip and zip), element e = (slot, lane) at frequency fft512_freq(lane, slot).
@@ -356,8 +356,11 @@ int convert_bsk_launch(const ConvertArgs& a) {
     if (a.N == 512)
       hipLaunchKernelGGL((convert_bsk_small_kernel<512, 4>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
                          reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt);
-    else
+    else if (a.k == 5)
       hipLaunchKernelGGL((convert_bsk_small_kernel<256, 6>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
+                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt);
+    else
+      hipLaunchKernelGGL((convert_bsk_small_kernel<256, 7>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
                          reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

@@ -62,28 +62,29 @@ constexpr size_t pbs1024k2_lds_bytes() {
          3 * K2_CTS * 4;  // + per-wave sync counters
 }
 
-// N = 512, k = 3 and N = 256, k = 5, l = 1 (pbs_small.hip): P = 1024 / N polynomials per register
+// N = 512, k = 3 and N = 256, k = 5 / 6, l = 1 (pbs_small.hip): P = 1024 / N polynomials per register
 // fft512, two waves per ciphertext, SM_CTS ciphertexts per workgroup, a ring of key groups (one limb
 // and one output column: the k + 1 row spectra).  Key: 4 balanced 16-bit limbs, scaled 1 / (512 P).
 constexpr int SM_CTS = 4;
 constexpr int SM_LIMBS = 4;
 constexpr int SM_SUB_BITS = 16;
-// largest digit: the certified bound (oracle/pyoracle.py:gpu_small_error_bound) is ~0.28 at N = 512,
-// k = 3 for any logB <= 24 and ~0.16 at N = 256, k = 5, logB <= 15 (one sub-digit, the table's
-// rows) on random keys of opt3 / opt1 size; wider digits run on the general path's companion key
-inline uint32_t pbs_small_max_logb(uint32_t N) { return N == 512 ? 24u : 15u; }
+// largest digit: the certified bound (oracle/pyoracle.py:gpu_small_error_bound) on random keys of
+// the table rows' size is 0.28 at N = 512, k = 3 and 0.34 / 0.39 at N = 256, k = 5 / 6 for any
+// logB <= 24 (0.17 / 0.19 with one sub-digit, logB <= 15); wider digits run on the general path
+inline uint32_t pbs_small_max_logb(uint32_t N) { return N == 512 || N == 256 ? 24u : 0u; }
 // key group = one limb and SM_GC(N) output columns (K1 row spectra each); SM_RS(N) ring slots
+// (two columns at N = 256 when k + 1 is even: half the key windows, 3 x 24 KB slots)
 #ifndef SM_GC256
 #define SM_GC256 2
 #endif
-constexpr int sm_gc(int N) { return N == 256 ? SM_GC256 : 1; }
-constexpr int sm_rs(int N) { return N == 256 ? (SM_GC256 == 2 ? 3 : 4) : 4; }
+constexpr int sm_gc(int N, int K1) { return N == 256 && K1 % SM_GC256 == 0 ? SM_GC256 : 1; }
+constexpr int sm_rs(int N, int K1) { return sm_gc(N, K1) == 2 ? 3 : 4; }
 constexpr size_t pbs_small_lds_bytes(int N, int K1) {
-  return PBS1024_TABLE_BYTES + 2 * SM_CTS * PBS1024_XCH_SLOTS * 16 + (size_t)sm_rs(N) * sm_gc(N) * K1 * (N / 2) * 16 +
-         2 * SM_CTS * 4;
+  return PBS1024_TABLE_BYTES + 2 * SM_CTS * PBS1024_XCH_SLOTS * 16 +
+         (size_t)sm_rs(N, K1) * sm_gc(N, K1) * K1 * (N / 2) * 16 + 2 * SM_CTS * 4;
 }
 inline bool pbs_small_shape(uint32_t k, uint32_t N, uint32_t level) {
-  return level == 1 && ((N == 512 && k == 3) || (N == 256 && k == 5));
+  return level == 1 && ((N == 512 && k == 3) || (N == 256 && (k == 5 || k == 6)));
 }
 
 // Device key formats.  N1024 / N2048: the hand-tuned kernels' layouts (pbs.hip, pbs2048.hip);

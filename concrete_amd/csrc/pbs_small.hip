@@ -1,12 +1,12 @@
 // pbs_small.hip — batched classic PBS for the optimizer's small rings: N = 512, k = 3 and
-// N = 256, k = 5, l = 1 (v0_last_128's 3- and 1-bit rows: opt3 n = 722 logB = 18, opt1 n = 592
-// logB = 15) on CDNA4 (gfx950).
+// N = 256, k = 5 / 6, l = 1 (v0_last_128's 1- to 3-bit rows: opt3 n = 722 logB = 18, opt1 n = 592
+// logB = 15, the k = 6 rows at log norm2 1-4 with logB = 18) on CDNA4 (gfx950).
 //
 // Same semantics as pbs.hip (concrete-cpu c_api/bootstrap.rs:347-414 -> tfhe 0.10
 // blind_rotate_assign + sample extract; oracle/tfhe_oracle.c:ora_pbs) and the exact arithmetic of
 // pbs1024k2.hip: 4 balanced 16-bit key limbs, digits split on the limb grid (d = d_lo + 2^16 d_hi;
 // logB <= 15 needs no split), slot m = sum over rows of d_lo g_m + d_hi g_{m-1}, certified error
-// < 1/2 (oracle/pyoracle.py:gpu_small_error_bound; logB <= 24 at N = 512, <= 15 at 256).
+// < 1/2 (oracle/pyoracle.py:gpu_small_error_bound; logB <= 24).
 //
 // P = 1024 / N polynomials share one register fft512 (fft512.hpp).  With z_{P j + p} = a_p[j] (the
 // folded N-point polynomial p), the transform's built-in twist zeta_1024^{P j + p} is the N-ring
@@ -17,8 +17,8 @@
 // backwards (zip, one inverse fft512 for P output polynomials).  Unnormalised unzip and zip scale the
 // products by P^2 M: the key is stored scaled by 1 / (512 P).
 //
-// Mapping: two waves per ciphertext, wave v owning polynomials [vP, vP + P) (k = 5, N = 256: the
-// second wave's last two are empty) — 16 u64 per lane, lane t holding coefficients
+// Mapping: two waves per ciphertext, wave v owning polynomials [vP, vP + P) (N = 256: the second
+// wave's last two (k = 5) or one (k = 6) are empty) — 16 u64 per lane, lane t holding coefficients
 // t / P + (64 / P) m and that + N / 2 of its polynomial t mod P.  Each wave transforms its own
 // polynomials' sub-digits, keeps half of the spectrum slots of every row, runs the key products
 // for all outputs on them, mails the outputs to their owners and runs the inverse of its own.
@@ -108,13 +108,13 @@ pbs_small_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
   constexpr int MS = SL / W;                // key-product slots per wave
   constexpr int NW = W * SM_CTS;
   constexpr int LOG2_2N = N == 512 ? 10 : 9;
-  constexpr int GC = sm_gc(N);              // output columns per key group
+  constexpr int GC = sm_gc(N, K1);          // output columns per key group
   constexpr int GROUP = GC * K1 * M;        // (limb, GC columns): their K1 row spectra each
   constexpr int NCG = K1 / GC;              // column groups per limb
   static_assert(K1 % GC == 0, "column groups");
   constexpr int NGRP = SM_LIMBS * NCG;
   constexpr int PER_I = NGRP * GROUP;
-  constexpr int RS = sm_rs(N), DIST = RS - 1;
+  constexpr int RS = sm_rs(N, K1), DIST = RS - 1;
   constexpr int PB = (GROUP * 16) % (NW * 1024) == 0 ? 16 : 4;  // LDS-DMA bytes per lane
   constexpr int GLDS = GROUP * 16 / (64 * PB) / NW;              // DMA instructions per wave per group
   constexpr int XS = (int)PBS1024_XCH_SLOTS;
@@ -444,11 +444,9 @@ static int launch_small_t(const PbsArgs& a) {
 
 template <int N, int K1>
 static int launch_small_n(const PbsArgs& a) {
-  // logB <= 15: |digit| <= 2^14 fits the 16-bit grid whole (one sub-digit; the only form at N = 256)
+  // logB <= 15: |digit| <= 2^14 fits the 16-bit grid whole (one sub-digit)
   if (a.base_log <= 15) return a.resid ? launch_small_t<N, K1, 1, true>(a) : launch_small_t<N, K1, 1, false>(a);
-  if constexpr (N == 512) return a.resid ? launch_small_t<N, K1, 2, true>(a) : launch_small_t<N, K1, 2, false>(a);
-  set_error("pbs: N=%d base_log=%u is outside the small-ring kernel's exact range", N, a.base_log);
-  return -2;
+  return a.resid ? launch_small_t<N, K1, 2, true>(a) : launch_small_t<N, K1, 2, false>(a);
 }
 
 int pbs_small_launch(const PbsArgs& a) {
@@ -459,7 +457,8 @@ int pbs_small_launch(const PbsArgs& a) {
     return -2;
   }
   if (a.num_samples == 0) return 0;
-  return a.N == 512 ? launch_small_n<512, 4>(a) : launch_small_n<256, 6>(a);
+  if (a.N == 512) return launch_small_n<512, 4>(a);
+  return a.k == 5 ? launch_small_n<256, 6>(a) : launch_small_n<256, 7>(a);
 }
 
 }  // namespace chip

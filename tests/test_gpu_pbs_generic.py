@@ -33,7 +33,7 @@ def B():
 # (label, k, N, n, l, logB, message bits): v0_last_128 rows with n reduced for the oracle
 CASES = [
     ("1bit_k5_N256", 5, 256, 24, 1, 15, 1),
-    ("2bit_k6_N256", 6, 256, 16, 1, 18, 2),
+    ("2bit_k6_N256", 6, 256, 16, 1, 18, 2),  # the small-ring kernel since round 4
     ("3bit_k3_N512", 3, 512, 16, 1, 18, 3),
     ("4bit_k2_N1024", 2, 1024, 12, 1, 23, 4),
     ("k1_N2048_l2", 1, 2048, 12, 2, 10, 3),
@@ -52,10 +52,11 @@ CASES = [
     # S = 2 / 4 workgroups (gen_split_*_kernel), the key converted the same way
     ("9bit_k1_N32768", 1, 32768, 2, 2, 15, 9),
     ("10bit_k1_N65536", 1, 65536, 2, 2, 14, 10),
-    # round 4: the 1-, 3- and 4-bit log-norm2-0 rows above run on their own kernels (pbs_small.hip,
-    # pbs1024k2.hip); these keep the one-launch tile kernels at N = 256 / 512 under test
+    # round 4: the 1- to 4-bit rows above run on their own kernels (pbs_small.hip, pbs1024k2.hip);
+    # these keep the one-launch tile kernels at N = 256 / 512 under test
     ("3bit_k4_N512_tile", 4, 512, 14, 1, 23, 3),
     ("2bit_k5_N256_l2_tile", 5, 256, 16, 2, 10, 2),
+    ("1bit_k6_N256_l2_tile", 6, 256, 12, 2, 12, 1),
 ]
 
 
@@ -109,7 +110,7 @@ def test_generic_pbs_bit_exact(B, oracle, torch_cuda, case):
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
 
 
-@pytest.mark.parametrize("ci", [1, 15, 16, 5], ids=[CASES[i][0] for i in (1, 15, 16, 5)])
+@pytest.mark.parametrize("ci", [17, 15, 16, 5], ids=[CASES[i][0] for i in (17, 15, 16, 5)])
 def test_generic_tile_many_workgroups(B, oracle, torch_cuda, ci):
     """The one-launch tile kernels over many workgroups (67 ciphertexts: not a multiple of any
     tile size, so the last workgroup runs empty groups) and the one-launch N = 4096 kernel (a
@@ -139,7 +140,7 @@ def test_generic_8bit_long_chain_decrypts(B, oracle, torch_cuda):
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
 
 
-@pytest.mark.parametrize("ci", [1, 15, 16, 9], ids=[CASES[i][0] for i in (1, 15, 16, 9)])
+@pytest.mark.parametrize("ci", [17, 15, 16, 9], ids=[CASES[i][0] for i in (17, 15, 16, 9)])
 def test_generic_index_arrays(B, oracle, torch_cuda, ci):
     """Mapped LUTs and permuted input/output rows (GPUDFG.cpp:1149-1205) on the general path:
     the one-launch tile kernels (N = 256: 4 ciphertexts per workgroup, the last one partly

@@ -1,6 +1,6 @@
 """GPU parity tests of the small-ring kernel (concrete_amd/csrc/pbs_small.hip): N = 512, k = 3 and
-N = 256, k = 5, l = 1 — the optimizer's 3- and 1-bit rows (v0_last_128: opt3 n = 722 logB = 18,
-opt1 n = 592 logB = 15; bench.py --config opt3 / opt1) — vs the CPU oracle.
+N = 256, k = 5 / 6, l = 1 — the optimizer's 1- to 3-bit rows (v0_last_128: opt3 n = 722 logB = 18,
+opt1 n = 592 logB = 15, k = 6 n = 596 logB = 18; bench.py --config opt3 / opt1) — vs the CPU oracle.
 
 Bit-exact u64 equality with the oracle's pure-integer Karatsuba product on the same keys and
 inputs, the measured rounding residual below the scheme's certified bound
@@ -16,7 +16,10 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-SHAPES = {"N512_k3": 3, "N256_k5": 1}  # optimizer row (bits) per shape
+# shape -> (optimizer row parameters, message bits): opt3, opt1 and the k = 6 row of v0_last_128 at
+# 1 bit, log norm2 2 (n = 596, br 1/18)
+SHAPES = {"N512_k3": (3, None), "N256_k5": (1, None), "N256_k6": (1, dict(n=596, k=6, N=256, level=1, base_log=18,
+                                                                          ks_level=3, ks_base_log=4))}
 
 
 @pytest.fixture(scope="module")
@@ -49,7 +52,8 @@ _cache = {}
 def small_setup(B, oracle, torch, shape, n=None, base_log=None, seed=9000):
     key = (shape, n, base_log, seed)
     if key not in _cache:
-        p = B.OPTIMIZER_SETS[SHAPES[shape]]
+        bits, explicit = SHAPES[shape]
+        p = B.PbsParams(**explicit) if explicit else B.OPTIMIZER_SETS[bits]
         p = replace(p, n=n if n is not None else p.n, base_log=base_log if base_log is not None else p.base_log)
         _cache[key] = Setup(B, oracle, torch, p, seed)
     return _cache[key]
@@ -152,10 +156,11 @@ def test_bit_exact_small(B, oracle, torch_cuda, shape, batch):
 
 
 @pytest.mark.parametrize("shape,logB", [("N512_k3", 6), ("N512_k3", 15), ("N512_k3", 16), ("N512_k3", 24),
-                                        ("N256_k5", 4), ("N256_k5", 12)])
+                                        ("N256_k5", 4), ("N256_k5", 12), ("N256_k5", 16), ("N256_k5", 24),
+                                        ("N256_k6", 15), ("N256_k6", 24)])
 def test_digit_forms(B, oracle, torch_cuda, shape, logB):
-    """N = 512: one sub-digit up to logB = 15, the split d = d_lo + 2^16 d_hi from 16 (|d_hi| = 1 at
-    the tie) to the largest accepted 24; N = 256: one sub-digit (its gate is logB <= 15)."""
+    """One sub-digit up to logB = 15, the split d = d_lo + 2^16 d_hi from 16 (|d_hi| = 1 at the tie)
+    to the largest accepted 24, at both ring sizes."""
     S = small_setup(B, oracle, torch_cuda, shape, n=10, base_log=logB, seed=9100 + logB)
     width = 2
     rng = np.random.RandomState(logB)
@@ -168,16 +173,16 @@ def test_digit_forms(B, oracle, torch_cuda, shape, logB):
 
 
 def test_n256_wide_digits_run_on_the_general_path(B, oracle, torch_cuda):
-    """N = 256, k = 5 past the kernel's gate (logB = 18): through a keyset (memref route) the call
+    """N = 256, k = 5 past the kernel's gate (logB = 25): through a keyset (memref route) the call
     runs on the general path's companion key, built from the keyset's standard key; bit-exact."""
     from concrete_amd import runtime as R
-    p = replace(B.OPTIMIZER_SETS[1], n=8, base_log=18)
+    p = replace(B.OPTIMIZER_SETS[1], n=8, base_log=25)
     assert B.pbs_supported(p)
     lwe_sk = B.binary_key(p.n, 9300)
     glwe_sk = B.binary_key(p.big_n, 9301)
     bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 9302)
     width = 2
-    rng = np.random.RandomState(18)
+    rng = np.random.RandomState(25)
     table = rng.randint(0, 4, size=4).astype(np.uint64)
     tlu = B.expand_lut(table, p.N, width)
     msgs = rng.randint(0, 4, size=5)
@@ -232,10 +237,10 @@ def test_edge_inputs(B, oracle, torch_cuda, shape):
 
 @pytest.mark.parametrize("shape", list(SHAPES))
 def test_full_row_bit_exact_and_bound(B, oracle, torch_cuda, shape):
-    """The full optimizer row (opt3: n = 722; opt1: n = 592): 512 samples decrypted, 3 bit-exact
+    """The full optimizer row (opt3: n = 722; opt1: n = 592; k = 6: n = 596): 512 samples decrypted, 3 bit-exact
     vs the exact oracle, the measured residual under the certified bound (< 1/2)."""
     S = small_setup(B, oracle, torch_cuda, shape)
-    width = SHAPES[shape]
+    width = SHAPES[shape][0]
     rng = np.random.RandomState(3)
     table = rng.randint(0, 1 << width, size=1 << width)
     nb = 512

@@ -114,13 +114,13 @@ def test_key_formats_and_exact_range():
     assert L.concrete_hip_fourier_bsk_size_bytes(801, 2, 1, 1024) == 801 * 4 * 9 * 512 * 16
     assert L.concrete_hip_pbs_supported(2, 1024, 1, 24) == 1
     assert L.concrete_hip_generic_error_bound(2, 1024, 1, 23, 0.0) == -1.0
-    # the optimizer's 1- and 3-bit rows (N = 256, k = 5 / N = 512, k = 3, l = 1): the small-ring kernel
-    # (pbs_small.hip, round 4), format code 5, digits up to 15 / 24 bits (wider: the general path)
-    assert fmt(3, 512, 1) == (5, 4, 16) and fmt(5, 256, 1) == (5, 4, 16)
+    # the optimizer's 1- to 3-bit rows (N = 256, k = 5 / 6, N = 512, k = 3, l = 1): the small-ring kernel
+    # (pbs_small.hip, round 4), format code 5, digits up to 24 bits (wider: the general path)
+    assert fmt(3, 512, 1) == (5, 4, 16) and fmt(5, 256, 1) == (5, 4, 16) and fmt(6, 256, 1) == (5, 4, 16)
     assert L.concrete_hip_fourier_bsk_size_bytes(722, 3, 1, 512) == 722 * 4 * 16 * 256 * 16
     assert L.concrete_hip_pbs_supported(3, 512, 1, 24) == 1 and L.concrete_hip_pbs_supported(5, 256, 1, 15) == 1
-    assert L.concrete_hip_pbs_supported(5, 256, 1, 18) == 1  # past the small-ring gate: the general path
-    for k, N, l, logB in [(6, 256, 1, 18), (4, 512, 1, 23), (2, 1024, 2, 15), (1, 4096, 1, 22),
+    assert L.concrete_hip_pbs_supported(5, 256, 1, 25) == 1  # past the small-ring gate: the general path
+    for k, N, l, logB in [(6, 256, 2, 12), (4, 512, 1, 23), (2, 1024, 2, 15), (1, 4096, 1, 22),
                           (1, 8192, 1, 22), (1, 16384, 2, 15), (1, 2048, 2, 10)]:
         kind, limbs, bits = fmt(k, N, l)
         assert kind == 3 and limbs * bits >= 64, (k, N, l)

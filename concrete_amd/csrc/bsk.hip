@@ -213,20 +213,23 @@ __global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__
 }
 #endif
 
-// N = 1024, k = 2, l = 1 (pbs1024k2.hip).  Block = (i, limb, col, row), in the order of the output
-// layout [n][limb][col][row][512]: limb `limb` of key polynomial (row, col), folded, twisted and
-// transformed like the k = 1 key.
+// N = 1024, k = 2, l = 1 or 2 (pbs1024k2.hip).  Block = (i, limb, col, q, row), in the order of the
+// output layout [n][limb][col][q][row][512]: limb `limb` of key polynomial (row, col) of level
+// v = l - 1 - q (q in digit order), folded, twisted and transformed like the k = 1 key.
 __global__ void __launch_bounds__(256) convert_bsk1024k2_kernel(cplx* __restrict__ dest,
                                                                const uint64_t* __restrict__ src,
                                                                const ddc* __restrict__ zeta_t,
-                                                               const ddc* __restrict__ tw_t) {
+                                                               const ddc* __restrict__ tw_t, uint32_t level) {
   constexpr int M = 512, LOGM = 9, N = 1024;
   __shared__ ddc buf[M];
   const uint64_t blk = blockIdx.x;
-  const uint32_t row = (uint32_t)(blk % 3), col = (uint32_t)((blk / 3) % 3);
-  const uint32_t limb = (uint32_t)((blk / 9) % K2_LIMBS);
-  const uint64_t i = blk / (9 * K2_LIMBS);
-  const uint64_t* g = src + ((i * 3 + row) * 3 + col) * N;  // [n][l = 1][row][col][N]
+  const uint32_t row = (uint32_t)(blk % 3);
+  const uint32_t q = (uint32_t)((blk / 3) % level);
+  const uint32_t col = (uint32_t)((blk / (3 * level)) % 3);
+  const uint32_t limb = (uint32_t)((blk / (9 * level)) % K2_LIMBS);
+  const uint64_t i = blk / (9 * level * K2_LIMBS);
+  const uint32_t v = level - 1 - q;
+  const uint64_t* g = src + (((i * level + v) * 3 + row) * 3 + col) * N;  // [n][l][row][col][N]
   for (int j = threadIdx.x; j < M; j += blockDim.x) {
     ddc z{dd_from(limb_value<K2_LIMBS>(g[j], limb)), dd_from(limb_value<K2_LIMBS>(g[j + M], limb))};
     z = ddc_mul(z, zeta_t[j]);
@@ -322,7 +325,7 @@ int convert_bsk_launch(const ConvertArgs& a) {
   if (key_format(a.k, a.N, a.level).kind == KeyKind::GENERIC) return convert_bsk_generic_launch(a);
   const bool n1024 = a.N == 1024 && a.k == 1 && a.limbs == 3 && a.level >= 1 && a.level <= 3;
   const bool n2048 = a.N == 2048 && a.k == 1 && a.limbs == (uint32_t)PBS2_LIMBS && a.level == 1;
-  const bool k2 = a.N == 1024 && a.k == 2 && a.limbs == (uint32_t)K2_LIMBS && a.level == 1;
+  const bool k2 = a.N == 1024 && a.k == 2 && a.limbs == (uint32_t)K2_LIMBS && (a.level == 1 || a.level == 2);
   const bool small = pbs_small_shape(a.k, a.N, a.level) && a.limbs == (uint32_t)SM_LIMBS;
   if (!n1024 && !n2048 && !k2 && !small) {
     set_error("unsupported BSK conversion parameters: N=%u k=%u level=%u limbs=%u", a.N, a.k, a.level, a.limbs);
@@ -368,9 +371,9 @@ int convert_bsk_launch(const ConvertArgs& a) {
       rc = -1;
     }
   } else if (k2) {
-    const uint64_t blocks = (uint64_t)a.n * K2_LIMBS * 9;
+    const uint64_t blocks = (uint64_t)a.n * K2_LIMBS * 9 * a.level;
     hipLaunchKernelGGL(convert_bsk1024k2_kernel, dim3((uint32_t)blocks), dim3(256), 0, a.stream,
-                       reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt);
+                       reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       set_error("convert launch failed: %s", hipGetErrorString(e));

@@ -20,7 +20,7 @@ inline bool pbs_needs_generic_key(uint32_t k, uint32_t N, uint32_t level, uint32
   if (f.kind == KeyKind::N1024 && !pbs1024_exact(k, level, base_log)) return generic_pbs_ok(k, N, level, base_log);
   if (f.kind == KeyKind::N2048 && !(base_log >= 1 && base_log <= PBS2_MAX_LOGB))
     return generic_pbs_ok(k, N, level, base_log);
-  if (f.kind == KeyKind::K2N1024 && !(base_log >= 1 && base_log <= K2_MAX_LOGB))
+  if (f.kind == KeyKind::K2N1024 && !(base_log >= 1 && base_log <= k2_max_logb(level)))
     return generic_pbs_ok(k, N, level, base_log);
   if (f.kind == KeyKind::SMALL && !(base_log >= 1 && base_log <= pbs_small_max_logb(N)))
     return generic_pbs_ok(k, N, level, base_log);

@@ -57,6 +57,8 @@ constexpr int K2_LIMBS = 4;
 constexpr int K2_SUBS = 2;
 constexpr int K2_SUB_BITS = 16;
 constexpr int K2_MAX_LOGB = 24;  // certified bound < 1/2 (oracle/pyoracle.py:gpu1024k2_error_bound)
+// l = 1: one digit split into two sub-digits (logB <= 24); l = 2: two whole digits (logB <= 15)
+inline uint32_t k2_max_logb(uint32_t level) { return level == 1 ? (uint32_t)K2_MAX_LOGB : level == 2 ? 15u : 0u; }
 constexpr size_t pbs1024k2_lds_bytes() {
   return PBS1024_TABLE_BYTES + 3 * K2_CTS * PBS1024_XCH_SLOTS * 16 + (size_t)K2_RING_SLOTS * 3 * 512 * 16 +
          3 * K2_CTS * 4;  // + per-wave sync counters
@@ -91,8 +93,8 @@ inline bool pbs_small_shape(uint32_t k, uint32_t N, uint32_t level) {
 // GENERIC: pbs_generic.hip, L balanced limbs of `bits` bits for any k <= GEN_MAX_K and
 // N = 256 .. 16384.  The format depends on (k, N, l) only: the runtime's key conversion call
 // carries no base_log (context.h:106-109).
-// K2N1024: pbs1024k2.hip (k = 2, N = 1024, l = 1); SMALL: pbs_small.hip (N = 512, k = 3 and N = 256,
-// k = 5, l = 1).  The values are the ABI's format codes
+// K2N1024: pbs1024k2.hip (k = 2, N = 1024, l = 1 or 2); SMALL: pbs_small.hip (N = 512, k = 3 and
+// N = 256, k = 5 / 6, l = 1).  The values are the ABI's format codes
 // (concrete_hip_bsk_format).
 enum class KeyKind { NONE, N1024, N2048, GENERIC, K2N1024, SMALL };
 struct KeyFormat {
@@ -129,7 +131,7 @@ inline bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_
     // one level whose digit splits into d_lo + 2^16 d_hi (pbs2048.hip)
     case KeyKind::N2048: return base_log >= 1 && base_log <= PBS2_MAX_LOGB;
     case KeyKind::GENERIC: return generic_pbs_ok(k, N, level, base_log);
-    case KeyKind::K2N1024: return base_log >= 1 && base_log <= K2_MAX_LOGB;
+    case KeyKind::K2N1024: return base_log >= 1 && base_log <= k2_max_logb(level);
     case KeyKind::SMALL: return base_log >= 1 && base_log <= pbs_small_max_logb(N);
     default: return false;
   }
@@ -139,7 +141,7 @@ inline bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_
 //   N1024:   [n][col][limb][row*l + q][512] complex f64
 //   N2048:   [n][limb][col][row][parity][512] complex f64 (pbs2048.hip)
 //   GENERIC: [n][col][limb][row][q][N/2] complex f64 (pbs_generic.hip)
-//   K2N1024: [n][limb][col][row][512] complex f64 (pbs1024k2.hip)
+//   K2N1024: [n][limb][col][q][row][512] complex f64 (pbs1024k2.hip; l = 1 or 2)
 //   SMALL:   [n][limb][col][row][N/2] complex f64 (pbs_small.hip)
 inline uint64_t fourier_bsk_bytes(uint32_t n, uint32_t k, uint32_t level, uint32_t N) {
   const KeyFormat f = key_format(k, N, level);

@@ -1,5 +1,6 @@
 // pbs1024k2.hip — batched classic PBS for N = 1024, k = 2, l = 1 (the optimizer's 4-bit rows,
-// v0-parameters: n = 801, logB = 23; bench.py --config opt4) on CDNA4 (gfx950).
+// v0-parameters: n = 801, logB = 23; bench.py --config opt4) and l = 2 at logB <= 15 (its rows at
+// log norm2 >= 1: br 2/15) on CDNA4 (gfx950).
 //
 // Same semantics as pbs.hip (concrete-cpu c_api/bootstrap.rs:347-414 -> tfhe 0.10
 // blind_rotate_assign + sample extract; restated in oracle/tfhe_oracle.c:ora_pbs) and the same
@@ -102,7 +103,10 @@ __device__ __forceinline__ void tri_wait(uint32_t* flags, int ctl, int v, uint32
 
 }  // namespace
 
-template <bool RESID>
+// LEVELS = false: l = 1, the two sub-digits of one digit (d_hi carried into the next slot);
+// LEVELS = true: l = 2 at logB <= 15, the two levels' digits whole (both in the same slot; the key
+// holds both levels, [n][limb][col][q][row][512], one ring group per level).
+template <bool RESID, bool LEVELS>
 __global__ void __launch_bounds__(K2_CTS * 192, 1)
 pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx,
                  const uint64_t* __restrict__ luts, const uint64_t* __restrict__ lut_idx,
@@ -111,8 +115,9 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
                  unsigned long long* __restrict__ resid_out, SyncGuard guard) {
   constexpr int N = 1024, LOG2_2N = 11, K1 = 3;
   constexpr int NW = 3 * K2_CTS;              // waves per workgroup
-  constexpr int GROUP = K1 * 512;             // (limb, column): the three row spectra
-  constexpr int NGRP = K2_LIMBS * K1;         // ring groups per CMUX step
+  constexpr int NQ = LEVELS ? 2 : 1;          // key levels per (limb, column)
+  constexpr int GROUP = K1 * 512;             // (limb, column[, level]): the three row spectra
+  constexpr int NGRP = K2_LIMBS * K1 * NQ;    // ring groups per CMUX step
   constexpr int PER_I = NGRP * GROUP;         // complex values per Fourier GGSW
   constexpr int RS = K2_RING_SLOTS, DIST = K2_RING_SLOTS - 1;
   constexpr int GLDS = GROUP / 64 / NW;       // 1 KB LDS-DMA pieces per wave per group
@@ -193,7 +198,7 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
     }
   }
 
-  const int nrep = 64 - (int)base_log;
+  const int nrep = 64 - NQ * (int)base_log;
   const int logB = (int)base_log;
   double max_resid = 0.0;
 
@@ -232,9 +237,14 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       const int32_t d = decomp_next_t(st[m], logB);
-      const int32_t lo = ((d + (1 << (K2_SUB_BITS - 1))) & ((1 << K2_SUB_BITS) - 1)) - (1 << (K2_SUB_BITS - 1));
-      dlo[m] = lo;
-      dhi[m] = (d - lo) >> K2_SUB_BITS;  // exact: d - lo is a multiple of 2^16
+      if constexpr (LEVELS) {
+        dlo[m] = d;                           // level q = 0 (least significant first)
+        dhi[m] = decomp_next_t(st[m], logB);  // level q = 1
+      } else {
+        const int32_t lo = ((d + (1 << (K2_SUB_BITS - 1))) & ((1 << K2_SUB_BITS) - 1)) - (1 << (K2_SUB_BITS - 1));
+        dlo[m] = lo;
+        dhi[m] = (d - lo) >> K2_SUB_BITS;  // exact: d - lo is a multiple of 2^16
+      }
     }
 #pragma unroll
     for (int sub = 0; sub < K2_SUBS; ++sub) {
@@ -283,72 +293,121 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
       for (int jj = 0; jj < MS; ++jj) Yc[cc][jj] = {0.0, 0.0};
     static_for<0, K2_LIMBS>([&](auto LI) __attribute__((always_inline)) {
       constexpr int li = decltype(LI)::value;
-      constexpr bool HI = li + 1 < K2_LIMBS;  // d_hi g_3 lands at 2^64: vanishes
-      cplx Yn[K1][MS];
-#pragma unroll
-      for (int cc = 0; cc < K1; ++cc)
-#pragma unroll
-        for (int jj = 0; jj < MS; ++jj) Yn[cc][jj] = {0.0, 0.0};
-#pragma unroll
-      for (int cc = 0; cc < K1; ++cc) {
-        const int r = li * K1 + cc;  // group within the step
-        // group r landed for this wave's pieces (the next DIST - 1 may stay in flight) ...
-        if (r + DIST - 1 < NGRP || !last_step) wait_vmcnt<GLDS * (DIST - 1)>();
-        else wait_vmcnt<0>();
-        if (!K2D_NOBAR) pair_barrier();  // ... for every wave; everyone is done with group r - 1
-        // refill the slot of group r - 1 with group r + DIST (RS = DIST + 1)
-        if (r + DIST < NGRP) issue_group(key_step, r + DIST);
-        else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
-        if constexpr (li == 0) {
-          if (cc == 0) {  // the last sub-digit's spectra (see above)
-#pragma unroll
-            for (int row = 0; row < K1; ++row)
-#pragma unroll
-              for (int jj = 0; jj < MS; ++jj)
-                if (has(jj)) X[row][K2_SUBS - 1][jj] = ctx[(K2D_NOXRD ? v : row) * XS + (sb + jj) * 64 + lane];
-          }
-        }
-        cplx Ya[MS];
-#pragma unroll
-        for (int jj = 0; jj < MS; ++jj) Ya[jj] = Yc[cc][jj];
-        const cplx* G = ring + (r % RS) * GROUP + sb * 64 + lane;
-#pragma unroll
-        for (int row = 0; row < K1; ++row) {
-          cplx g[MS];
-#pragma unroll
-          for (int jj = 0; jj < MS; ++jj)
-            if (has(jj)) g[jj] = G[row * 512 + jj * 64];
-#pragma unroll
-          for (int jj = 0; jj < (K2D_NOMAC ? 0 : MS); ++jj) {
-            if (has(jj)) {
-              const cplx x0 = X[row][0][jj];
-              Ya[jj].re = __builtin_fma(x0.re, g[jj].re, __builtin_fma(-x0.im, g[jj].im, Ya[jj].re));
-              Ya[jj].im = __builtin_fma(x0.re, g[jj].im, __builtin_fma(x0.im, g[jj].re, Ya[jj].im));
-              if constexpr (HI) {
-                const cplx x1 = X[row][1][jj];
-                Yn[cc][jj].re = __builtin_fma(x1.re, g[jj].re, __builtin_fma(-x1.im, g[jj].im, Yn[cc][jj].re));
-                Yn[cc][jj].im = __builtin_fma(x1.re, g[jj].im, __builtin_fma(x1.im, g[jj].re, Yn[cc][jj].im));
-              }
-            }
-          }
-        }
-        // column cc of slot li is complete: my slots straight into wave cc's mailbox.  Every
-        // scratch has been idle (for writes of its owner) since this limb's first barrier, and
-        // each wave only ever touches its own slots of a partner's scratch.
-#pragma unroll
-        for (int jj = 0; jj < MS; ++jj)
-          if (has(jj)) ctx[cc * XS + (sb + jj) * 64 + lane] = Ya[jj];
-#pragma unroll
-        for (int jj = 0; jj < MS; ++jj) {
-          pin(Ya[jj]);
-          if constexpr (HI) pin(Yn[cc][jj]);
-        }
-      }
-      if constexpr (HI) {
+      if constexpr (!LEVELS) {
+        constexpr bool HI = li + 1 < K2_LIMBS;  // d_hi g_3 lands at 2^64: vanishes
+        cplx Yn[K1][MS];
 #pragma unroll
         for (int cc = 0; cc < K1; ++cc)
 #pragma unroll
-          for (int jj = 0; jj < MS; ++jj) Yc[cc][jj] = Yn[cc][jj];
+          for (int jj = 0; jj < MS; ++jj) Yn[cc][jj] = {0.0, 0.0};
+#pragma unroll
+        for (int cc = 0; cc < K1; ++cc) {
+          const int r = li * K1 + cc;  // group within the step
+          // group r landed for this wave's pieces (the next DIST - 1 may stay in flight) ...
+          if (r + DIST - 1 < NGRP || !last_step) wait_vmcnt<GLDS * (DIST - 1)>();
+          else wait_vmcnt<0>();
+          if (!K2D_NOBAR) pair_barrier();  // ... for every wave; everyone is done with group r - 1
+          // refill the slot of group r - 1 with group r + DIST (RS = DIST + 1)
+          if (r + DIST < NGRP) issue_group(key_step, r + DIST);
+          else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
+          if constexpr (li == 0) {
+            if (cc == 0) {  // the last sub-digit's spectra (see above)
+#pragma unroll
+              for (int row = 0; row < K1; ++row)
+#pragma unroll
+                for (int jj = 0; jj < MS; ++jj)
+                  if (has(jj)) X[row][K2_SUBS - 1][jj] = ctx[(K2D_NOXRD ? v : row) * XS + (sb + jj) * 64 + lane];
+            }
+          }
+          cplx Ya[MS];
+#pragma unroll
+          for (int jj = 0; jj < MS; ++jj) Ya[jj] = Yc[cc][jj];
+          const cplx* G = ring + (r % RS) * GROUP + sb * 64 + lane;
+#pragma unroll
+          for (int row = 0; row < K1; ++row) {
+            cplx g[MS];
+#pragma unroll
+            for (int jj = 0; jj < MS; ++jj)
+              if (has(jj)) g[jj] = G[row * 512 + jj * 64];
+#pragma unroll
+            for (int jj = 0; jj < (K2D_NOMAC ? 0 : MS); ++jj) {
+              if (has(jj)) {
+                const cplx x0 = X[row][0][jj];
+                Ya[jj].re = __builtin_fma(x0.re, g[jj].re, __builtin_fma(-x0.im, g[jj].im, Ya[jj].re));
+                Ya[jj].im = __builtin_fma(x0.re, g[jj].im, __builtin_fma(x0.im, g[jj].re, Ya[jj].im));
+                if constexpr (HI) {
+                  const cplx x1 = X[row][1][jj];
+                  Yn[cc][jj].re = __builtin_fma(x1.re, g[jj].re, __builtin_fma(-x1.im, g[jj].im, Yn[cc][jj].re));
+                  Yn[cc][jj].im = __builtin_fma(x1.re, g[jj].im, __builtin_fma(x1.im, g[jj].re, Yn[cc][jj].im));
+                }
+              }
+            }
+          }
+          // column cc of slot li is complete: my slots straight into wave cc's mailbox.  Every
+          // scratch has been idle (for writes of its owner) since this limb's first barrier, and
+          // each wave only ever touches its own slots of a partner's scratch.
+#pragma unroll
+          for (int jj = 0; jj < MS; ++jj)
+            if (has(jj)) ctx[cc * XS + (sb + jj) * 64 + lane] = Ya[jj];
+#pragma unroll
+          for (int jj = 0; jj < MS; ++jj) {
+            pin(Ya[jj]);
+            if constexpr (HI) pin(Yn[cc][jj]);
+          }
+        }
+        if constexpr (HI) {
+#pragma unroll
+          for (int cc = 0; cc < K1; ++cc)
+#pragma unroll
+            for (int jj = 0; jj < MS; ++jj) Yc[cc][jj] = Yn[cc][jj];
+        }
+      } else {
+        // l = 2: both levels' products land in slot li, one key window per (column, level)
+#pragma unroll
+        for (int cc = 0; cc < K1; ++cc) {
+          cplx Ya[MS];
+#pragma unroll
+          for (int jj = 0; jj < MS; ++jj) Ya[jj] = {0.0, 0.0};
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            const int r = (li * K1 + cc) * NQ + q;  // group within the step
+            if (r + DIST - 1 < NGRP || !last_step) wait_vmcnt<GLDS * (DIST - 1)>();
+            else wait_vmcnt<0>();
+            if (!K2D_NOBAR) pair_barrier();
+            if (r + DIST < NGRP) issue_group(key_step, r + DIST);
+            else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
+            if constexpr (li == 0) {
+              if (cc == 0 && q == 0) {  // the second level's spectra (published by this barrier)
+#pragma unroll
+                for (int row = 0; row < K1; ++row)
+#pragma unroll
+                  for (int jj = 0; jj < MS; ++jj)
+                    if (has(jj)) X[row][K2_SUBS - 1][jj] = ctx[row * XS + (sb + jj) * 64 + lane];
+              }
+            }
+            const cplx* G = ring + (r % RS) * GROUP + sb * 64 + lane;
+#pragma unroll
+            for (int row = 0; row < K1; ++row) {
+              cplx g[MS];
+#pragma unroll
+              for (int jj = 0; jj < MS; ++jj)
+                if (has(jj)) g[jj] = G[row * 512 + jj * 64];
+#pragma unroll
+              for (int jj = 0; jj < MS; ++jj) {
+                if (has(jj)) {
+                  const cplx x = X[row][q][jj];
+                  Ya[jj].re = __builtin_fma(x.re, g[jj].re, __builtin_fma(-x.im, g[jj].im, Ya[jj].re));
+                  Ya[jj].im = __builtin_fma(x.re, g[jj].im, __builtin_fma(x.im, g[jj].re, Ya[jj].im));
+                }
+              }
+            }
+#pragma unroll
+            for (int jj = 0; jj < MS; ++jj) pin(Ya[jj]);
+          }
+#pragma unroll
+          for (int jj = 0; jj < MS; ++jj)
+            if (has(jj)) ctx[cc * XS + (sb + jj) * 64 + lane] = Ya[jj];
+        }
       }
       cplx V[8];
       tri_sync(tflags, ctl, v, tcnt, guard);
@@ -405,10 +464,10 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
   }
 }
 
-template <bool RESID>
+template <bool RESID, bool LEVELS>
 static int launch_k2_t(const PbsArgs& a) {
   const size_t lds = pbs1024k2_lds_bytes();
-  auto kern = pbs1024k2_kernel<RESID>;
+  auto kern = pbs1024k2_kernel<RESID, LEVELS>;
   CHIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const uint32_t blocks = (a.num_samples + K2_CTS - 1) / K2_CTS;
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(K2_CTS * 192), lds, a.stream, a.out, a.out_idx, a.luts, a.lut_idx,
@@ -423,14 +482,15 @@ static int launch_k2_t(const PbsArgs& a) {
 }
 
 int pbs1024k2_launch(const PbsArgs& a) {
-  if (!(a.N == 1024 && a.k == 2 && a.level == 1 && a.limbs == (uint32_t)K2_LIMBS && a.base_log >= 1 &&
-        a.base_log <= (uint32_t)K2_MAX_LOGB)) {
+  if (!(a.N == 1024 && a.k == 2 && a.limbs == (uint32_t)K2_LIMBS && a.base_log >= 1 &&
+        a.base_log <= k2_max_logb(a.level))) {
     set_error("unsupported PBS parameters: N=%u k=%u level=%u base_log=%u limbs=%u", a.N, a.k, a.level, a.base_log,
               a.limbs);
     return -2;
   }
   if (a.num_samples == 0) return 0;
-  return a.resid ? launch_k2_t<true>(a) : launch_k2_t<false>(a);
+  if (a.level == 2) return a.resid ? launch_k2_t<true, true>(a) : launch_k2_t<false, true>(a);
+  return a.resid ? launch_k2_t<true, false>(a) : launch_k2_t<false, false>(a);
 }
 
 }  // namespace chip

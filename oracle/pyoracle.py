@@ -131,7 +131,7 @@ def gpu2048_error_bound(fbsk_gpu: np.ndarray, logB: int = 23) -> float:
     return float(main + 4.0 * u * max_out)
 
 
-def gpu1024k2_error_bound(fbsk_gpu: np.ndarray, logB: int = 23) -> float:
+def gpu1024k2_error_bound(fbsk_gpu: np.ndarray, logB: int = 23, level: int = 1) -> float:
     """Certified bound on |x - round(x)| for the GPU's k = 2, N = 1024, l = 1 scheme
     (concrete_amd/csrc/pbs1024k2.hip): the N = 1024 products of pbs.hip
     (512-point folded, twisted transforms, log M = 9, correctly rounded tables: mu = u) on the
@@ -145,9 +145,12 @@ def gpu1024k2_error_bound(fbsk_gpu: np.ndarray, logB: int = 23) -> float:
     gamma = logM * eta / (1.0 - logM * eta)
     f = np.asarray(fbsk_gpu, dtype=np.float64).reshape(-1, 2)
     maxG = float(np.max(np.hypot(f[:, 0], f[:, 1]))) * 512.0
-    dlo = 2.0 ** 15
-    dhi = 2.0 ** max(logB - 17, 0) + 1.0
-    dsum = 3.0 * (dlo + dhi)                    # sum over the 6 products of max |digit|
+    if level == 1:
+        dlo = 2.0 ** 15
+        dhi = 2.0 ** max(logB - 17, 0) + 1.0
+        dsum = 3.0 * (dlo + dhi)                # sum over the 6 products of max |digit|
+    else:                                       # l = 2, logB <= 15: two whole digits per row
+        dsum = 3.0 * level * 2.0 ** (logB - 1)
     # forward transform, key rounding, pointwise product and inverse of each product, plus the
     # accumulation additions: (4 gamma + 5 u), as for the N = 2048 products
     main = np.sqrt(1024.0) * dsum * maxG * (4.0 * gamma + 5.0 * u) * 1.0001

@@ -1,5 +1,6 @@
-"""GPU parity tests of the k = 2, N = 1024, l = 1 path (the optimizer's 4-bit rows, v0_last_128:
-n = 801, logB = 23; bench.py --config opt4) — concrete_amd/csrc/pbs1024k2.hip vs the CPU oracle.
+"""GPU parity tests of the k = 2, N = 1024, l = 1 / 2 path (the optimizer's 4-bit rows, v0_last_128:
+n = 801, logB = 23, bench.py --config opt4; and n = 742-754, l = 2, logB = 15 at log norm2 7-13)
+— concrete_amd/csrc/pbs1024k2.hip vs the CPU oracle.
 
 Bit-exact u64 equality with the oracle's pure-integer Karatsuba product on the same keys and
 inputs, the measured rounding residual below the GPU scheme's certified bound
@@ -207,11 +208,13 @@ def test_opt4_full_bit_exact_and_bound(B, oracle, opt4, torch_cuda):
     assert np.array_equal(got[pick], run_oracle(oracle, opt4, cts[pick], acc))
 
 
+@pytest.mark.parametrize("level", [1, 2])
 @pytest.mark.parametrize("n", [1, 2, 3])
-def test_tiny_n(B, oracle, torch_cuda, n):
+def test_tiny_n(B, oracle, torch_cuda, n, level):
     """Blind rotations of 1-3 steps: the key ring's prologue and tail (the last step issues no
     further groups and waits for fewer in flight) meet within one or two steps."""
-    S = Setup(B, oracle, torch_cuda, replace(B.OPTIMIZER_SETS[4], n=n), 8400 + n)
+    p = replace(B.OPTIMIZER_SETS[4], n=n, level=level, base_log=23 if level == 1 else 15)
+    S = Setup(B, oracle, torch_cuda, p, 8400 + 10 * level + n)
     width = 3
     rng = np.random.RandomState(n)
     msgs = rng.randint(0, 8, size=5)
@@ -219,3 +222,61 @@ def test_tiny_n(B, oracle, torch_cuda, n):
     acc = lut_acc(B, S, rng.randint(0, 8, size=8), width)
     got = run_gpu(B, S, cts, acc, torch_cuda)
     assert np.array_equal(got, run_oracle(oracle, S, cts, acc))
+
+
+# ---- l = 2 (the rows at log norm2 7-13: br 2/15, n = 742-754) ------------------------------
+def test_two_level_key_layout(B, oracle, torch_cuda):
+    """Device key [n][limb][col][q][row][slot][lane]: level v = 1 - q of key polynomial (row, col)."""
+    S = Setup(B, oracle, torch_cuda, replace(B.OPTIMIZER_SETS[4], n=4, level=2, base_log=15), 8500)
+    p = S.p
+    assert B.bsk_format(p) == (4, 4, 16)
+    assert B.fourier_bsk_bytes(p) == p.n * 2 * 4 * 9 * 512 * 16
+    got = B.to_host(S.fbsk).view(np.float64).reshape(p.n, 4, 3, 2, 3, 8, 64, 2)
+    bsk = S.bsk.reshape(p.n, 2, 3, 3, 1024)
+    lane = np.arange(64)
+    slot = np.arange(8)
+    K = (lane[None, :] >> 3) + 8 * (lane[None, :] & 7) + 64 * slot[:, None]
+    tw = np.exp(1j * np.pi * np.arange(512) / 1024.0)
+    worst = 0.0
+    for i in (0, p.n - 1):
+        for li in range(4):
+            for col in range(3):
+                for q in range(2):
+                    for row in range(3):
+                        lv = signed_limb(bsk[i, 1 - q, row, col], li)
+                        ref = np.fft.fft((lv[:512] + 1j * lv[512:]) * tw)[K] / 512.0
+                        gg = got[i, li, col, q, row]
+                        worst = max(worst, np.max(np.abs(gg[..., 0] + 1j * gg[..., 1] - ref)) / np.max(np.abs(ref)))
+    assert worst < 1e-13, worst
+
+
+@pytest.mark.parametrize("logB,batch", [(15, 5), (8, 3), (1, 2)])
+def test_two_levels_bit_exact(B, oracle, torch_cuda, logB, batch):
+    S = Setup(B, oracle, torch_cuda, replace(B.OPTIMIZER_SETS[4], n=10, level=2, base_log=logB), 8600 + logB)
+    width = 3
+    rng = np.random.RandomState(logB)
+    msgs = rng.randint(0, 8, size=batch)
+    cts = encrypt(B, S, msgs, width, 70 + logB, std=2.0 ** -30)
+    acc = lut_acc(B, S, rng.randint(0, 8, size=8), width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    assert np.array_equal(got, run_oracle(oracle, S, cts, acc))
+    assert resid < oracle.gpu1024k2_error_bound(B.to_host(S.fbsk).view(np.float64), logB, 2) < 0.5
+
+
+def test_two_levels_full_row(B, oracle, torch_cuda):
+    """v0_last_128's 4-bit row at log norm2 7 (k = 2, N = 1024, n = 742, br 2/15): 256 samples
+    decrypted, 2 bit-exact vs the exact oracle, residual under the certified bound."""
+    S = Setup(B, oracle, torch_cuda, B.PbsParams(n=742, k=2, N=1024, level=2, base_log=15, ks_level=3,
+                                                ks_base_log=4), 8700)
+    width = 4
+    rng = np.random.RandomState(7)
+    table = rng.randint(0, 16, size=16)
+    msgs = rng.randint(0, 16, size=256)
+    cts = encrypt(B, S, msgs, width, 99)
+    acc = lut_acc(B, S, table, width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    bound = oracle.gpu1024k2_error_bound(B.to_host(S.fbsk).view(np.float64), 15, 2)
+    assert resid < bound < 0.5, (resid, bound)
+    dec = B.lwe_decrypt(S.glwe_sk, got, S.p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+    assert np.array_equal(got[:2], run_oracle(oracle, S, cts[:2], acc))

@@ -43,7 +43,7 @@ CASES = [
     # shapes off the tile kernels' instances (T = 1): k = 3, N = 512 at logB = 12 (the small-ring
     # kernel's one-sub-digit form since round 4) and the two-launch path at N = 1024
     ("k3_N512_logB12_small", 3, 512, 12, 1, 12, 3),
-    ("k2_N1024_l2_two_launch", 2, 1024, 10, 2, 10, 3),
+    ("k2_N1024_l2", 2, 1024, 10, 2, 10, 3),  # the k = 2 kernel's two-level form since round 4
     # four-step kernel with a 64-bit decomposition state (level * logB > 31): R = 4, 8, 16 rows
     ("k1_N4096_l3_wide_state", 1, 4096, 4, 3, 12, 3),
     ("k1_N8192_l2_wide_state", 1, 8192, 3, 2, 17, 4),
@@ -52,11 +52,13 @@ CASES = [
     # S = 2 / 4 workgroups (gen_split_*_kernel), the key converted the same way
     ("9bit_k1_N32768", 1, 32768, 2, 2, 15, 9),
     ("10bit_k1_N65536", 1, 65536, 2, 2, 14, 10),
-    # round 4: the 1- to 4-bit rows above run on their own kernels (pbs_small.hip, pbs1024k2.hip);
-    # these keep the one-launch tile kernels at N = 256 / 512 under test
-    ("3bit_k4_N512_tile", 4, 512, 14, 1, 23, 3),
-    ("2bit_k5_N256_l2_tile", 5, 256, 16, 2, 10, 2),
-    ("1bit_k6_N256_l2_tile", 6, 256, 12, 2, 12, 1),
+    # round 4: the 1- to 4-bit log-norm2-0 rows above run on their own kernels (pbs_small.hip,
+    # pbs1024k2.hip); these small-ring rows at log norm2 > 0 stay on the general path (its
+    # two-launch kernels: the tile kernels serve the general-format key of the three shapes above,
+    # test_generic_tile_kernels_on_the_general_format_key)
+    ("3bit_k4_N512", 4, 512, 14, 1, 23, 3),
+    ("2bit_k5_N256_l2", 5, 256, 16, 2, 10, 2),
+    ("1bit_k6_N256_l2", 6, 256, 12, 2, 12, 1),
 ]
 
 
@@ -97,8 +99,8 @@ def test_generic_pbs_bit_exact(B, oracle, torch_cuda, case):
     ref, _ = oracle.pbs_batch(op, cts, acc[None, :], bsk=bsk, mode=oracle.MODE_KARATSUBA)
     assert np.array_equal(got, ref), f"{case[0]}: GPU differs from the exact oracle"
     kind, limbs, bits = B.bsk_format(p)
-    if kind == 4:  # k = 2, N = 1024, l = 1: its own kernel since round 4 (test_gpu_pbs1024k2.py)
-        bound = oracle.gpu1024k2_error_bound(B.to_host(fbsk).view(np.float64), p.base_log)
+    if kind == 4:  # k = 2, N = 1024, l = 1 / 2: its own kernel since round 4 (test_gpu_pbs1024k2.py)
+        bound = oracle.gpu1024k2_error_bound(B.to_host(fbsk).view(np.float64), p.base_log, p.level)
     elif kind == 5:  # N = 512, k = 3 / N = 256, k = 5, l = 1: pbs_small.hip (test_gpu_pbs_small.py)
         bound = oracle.gpu_small_error_bound(B.to_host(fbsk).view(np.float64), p.N, p.k, p.base_log)
     else:
@@ -112,9 +114,9 @@ def test_generic_pbs_bit_exact(B, oracle, torch_cuda, case):
 
 @pytest.mark.parametrize("ci", [17, 15, 16, 5], ids=[CASES[i][0] for i in (17, 15, 16, 5)])
 def test_generic_tile_many_workgroups(B, oracle, torch_cuda, ci):
-    """The one-launch tile kernels over many workgroups (67 ciphertexts: not a multiple of any
-    tile size, so the last workgroup runs empty groups) and the one-launch N = 4096 kernel (a
-    workgroup per ciphertext), bit-exact vs the exact oracle."""
+    """The general path over many ciphertexts (67: not a multiple of any workgroup's ciphertext
+    count, so the last workgroup runs empty slots): the small-ring rows at log norm2 > 0 and the
+    one-launch N = 4096 kernel (a workgroup per ciphertext), bit-exact vs the exact oracle."""
     case = CASES[ci][:3] + (4,) + CASES[ci][4:]
     p, glwe_sk, bsk, fbsk, cts, acc, table, msgs, got, resid = run_case(B, oracle, torch_cuda, case, 7500, batch=67)
     op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
@@ -389,3 +391,36 @@ def test_optimizer_rows_at_nonzero_log_norm2(B, oracle, torch_cuda, case):
     torch_cuda.cuda.synchronize()
     opk = oracle.Params(n=n_full, k=1, N=kN, l=l, logB=logB, ks_l=ks_l, ks_logB=ks_logB)
     assert np.array_equal(B.to_host(out), oracle.keyswitch_batch(opk, big, ksk))
+
+
+@pytest.mark.parametrize("ci", [0, 2, 3], ids=[CASES[i][0] for i in (0, 2, 3)])
+def test_generic_tile_kernels_on_the_general_format_key(B, oracle, torch_cuda, ci):
+    """The one-launch tile kernels (gen_tile_kernel) run the log-norm2-0 shapes of N = 256 / 512 /
+    1024 on the general-format key (concrete_hip_convert_bsk_generic + concrete_hip_pbs_generic:
+    a caller-converted key, or the companion key of a wide-digit call), 67 ciphertexts; bit-exact
+    vs the exact oracle."""
+    from concrete_amd import _native
+    label, k, N, n, l, logB, width = CASES[ci]
+    L = _native.lib()
+    p = B.PbsParams(n=4, k=k, N=N, level=l, base_log=logB)
+    lwe_sk, glwe_sk = B.binary_key(p.n, 7800), B.binary_key(p.big_n, 7801)
+    bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 7802)
+    rng = np.random.RandomState(ci)
+    table = rng.randint(0, 1 << width, size=1 << width).astype(np.uint64)
+    msgs = rng.randint(0, 1 << width, size=67)
+    cts = B.lwe_encrypt(lwe_sk, [B.encode(m, width) for m in msgs], p.n, 2.0 ** -30, 7803)
+    acc = B.trivial_glwe(p, B.expand_lut(table, p.N, width))
+    dev = "cuda:0"
+    g = torch_cuda.empty(L.concrete_hip_generic_bsk_size_bytes(p.n, p.k, p.level, p.N) // 8, dtype=torch_cuda.int64,
+                         device=dev)
+    st, gi = B._stream(torch_cuda.device(dev)), B._gpu_index(torch_cuda.device(dev))
+    _native.check(L.concrete_hip_convert_bsk_generic(st, gi, B._ptr(g), bsk.ctypes.data, 0, p.n, p.k, p.level, p.N),
+                  "convert_bsk_generic")
+    d_in, d_acc = B.to_device(cts, dev), B.to_device(acc[None, :], dev)
+    out = torch_cuda.zeros((67, p.lwe_out_size), dtype=torch_cuda.int64, device=dev)
+    _native.check(L.concrete_hip_pbs_generic(st, gi, B._ptr(out), None, B._ptr(d_acc), None, B._ptr(d_in), None,
+                                             B._ptr(g), p.n, p.k, p.N, p.base_log, p.level, 67, None), "pbs_generic")
+    torch_cuda.cuda.synchronize()
+    op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
+    ref, _ = oracle.pbs_batch(op, cts, acc[None, :], bsk=bsk, mode=oracle.MODE_KARATSUBA)
+    assert np.array_equal(B.to_host(out), ref)

@@ -110,7 +110,8 @@ def test_key_formats_and_exact_range():
     assert L.concrete_hip_generic_bsk_size_bytes(10, 1, 1, 131072) == 0
     # the optimizer's 4-bit rows (k = 2, N = 1024, l = 1): their own kernel (pbs1024k2.hip, round 4),
     # 4 limbs of 16 bits, the digit split on the limb grid as at N = 2048
-    assert fmt(2, 1024, 1) == (4, 4, 16)
+    assert fmt(2, 1024, 1) == (4, 4, 16) and fmt(2, 1024, 2) == (4, 4, 16)
+    assert L.concrete_hip_pbs_supported(2, 1024, 2, 15) == 1  # two levels: whole digits up to 15 bits
     assert L.concrete_hip_fourier_bsk_size_bytes(801, 2, 1, 1024) == 801 * 4 * 9 * 512 * 16
     assert L.concrete_hip_pbs_supported(2, 1024, 1, 24) == 1
     assert L.concrete_hip_generic_error_bound(2, 1024, 1, 23, 0.0) == -1.0
@@ -120,7 +121,7 @@ def test_key_formats_and_exact_range():
     assert L.concrete_hip_fourier_bsk_size_bytes(722, 3, 1, 512) == 722 * 4 * 16 * 256 * 16
     assert L.concrete_hip_pbs_supported(3, 512, 1, 24) == 1 and L.concrete_hip_pbs_supported(5, 256, 1, 15) == 1
     assert L.concrete_hip_pbs_supported(5, 256, 1, 25) == 1  # past the small-ring gate: the general path
-    for k, N, l, logB in [(6, 256, 2, 12), (4, 512, 1, 23), (2, 1024, 2, 15), (1, 4096, 1, 22),
+    for k, N, l, logB in [(6, 256, 2, 12), (4, 512, 1, 23), (2, 1024, 3, 12), (1, 4096, 1, 22),
                           (1, 8192, 1, 22), (1, 16384, 2, 15), (1, 2048, 2, 10)]:
         kind, limbs, bits = fmt(k, N, l)
         assert kind == 3 and limbs * bits >= 64, (k, N, l)

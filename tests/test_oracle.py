@@ -361,7 +361,7 @@ def test_generic_error_bound_matches_the_kernel_gate(oracle):
 
     from concrete_amd import _native
     L = _native.lib()
-    for k, N, l, logB in [(6, 256, 2, 12), (4, 512, 1, 23), (2, 1024, 2, 15), (1, 4096, 1, 22), (1, 16384, 2, 15),
+    for k, N, l, logB in [(6, 256, 2, 12), (4, 512, 1, 23), (2, 1024, 3, 12), (1, 4096, 1, 22), (1, 16384, 2, 15),
                           (4, 512, 3, 12), (1, 2048, 2, 10)]:
         limbs, bits = C.c_uint32(), C.c_uint32()
         assert L.concrete_hip_bsk_format(k, N, l, C.byref(limbs), C.byref(bits)) == 3

@@ -240,22 +240,35 @@ __global__ void __launch_bounds__(256) convert_bsk1024k2_kernel(cplx* __restrict
   dd_fft_scatter<M>(buf, tw_t, [&](int e) { return dest + blk * M + e; });
 }
 
-// N = 512, k = 3 / N = 256, k = 5, 6, l = 1 (pbs_small.hip).  Block = (i, limb, col, row) in the order of
-// the output layout [n][limb][col][row][N/2]: limb `limb` of key polynomial (row, col), folded,
-// twisted by zeta_2N^j and transformed (M = N / 2 points), scaled 1 / (512 P) with P = 1024 / N (the
-// kernel's unnormalised unzip and zip), element e = (slot, lane) at frequency fft512_freq(lane, slot).
+// N = 512, k = 3 / N = 256, k = 5, 6, l <= 3 (pbs_small.hip) and N = 512, k = 4, l = 1, 3 .. 5
+// (pbs512k4.hip).  Block = (i, limb, cg, q, c2, row) in the order of the output layout
+// [n][limb][cg][q][c2][row][N/2] (a key group: one limb, one level, GC = sm_gc(N, K1) output columns
+// col = cg GC + c2): limb `limb` of key polynomial (row, col) of level v = l - 1 - q (q in digit
+// order), folded, twisted by zeta_2N^j and transformed (M = N / 2 points), scaled 1 / (512 P) with
+// P = 1024 / N (the kernels' unnormalised unzip and zip), element e = (slot, lane) at frequency
+// fft512_freq(lane, slot).
 template <int N, int K1>
 __global__ void __launch_bounds__(256) convert_bsk_small_kernel(cplx* __restrict__ dest,
                                                                const uint64_t* __restrict__ src,
                                                                const ddc* __restrict__ zeta_t,
-                                                               const ddc* __restrict__ tw_t) {
+                                                               const ddc* __restrict__ tw_t, uint32_t level) {
   constexpr int M = N / 2, LOGM = N == 512 ? 8 : 7, P = 1024 / N;
+  constexpr int GC = sm_gc(N, K1), NCG = K1 / GC;
   __shared__ ddc buf[M];
   const uint64_t blk = blockIdx.x;
-  const uint32_t row = (uint32_t)(blk % K1), col = (uint32_t)((blk / K1) % K1);
-  const uint32_t limb = (uint32_t)((blk / (K1 * K1)) % SM_LIMBS);
-  const uint64_t i = blk / (K1 * K1 * SM_LIMBS);
-  const uint64_t* g = src + ((i * K1 + row) * K1 + col) * N;  // [n][l = 1][row][col][N]
+  uint64_t t = blk;
+  const uint32_t row = (uint32_t)(t % K1);
+  t /= K1;
+  const uint32_t c2 = (uint32_t)(t % GC);
+  t /= GC;
+  const uint32_t q = (uint32_t)(t % level);
+  t /= level;
+  const uint32_t cg = (uint32_t)(t % NCG);
+  t /= NCG;
+  const uint32_t limb = (uint32_t)(t % SM_LIMBS);
+  const uint64_t i = t / SM_LIMBS;
+  const uint32_t col = cg * GC + c2, v = level - 1 - q;
+  const uint64_t* g = src + (((i * level + v) * K1 + row) * K1 + col) * N;  // [n][l][row][col][N]
   for (int j = threadIdx.x; j < M; j += blockDim.x) {
     ddc z{dd_from(limb_value<SM_LIMBS>(g[j], limb)), dd_from(limb_value<SM_LIMBS>(g[j + M], limb))};
     z = ddc_mul(z, zeta_t[j]);
@@ -355,16 +368,19 @@ int convert_bsk_launch(const ConvertArgs& a) {
       rc = -1;
     }
   } else if (small) {
-    const uint64_t blocks = (uint64_t)a.n * SM_LIMBS * (a.k + 1) * (a.k + 1);
-    if (a.N == 512)
+    const uint64_t blocks = (uint64_t)a.n * SM_LIMBS * (a.k + 1) * (a.k + 1) * a.level;
+    if (a.N == 512 && a.k == 3)
       hipLaunchKernelGGL((convert_bsk_small_kernel<512, 4>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
-                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt);
+                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level);
+    else if (a.N == 512)
+      hipLaunchKernelGGL((convert_bsk_small_kernel<512, 5>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
+                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level);
     else if (a.k == 5)
       hipLaunchKernelGGL((convert_bsk_small_kernel<256, 6>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
-                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt);
+                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level);
     else
       hipLaunchKernelGGL((convert_bsk_small_kernel<256, 7>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
-                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt);
+                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       set_error("convert launch failed: %s", hipGetErrorString(e));

@@ -22,7 +22,7 @@ inline bool pbs_needs_generic_key(uint32_t k, uint32_t N, uint32_t level, uint32
     return generic_pbs_ok(k, N, level, base_log);
   if (f.kind == KeyKind::K2N1024 && !(base_log >= 1 && base_log <= k2_max_logb(level)))
     return generic_pbs_ok(k, N, level, base_log);
-  if (f.kind == KeyKind::SMALL && !(base_log >= 1 && base_log <= pbs_small_max_logb(N)))
+  if (f.kind == KeyKind::SMALL && !pbs_small_ok(k, N, level, base_log))
     return generic_pbs_ok(k, N, level, base_log);
   return false;
 }

@@ -64,12 +64,15 @@ constexpr size_t pbs1024k2_lds_bytes() {
          3 * K2_CTS * 4;  // + per-wave sync counters
 }
 
-// N = 512, k = 3 and N = 256, k = 5 / 6, l = 1 (pbs_small.hip): P = 1024 / N polynomials per register
+// N = 512, k = 3 and N = 256, k = 5 / 6, l <= 3 (pbs_small.hip): P = 1024 / N polynomials per register
 // fft512, two waves per ciphertext, SM_CTS ciphertexts per workgroup, a ring of key groups (one limb
 // and one output column: the k + 1 row spectra).  Key: 4 balanced 16-bit limbs, scaled 1 / (512 P).
 constexpr int SM_CTS = 4;
 constexpr int SM_LIMBS = 4;
 constexpr int SM_SUB_BITS = 16;
+// l = 2, 3: whole digits (l 2^(logB-1) <= 2^15, the l = 1, logB = 16 magnitude), the levels' products
+// summed into the same slot (the optimizer's rows at br 2/10, 2/12, 3/9)
+constexpr uint32_t SM_MAX_LEVEL = 3;
 // largest digit: the certified bound (oracle/pyoracle.py:gpu_small_error_bound) on random keys of
 // the table rows' size is 0.28 at N = 512, k = 3 and 0.34 / 0.39 at N = 256, k = 5 / 6 for any
 // logB <= 24 (0.17 / 0.19 with one sub-digit, logB <= 15); wider digits run on the general path
@@ -85,8 +88,27 @@ constexpr size_t pbs_small_lds_bytes(int N, int K1) {
   return PBS1024_TABLE_BYTES + 2 * SM_CTS * PBS1024_XCH_SLOTS * 16 +
          (size_t)sm_rs(N, K1) * sm_gc(N, K1) * K1 * (N / 2) * 16 + 2 * SM_CTS * 4;
 }
+// N = 512, k = 4 (pbs512k4.hip): the same key format and packing; five polynomials make three packed
+// transforms: four waves per ciphertext (three transform owners, one slot each), K4_CTS ciphertexts per
+// workgroup and a ring of K4_RING_SLOTS 20 KB key groups.  l = 1 (logB <= 24) or l = 3 .. K4_MAX_LEVEL
+// whole digits with l 2^(logB-1) <= 2^15 (the l = 1, logB = 16 magnitude: certified bound 0.35).  Not
+// l = 2: the optimizer's k = 4, N = 512, l = 2 rows have logB = 16 (bound 0.69), and the key format
+// depends on (k, N, l) only, so that shape keeps the general path's format.
+constexpr int K4_CTS = 2;
+constexpr int K4_RING_SLOTS = 4;
+constexpr uint32_t K4_MAX_LEVEL = 5;
+constexpr size_t pbs512k4_lds_bytes() {
+  return PBS1024_TABLE_BYTES + 3 * K4_CTS * PBS1024_XCH_SLOTS * 16 + (size_t)K4_RING_SLOTS * 5 * 256 * 16 +
+         3 * K4_CTS * 4;
+}
 inline bool pbs_small_shape(uint32_t k, uint32_t N, uint32_t level) {
-  return level == 1 && ((N == 512 && k == 3) || (N == 256 && (k == 5 || k == 6)));
+  if (N == 512 && k == 4) return level == 1 || (level >= 3 && level <= K4_MAX_LEVEL);
+  return level >= 1 && level <= SM_MAX_LEVEL && ((N == 512 && k == 3) || (N == 256 && (k == 5 || k == 6)));
+}
+inline bool pbs_small_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
+  if (!pbs_small_shape(k, N, level) || base_log < 1) return false;
+  if (level == 1) return base_log <= pbs_small_max_logb(N);
+  return base_log <= 15 && ((uint64_t)level << (base_log - 1)) <= (1ull << 15);
 }
 
 // Device key formats.  N1024 / N2048: the hand-tuned kernels' layouts (pbs.hip, pbs2048.hip);
@@ -94,7 +116,7 @@ inline bool pbs_small_shape(uint32_t k, uint32_t N, uint32_t level) {
 // N = 256 .. 16384.  The format depends on (k, N, l) only: the runtime's key conversion call
 // carries no base_log (context.h:106-109).
 // K2N1024: pbs1024k2.hip (k = 2, N = 1024, l = 1 or 2); SMALL: pbs_small.hip (N = 512, k = 3 and
-// N = 256, k = 5 / 6, l = 1).  The values are the ABI's format codes
+// N = 256, k = 5 / 6, l <= 3) and pbs512k4.hip (N = 512, k = 4, l = 1, 3 .. 5).  The values are the ABI's format codes
 // (concrete_hip_bsk_format).
 enum class KeyKind { NONE, N1024, N2048, GENERIC, K2N1024, SMALL };
 struct KeyFormat {
@@ -132,7 +154,7 @@ inline bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_
     case KeyKind::N2048: return base_log >= 1 && base_log <= PBS2_MAX_LOGB;
     case KeyKind::GENERIC: return generic_pbs_ok(k, N, level, base_log);
     case KeyKind::K2N1024: return base_log >= 1 && base_log <= k2_max_logb(level);
-    case KeyKind::SMALL: return base_log >= 1 && base_log <= pbs_small_max_logb(N);
+    case KeyKind::SMALL: return pbs_small_ok(k, N, level, base_log);
     default: return false;
   }
 }
@@ -142,7 +164,8 @@ inline bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_
 //   N2048:   [n][limb][col][row][parity][512] complex f64 (pbs2048.hip)
 //   GENERIC: [n][col][limb][row][q][N/2] complex f64 (pbs_generic.hip)
 //   K2N1024: [n][limb][col][q][row][512] complex f64 (pbs1024k2.hip; l = 1 or 2)
-//   SMALL:   [n][limb][col][row][N/2] complex f64 (pbs_small.hip)
+//   SMALL:   [n][limb][cg][q][c2][row][N/2] complex f64, col = cg GC + c2 (pbs_small.hip, pbs512k4.hip;
+//            GC = sm_gc(N, k + 1))
 inline uint64_t fourier_bsk_bytes(uint32_t n, uint32_t k, uint32_t level, uint32_t N) {
   const KeyFormat f = key_format(k, N, level);
   switch (f.kind) {
@@ -175,6 +198,7 @@ int pbs1024_quad_launch(const PbsArgs& a, int cts);  // pbs1024_quad.hip (cts = 
 int pbs_generic_launch(const PbsArgs& a);     // pbs_generic.hip
 int pbs1024k2_launch(const PbsArgs& a);       // pbs1024k2.hip
 int pbs_small_launch(const PbsArgs& a);       // pbs_small.hip
+int pbs512k4_launch(const PbsArgs& a);        // pbs512k4.hip
 
 struct ConvertArgs {
   hipStream_t stream;

@@ -29,6 +29,8 @@
 #include "kernel_util.hpp"
 #include "pbs.hpp"
 
+#include <type_traits>
+
 // Diagnostic builds only (timing; wrong results): SMD_NOMAC / SMD_NOINV / SMD_NOFWD drop the key
 // products / inverse transforms / forward transforms, SMD_NOZIP the unzip and zip.
 #ifndef SMD_NOMAC
@@ -93,7 +95,10 @@ __device__ __forceinline__ void dftp(cplx (&x)[P], bool inverse) {
 
 }  // namespace
 
-template <int N, int K1, int SUBS, bool RESID>
+// SUBS = 2, NQ = 1: one digit split into d_lo + 2^16 d_hi (16 < logB <= 24); SUBS = 1: NQ = l whole
+// digits (l = 2, 3 with l 2^(logB-1) <= 2^15), each level's products landing in the same slot (the
+// key holds the levels, [n][limb][cg][q][c2][row][M], one ring group per level).
+template <int N, int K1, int SUBS, int NQ, bool RESID>
 __global__ void __launch_bounds__(SM_CTS * 128, 1)
 pbs_small_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx,
                  const uint64_t* __restrict__ luts, const uint64_t* __restrict__ lut_idx,
@@ -112,7 +117,10 @@ pbs_small_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
   constexpr int GROUP = GC * K1 * M;        // (limb, GC columns): their K1 row spectra each
   constexpr int NCG = K1 / GC;              // column groups per limb
   static_assert(K1 % GC == 0, "column groups");
-  constexpr int NGRP = SM_LIMBS * NCG;
+  constexpr int NGRP = SM_LIMBS * NCG * NQ;
+  constexpr int NF = SUBS * NQ;             // forward transforms per step (sub-digits or levels)
+  static_assert(SUBS == 1 || NQ == 1, "sub-digits or levels");
+  using StT = std::conditional_t<(NQ > 1), uint64_t, uint32_t>;  // decomposition state (l logB bits)
   constexpr int PER_I = NGRP * GROUP;
   constexpr int RS = sm_rs(N, K1), DIST = RS - 1;
   constexpr int PB = (GROUP * 16) % (NW * 1024) == 0 ? 16 : 4;  // LDS-DMA bytes per lane
@@ -195,7 +203,7 @@ pbs_small_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
     }
   }
 
-  const int nrep = 64 - (int)base_log;
+  const int nrep = 64 - NQ * (int)base_log;
   const int logB = (int)base_log;
   double max_resid = 0.0;
 
@@ -208,7 +216,7 @@ pbs_small_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
     const uint32_t at = modswitch(ai, LOG2_2N);
 
     // ---- ct1 = X^{at} acc - acc in my own scratch (P polynomials of N u64) ---------------
-    uint32_t st[16];
+    StT st[16];
     {
 #pragma unroll
       for (int m = 0; m < 16; ++m) xch64[pl * N + jb + (64 / P) * (m & 7) + (m >= 8 ? M : 0)] = A[m];
@@ -224,31 +232,34 @@ pbs_small_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
       for (int m = 0; m < 16; ++m) {
         const int c = jb + (64 / P) * (m & 7) + (m >= 8 ? M : 0);
         const uint32_t sp = (uint32_t)(c - (int)at) & (2 * N - 1);
-        st[m] = (uint32_t)decomp_init((sp < N ? rv[m] : 0ull - rv[m]) - A[m], nrep);
+        st[m] = (StT)decomp_init((sp < N ? rv[m] : 0ull - rv[m]) - A[m], nrep);
       }
       wave_lds_fence();
     }
 
-    // ---- digits and forward transforms; X[row][sub][js]: row's spectrum at slot sv + js -----
-    cplx X[K1][SUBS][MS];
-    int32_t dd[SUBS][16];
+    // ---- digits and forward transforms; X[row][f][js]: row's spectrum of digit polynomial f
+    //      (sub-digit or level) at slot sv + js
+    cplx X[K1][NF][MS];
+    int32_t dd[SUBS][16];  // SUBS = 2: both sub-digits; else the current level's digits
+    if constexpr (SUBS == 2) {
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      const int32_t d = decomp_next_t(st[m], logB);
-      if constexpr (SUBS == 1) {
-        dd[0][m] = d;
-      } else {
+      for (int m = 0; m < 16; ++m) {
+        const int32_t d = decomp_next_t(st[m], logB);
         const int32_t lo = ((d + (1 << (SM_SUB_BITS - 1))) & ((1 << SM_SUB_BITS) - 1)) - (1 << (SM_SUB_BITS - 1));
         dd[0][m] = lo;
-        dd[SUBS - 1][m] = (d - lo) >> SM_SUB_BITS;
+        dd[1][m] = (d - lo) >> SM_SUB_BITS;
       }
     }
 #pragma unroll
-    for (int sub = 0; sub < SUBS; ++sub) {
+    for (int sub = 0; sub < NF; ++sub) {
       {
+        if constexpr (SUBS == 1) {
+#pragma unroll
+          for (int m = 0; m < 16; ++m) dd[0][m] = decomp_next_t(st[m], logB);  // level q = sub
+        }
         cplx vv[8];
 #pragma unroll
-        for (int m = 0; m < 8; ++m) vv[m] = {(double)dd[sub][m], (double)dd[sub][m + 8]};
+        for (int m = 0; m < 8; ++m) vv[m] = {(double)dd[SUBS == 2 ? sub : 0][m], (double)dd[SUBS == 2 ? sub : 0][m + 8]};
         cplx tw2[4], tw3[4];
         fwd_p2_tw(tw2, T, lane >> 3);
         fwd_p3_tw(tw3, T, lane);
@@ -268,8 +279,8 @@ pbs_small_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
             xch[(p * SL + sl) * 64 + lane] = p == 0 || SMD_NOZIP ? y[p] : cmulc(y[p], tz[p][sl]);
         }
       }
-      // the last sub-digit's spectra are published by the first key window's barrier
-      if (sub + 1 < SUBS) {
+      // the last digit polynomial's spectra are published by the first key window's barrier
+      if (sub + 1 < NF) {
         sm_sync(sflags, ctl, v, scnt, guard);
 #pragma unroll
         for (int row = 0; row < K1; ++row)
@@ -292,72 +303,129 @@ pbs_small_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
       for (int js = 0; js < MS; ++js) Yc[cc][js] = {0.0, 0.0};
     static_for<0, SM_LIMBS>([&](auto LI) __attribute__((always_inline)) {
       constexpr int li = decltype(LI)::value;
-      constexpr bool HI = SUBS == 2 && li + 1 < SM_LIMBS;
-      cplx Yn[K1][MS];
-#pragma unroll
-      for (int cc = 0; cc < K1; ++cc)
-#pragma unroll
-        for (int js = 0; js < MS; ++js) Yn[cc][js] = {0.0, 0.0};
-#pragma unroll
-      for (int cg = 0; cg < NCG; ++cg) {
-        const int r = li * NCG + cg;
-        static_assert(DIST <= 3, "vmcnt tail cases");
-        if (r + DIST - 1 < NGRP || !last_step) wait_vmcnt<GLDS * (DIST - 1)>();
-        else if (r + 1 == NGRP) wait_vmcnt<0>();
-        else if (r + 2 == NGRP) wait_vmcnt<GLDS>();
-        else wait_vmcnt<GLDS * 2>();
-        pair_barrier();
-        if (r + DIST < NGRP) issue_group(key_step, r + DIST);
-        else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
-        if constexpr (li == 0) {
-          if (cg == 0) {
-#pragma unroll
-            for (int row = 0; row < K1; ++row)
-#pragma unroll
-              for (int js = 0; js < MS; ++js)
-                X[row][SUBS - 1][js] = ctx[(row / P) * XS + ((row % P) * SL + sv + js) * 64 + lane];
-          }
-        }
-#pragma unroll
-      for (int c2 = 0; c2 < GC; ++c2) {
-        const int cc = cg * GC + c2;
-        cplx Ya[MS];
-#pragma unroll
-        for (int js = 0; js < MS; ++js) Ya[js] = Yc[cc][js];
-        const cplx* G = ring + (r % RS) * GROUP + c2 * K1 * M + sv * 64 + lane;
-#pragma unroll
-        for (int row = 0; row < K1; ++row) {
-          cplx g[MS];
-#pragma unroll
-          for (int js = 0; js < MS; ++js) g[js] = G[row * M + js * 64];
-#pragma unroll
-          for (int js = 0; js < (SMD_NOMAC ? 0 : MS); ++js) {
-            const cplx x0 = X[row][0][js];
-            Ya[js].re = __builtin_fma(x0.re, g[js].re, __builtin_fma(-x0.im, g[js].im, Ya[js].re));
-            Ya[js].im = __builtin_fma(x0.re, g[js].im, __builtin_fma(x0.im, g[js].re, Ya[js].im));
-            if constexpr (HI) {
-              const cplx x1 = X[row][SUBS - 1][js];
-              Yn[cc][js].re = __builtin_fma(x1.re, g[js].re, __builtin_fma(-x1.im, g[js].im, Yn[cc][js].re));
-              Yn[cc][js].im = __builtin_fma(x1.re, g[js].im, __builtin_fma(x1.im, g[js].re, Yn[cc][js].im));
-            }
-          }
-        }
-        // column cc of slot li: my slots into its owner's mailbox (each wave only ever touches its
-        // own slots of a partner's scratch; the owner reads it behind the limb's pair sync)
-#pragma unroll
-        for (int js = 0; js < MS; ++js) ctx[(cc / P) * XS + ((cc % P) * SL + sv + js) * 64 + lane] = Ya[js];
-#pragma unroll
-        for (int js = 0; js < MS; ++js) {
-          pin(Ya[js]);
-          if constexpr (HI) pin(Yn[cc][js]);
-        }
-      }
-      }
-      if constexpr (HI) {
+      if constexpr (NQ == 1) {
+        constexpr bool HI = SUBS == 2 && li + 1 < SM_LIMBS;
+        cplx Yn[K1][MS];
 #pragma unroll
         for (int cc = 0; cc < K1; ++cc)
 #pragma unroll
-          for (int js = 0; js < MS; ++js) Yc[cc][js] = Yn[cc][js];
+          for (int js = 0; js < MS; ++js) Yn[cc][js] = {0.0, 0.0};
+#pragma unroll
+        for (int cg = 0; cg < NCG; ++cg) {
+          const int r = li * NCG + cg;
+          static_assert(DIST <= 3, "vmcnt tail cases");
+          if (r + DIST - 1 < NGRP || !last_step) wait_vmcnt<GLDS * (DIST - 1)>();
+          else if (r + 1 == NGRP) wait_vmcnt<0>();
+          else if (r + 2 == NGRP) wait_vmcnt<GLDS>();
+          else wait_vmcnt<GLDS * 2>();
+          pair_barrier();
+          if (r + DIST < NGRP) issue_group(key_step, r + DIST);
+          else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
+          if constexpr (li == 0) {
+            if (cg == 0) {
+#pragma unroll
+              for (int row = 0; row < K1; ++row)
+#pragma unroll
+                for (int js = 0; js < MS; ++js)
+                  X[row][SUBS - 1][js] = ctx[(row / P) * XS + ((row % P) * SL + sv + js) * 64 + lane];
+            }
+          }
+#pragma unroll
+        for (int c2 = 0; c2 < GC; ++c2) {
+          const int cc = cg * GC + c2;
+          cplx Ya[MS];
+#pragma unroll
+          for (int js = 0; js < MS; ++js) Ya[js] = Yc[cc][js];
+          const cplx* G = ring + (r % RS) * GROUP + c2 * K1 * M + sv * 64 + lane;
+#pragma unroll
+          for (int row = 0; row < K1; ++row) {
+            cplx g[MS];
+#pragma unroll
+            for (int js = 0; js < MS; ++js) g[js] = G[row * M + js * 64];
+#pragma unroll
+            for (int js = 0; js < (SMD_NOMAC ? 0 : MS); ++js) {
+              const cplx x0 = X[row][0][js];
+              Ya[js].re = __builtin_fma(x0.re, g[js].re, __builtin_fma(-x0.im, g[js].im, Ya[js].re));
+              Ya[js].im = __builtin_fma(x0.re, g[js].im, __builtin_fma(x0.im, g[js].re, Ya[js].im));
+              if constexpr (HI) {
+                const cplx x1 = X[row][SUBS - 1][js];
+                Yn[cc][js].re = __builtin_fma(x1.re, g[js].re, __builtin_fma(-x1.im, g[js].im, Yn[cc][js].re));
+                Yn[cc][js].im = __builtin_fma(x1.re, g[js].im, __builtin_fma(x1.im, g[js].re, Yn[cc][js].im));
+              }
+            }
+          }
+          // column cc of slot li: my slots into its owner's mailbox (each wave only ever touches its
+          // own slots of a partner's scratch; the owner reads it behind the limb's pair sync)
+#pragma unroll
+          for (int js = 0; js < MS; ++js) ctx[(cc / P) * XS + ((cc % P) * SL + sv + js) * 64 + lane] = Ya[js];
+#pragma unroll
+          for (int js = 0; js < MS; ++js) {
+            pin(Ya[js]);
+            if constexpr (HI) pin(Yn[cc][js]);
+          }
+        }
+        }
+        if constexpr (HI) {
+#pragma unroll
+          for (int cc = 0; cc < K1; ++cc)
+#pragma unroll
+            for (int js = 0; js < MS; ++js) Yc[cc][js] = Yn[cc][js];
+        }
+      } else {
+        // levels: each column group's windows sum the NQ levels' groups, then mail
+#pragma unroll
+        for (int cg = 0; cg < NCG; ++cg) {
+          cplx Ya[GC][MS];
+#pragma unroll
+          for (int c2 = 0; c2 < GC; ++c2)
+#pragma unroll
+            for (int js = 0; js < MS; ++js) Ya[c2][js] = {0.0, 0.0};
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            const int r = (li * NCG + cg) * NQ + q;
+            if (r + DIST - 1 < NGRP || !last_step) wait_vmcnt<GLDS * (DIST - 1)>();
+            else if (r + 1 == NGRP) wait_vmcnt<0>();
+            else if (r + 2 == NGRP) wait_vmcnt<GLDS>();
+            else wait_vmcnt<GLDS * 2>();
+            pair_barrier();
+            if (r + DIST < NGRP) issue_group(key_step, r + DIST);
+            else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
+            if constexpr (li == 0) {
+              if (cg == 0 && q == 0) {  // the last level's spectra (published by this barrier)
+#pragma unroll
+                for (int row = 0; row < K1; ++row)
+#pragma unroll
+                  for (int js = 0; js < MS; ++js)
+                    X[row][NF - 1][js] = ctx[(row / P) * XS + ((row % P) * SL + sv + js) * 64 + lane];
+              }
+            }
+#pragma unroll
+            for (int c2 = 0; c2 < GC; ++c2) {
+              const cplx* G = ring + (r % RS) * GROUP + c2 * K1 * M + sv * 64 + lane;
+#pragma unroll
+              for (int row = 0; row < K1; ++row) {
+#pragma unroll
+                for (int js = 0; js < MS; ++js) {
+                  const cplx g = G[row * M + js * 64];
+                  const cplx x = X[row][q][js];
+                  Ya[c2][js].re = __builtin_fma(x.re, g.re, __builtin_fma(-x.im, g.im, Ya[c2][js].re));
+                  Ya[c2][js].im = __builtin_fma(x.re, g.im, __builtin_fma(x.im, g.re, Ya[c2][js].im));
+                }
+              }
+            }
+#pragma unroll
+            for (int c2 = 0; c2 < GC; ++c2)
+#pragma unroll
+              for (int js = 0; js < MS; ++js) pin(Ya[c2][js]);
+          }
+#pragma unroll
+          for (int c2 = 0; c2 < GC; ++c2) {
+            const int cc = cg * GC + c2;
+#pragma unroll
+            for (int js = 0; js < MS; ++js)
+              ctx[(cc / P) * XS + ((cc % P) * SL + sv + js) * 64 + lane] = Ya[c2][js];
+          }
+        }
       }
       sm_sync(sflags, ctl, v, scnt, guard);
       cplx V[8];
@@ -425,10 +493,10 @@ pbs_small_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
   }
 }
 
-template <int N, int K1, int SUBS, bool RESID>
+template <int N, int K1, int SUBS, int NQ, bool RESID>
 static int launch_small_t(const PbsArgs& a) {
   const size_t lds = pbs_small_lds_bytes(N, K1);
-  auto kern = pbs_small_kernel<N, K1, SUBS, RESID>;
+  auto kern = pbs_small_kernel<N, K1, SUBS, NQ, RESID>;
   CHIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const uint32_t blocks = (a.num_samples + SM_CTS - 1) / SM_CTS;
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(SM_CTS * 128), lds, a.stream, a.out, a.out_idx, a.luts, a.lut_idx, a.in,
@@ -442,16 +510,22 @@ static int launch_small_t(const PbsArgs& a) {
   return 0;
 }
 
+template <int N, int K1, int SUBS, int NQ>
+static int launch_small_r(const PbsArgs& a) {
+  return a.resid ? launch_small_t<N, K1, SUBS, NQ, true>(a) : launch_small_t<N, K1, SUBS, NQ, false>(a);
+}
+
 template <int N, int K1>
 static int launch_small_n(const PbsArgs& a) {
+  if (a.level == 2) return launch_small_r<N, K1, 1, 2>(a);
+  if (a.level == 3) return launch_small_r<N, K1, 1, 3>(a);
   // logB <= 15: |digit| <= 2^14 fits the 16-bit grid whole (one sub-digit)
-  if (a.base_log <= 15) return a.resid ? launch_small_t<N, K1, 1, true>(a) : launch_small_t<N, K1, 1, false>(a);
-  return a.resid ? launch_small_t<N, K1, 2, true>(a) : launch_small_t<N, K1, 2, false>(a);
+  return a.base_log <= 15 ? launch_small_r<N, K1, 1, 1>(a) : launch_small_r<N, K1, 2, 1>(a);
 }
 
 int pbs_small_launch(const PbsArgs& a) {
-  if (!(pbs_small_shape(a.k, a.N, a.level) && a.limbs == (uint32_t)SM_LIMBS && a.base_log >= 1 &&
-        a.base_log <= pbs_small_max_logb(a.N))) {
+  if (a.N == 512 && a.k == 4) return pbs512k4_launch(a);  // five polynomials: four waves (pbs512k4.hip)
+  if (!(a.limbs == (uint32_t)SM_LIMBS && pbs_small_ok(a.k, a.N, a.level, a.base_log))) {
     set_error("unsupported PBS parameters: N=%u k=%u level=%u base_log=%u limbs=%u", a.N, a.k, a.level, a.base_log,
               a.limbs);
     return -2;

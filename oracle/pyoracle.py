@@ -158,15 +158,16 @@ def gpu1024k2_error_bound(fbsk_gpu: np.ndarray, logB: int = 23, level: int = 1) 
     return float(main + 4.0 * u * max_out)
 
 
-def gpu_small_error_bound(fbsk_gpu: np.ndarray, N: int, k: int, logB: int) -> float:
+def gpu_small_error_bound(fbsk_gpu: np.ndarray, N: int, k: int, logB: int, level: int = 1) -> float:
     """Certified bound on |x - round(x)| for the GPU's small-ring scheme (concrete_amd/csrc/
     pbs_small.hip, DESIGN.md §4.9: N = 512, k = 3 / N = 256, k = 5, l = 1).  P = 1024 / N
     polynomials share one 512-point transform: their M-point spectra come out of the fft512 through a
     P-point DFT and one twiddle product (sincospi, mu = 2u), i.e. a transform of 9 + log2 P + 1
     stages, and its error is relative to the norm of all P polynomials together: the 2-norm factor
     is sqrt(P N) = 32 instead of sqrt(N).  Digits on the 16-bit limb grid as in pbs1024k2.hip
-    (logB <= 15: one sub-digit, |d| <= 2^(logB-1)).  fbsk_gpu: the device key (f64 view; spectra
-    scaled by 1 / (512 P))."""
+    (logB <= 15: one sub-digit, |d| <= 2^(logB-1)); level > 1 (pbs512k4.hip, logB <= 15): the l
+    levels' whole digits sum into the same slot, dsum = (k + 1) l 2^(logB-1).  fbsk_gpu: the device
+    key (f64 view; spectra scaled by 1 / (512 P))."""
     u = 2.0 ** -53
     P = 1024 // N
     logM = 9.0 + np.log2(P) + 1.0
@@ -176,8 +177,9 @@ def gpu_small_error_bound(fbsk_gpu: np.ndarray, N: int, k: int, logB: int) -> fl
     f = np.asarray(fbsk_gpu, dtype=np.float64).reshape(-1, 2)
     maxG = float(np.max(np.hypot(f[:, 0], f[:, 1]))) * 512.0 * P
     if logB <= 15:
-        dmax = 2.0 ** (logB - 1)
+        dmax = 2.0 ** (logB - 1) * level
     else:
+        assert level == 1
         dmax = 2.0 ** 15 + 2.0 ** max(logB - 17, 0) + 1.0
     dsum = (k + 1) * dmax
     main = np.sqrt(1024.0) * dsum * maxG * (4.0 * gamma + 5.0 * u) * 1.0001

@@ -53,12 +53,19 @@ CASES = [
     ("9bit_k1_N32768", 1, 32768, 2, 2, 15, 9),
     ("10bit_k1_N65536", 1, 65536, 2, 2, 14, 10),
     # round 4: the 1- to 4-bit log-norm2-0 rows above run on their own kernels (pbs_small.hip,
-    # pbs1024k2.hip); these small-ring rows at log norm2 > 0 stay on the general path (its
-    # two-launch kernels: the tile kernels serve the general-format key of the three shapes above,
+    # pbs1024k2.hip), and so do the small-ring rows at l = 2, 3 whose digits fit whole (the next two);
+    # k = 4, N = 512, l = 2 (logB = 16) stays on the general path (its two-launch kernels; the tile
+    # kernels serve the general-format key of the shapes above,
     # test_generic_tile_kernels_on_the_general_format_key)
-    ("3bit_k4_N512", 4, 512, 14, 1, 23, 3),
+    ("3bit_k4_N512_l2", 4, 512, 12, 2, 16, 3),
     ("2bit_k5_N256_l2", 5, 256, 16, 2, 10, 2),
     ("1bit_k6_N256_l2", 6, 256, 12, 2, 12, 1),
+    ("3bit_k4_N512", 4, 512, 14, 1, 23, 3),  # pbs512k4.hip since round 4 (test_gpu_pbs_small.py)
+    # shapes that stay on the general path's two-launch kernels: l = 4 at N = 256 (no table row) and
+    # k = 2, N = 1024, l = 3 (br 3/12)
+    ("k5_N256_l4", 5, 256, 12, 4, 7, 2),
+    ("k2_N1024_l3", 2, 1024, 10, 3, 12, 3),
+    ("k6_N256_l4", 6, 256, 10, 4, 8, 1),
 ]
 
 
@@ -101,8 +108,8 @@ def test_generic_pbs_bit_exact(B, oracle, torch_cuda, case):
     kind, limbs, bits = B.bsk_format(p)
     if kind == 4:  # k = 2, N = 1024, l = 1 / 2: its own kernel since round 4 (test_gpu_pbs1024k2.py)
         bound = oracle.gpu1024k2_error_bound(B.to_host(fbsk).view(np.float64), p.base_log, p.level)
-    elif kind == 5:  # N = 512, k = 3 / N = 256, k = 5, l = 1: pbs_small.hip (test_gpu_pbs_small.py)
-        bound = oracle.gpu_small_error_bound(B.to_host(fbsk).view(np.float64), p.N, p.k, p.base_log)
+    elif kind == 5:  # N = 512, k = 3 / 4, N = 256, k = 5 / 6, l = 1: pbs_small.hip, pbs512k4.hip
+        bound = oracle.gpu_small_error_bound(B.to_host(fbsk).view(np.float64), p.N, p.k, p.base_log, p.level)
     else:
         bound = oracle.generic_error_bound(p.k, p.N, p.level, p.base_log, bits, B.to_host(fbsk).view(np.float64))
     assert bound < 0.5, f"{case[0]}: certified bound {bound}"
@@ -112,10 +119,10 @@ def test_generic_pbs_bit_exact(B, oracle, torch_cuda, case):
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
 
 
-@pytest.mark.parametrize("ci", [17, 15, 16, 5], ids=[CASES[i][0] for i in (17, 15, 16, 5)])
+@pytest.mark.parametrize("ci", [19, 15, 21, 5], ids=[CASES[i][0] for i in (19, 15, 21, 5)])
 def test_generic_tile_many_workgroups(B, oracle, torch_cuda, ci):
     """The general path over many ciphertexts (67: not a multiple of any workgroup's ciphertext
-    count, so the last workgroup runs empty slots): the small-ring rows at log norm2 > 0 and the
+    count, so the last workgroup runs empty slots): small-ring shapes off the hand-tuned kernels and the
     one-launch N = 4096 kernel (a workgroup per ciphertext), bit-exact vs the exact oracle."""
     case = CASES[ci][:3] + (4,) + CASES[ci][4:]
     p, glwe_sk, bsk, fbsk, cts, acc, table, msgs, got, resid = run_case(B, oracle, torch_cuda, case, 7500, batch=67)
@@ -142,7 +149,7 @@ def test_generic_8bit_long_chain_decrypts(B, oracle, torch_cuda):
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
 
 
-@pytest.mark.parametrize("ci", [17, 15, 16, 9], ids=[CASES[i][0] for i in (17, 15, 16, 9)])
+@pytest.mark.parametrize("ci", [19, 15, 21, 20], ids=[CASES[i][0] for i in (19, 15, 21, 20)])
 def test_generic_index_arrays(B, oracle, torch_cuda, ci):
     """Mapped LUTs and permuted input/output rows (GPUDFG.cpp:1149-1205) on the general path:
     the one-launch tile kernels (N = 256: 4 ciphertexts per workgroup, the last one partly

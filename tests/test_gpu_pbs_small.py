@@ -1,6 +1,7 @@
-"""GPU parity tests of the small-ring kernel (concrete_amd/csrc/pbs_small.hip): N = 512, k = 3 and
-N = 256, k = 5 / 6, l = 1 — the optimizer's 1- to 3-bit rows (v0_last_128: opt3 n = 722 logB = 18,
-opt1 n = 592 logB = 15, k = 6 n = 596 logB = 18; bench.py --config opt3 / opt1) — vs the CPU oracle.
+"""GPU parity tests of the small-ring kernels (concrete_amd/csrc/pbs_small.hip: N = 512, k = 3 and
+N = 256, k = 5 / 6; pbs512k4.hip: N = 512, k = 4; l = 1) — the optimizer's 1- to 3-bit rows
+(v0_last_128: opt3 n = 722 logB = 18, opt1 n = 592 logB = 15, k = 6 n = 596 logB = 18, k = 4 n = 731
+logB = 23; bench.py --config opt3 / opt1) — vs the CPU oracle.
 
 Bit-exact u64 equality with the oracle's pure-integer Karatsuba product on the same keys and
 inputs, the measured rounding residual below the scheme's certified bound
@@ -16,10 +17,11 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-# shape -> (optimizer row parameters, message bits): opt3, opt1 and the k = 6 row of v0_last_128 at
-# 1 bit, log norm2 2 (n = 596, br 1/18)
-SHAPES = {"N512_k3": (3, None), "N256_k5": (1, None), "N256_k6": (1, dict(n=596, k=6, N=256, level=1, base_log=18,
-                                                                          ks_level=3, ks_base_log=4))}
+# shape -> (message bits, optimizer row parameters): opt3, opt1, the k = 6 row of v0_last_128 at
+# 1 bit, log norm2 2 (n = 596, br 1/18) and the k = 4 row at 3 bits, log norm2 3 (n = 731, br 1/23)
+SHAPES = {"N512_k3": (3, None), "N256_k5": (1, None),
+          "N256_k6": (1, dict(n=596, k=6, N=256, level=1, base_log=18, ks_level=3, ks_base_log=4)),
+          "N512_k4": (3, dict(n=731, k=4, N=512, level=1, base_log=23, ks_level=3, ks_base_log=4))}
 
 
 @pytest.fixture(scope="module")
@@ -93,7 +95,7 @@ def run_oracle(oracle, S, cts, luts, lut_idx=None, in_idx=None, out_idx=None):
 
 
 def bound(B, oracle, S):
-    return oracle.gpu_small_error_bound(B.to_host(S.fbsk).view(np.float64), S.p.N, S.p.k, S.p.base_log)
+    return oracle.gpu_small_error_bound(B.to_host(S.fbsk).view(np.float64), S.p.N, S.p.k, S.p.base_log, S.p.level)
 
 
 def signed_limb(x, limb, limbs=4):
@@ -157,7 +159,8 @@ def test_bit_exact_small(B, oracle, torch_cuda, shape, batch):
 
 @pytest.mark.parametrize("shape,logB", [("N512_k3", 6), ("N512_k3", 15), ("N512_k3", 16), ("N512_k3", 24),
                                         ("N256_k5", 4), ("N256_k5", 12), ("N256_k5", 16), ("N256_k5", 24),
-                                        ("N256_k6", 15), ("N256_k6", 24)])
+                                        ("N256_k6", 15), ("N256_k6", 24),
+                                        ("N512_k4", 4), ("N512_k4", 15), ("N512_k4", 16), ("N512_k4", 24)])
 def test_digit_forms(B, oracle, torch_cuda, shape, logB):
     """One sub-digit up to logB = 15, the split d = d_lo + 2^16 d_hi from 16 (|d_hi| = 1 at the tie)
     to the largest accepted 24, at both ring sizes."""
@@ -237,7 +240,7 @@ def test_edge_inputs(B, oracle, torch_cuda, shape):
 
 @pytest.mark.parametrize("shape", list(SHAPES))
 def test_full_row_bit_exact_and_bound(B, oracle, torch_cuda, shape):
-    """The full optimizer row (opt3: n = 722; opt1: n = 592; k = 6: n = 596): 512 samples decrypted, 3 bit-exact
+    """The full optimizer row (opt3: n = 722; opt1: n = 592; k = 6: n = 596; k = 4: n = 731): 512 samples decrypted, 3 bit-exact
     vs the exact oracle, the measured residual under the certified bound (< 1/2)."""
     S = small_setup(B, oracle, torch_cuda, shape)
     width = SHAPES[shape][0]
@@ -269,3 +272,154 @@ def test_tiny_n(B, oracle, torch_cuda, shape, n):
     acc = lut_acc(B, S, rng.randint(0, 4, size=4), width)
     got = run_gpu(B, S, cts, acc, torch_cuda)
     assert np.array_equal(got, run_oracle(oracle, S, cts, acc))
+
+
+# ---- N = 512, k = 4 at l = 3 .. 5 (pbs512k4.hip's levels: the rows at br 3/12, 4/9, 5/8) ----------
+K4_LEVEL_ROWS = {3: (12, 700), 4: (9, 702), 5: (8, 689)}  # level -> (logB, a 3-bit optimizer row's n)
+
+
+def k4_level_setup(B, oracle, torch, level, n, seed):
+    key = ("k4l", level, n, seed)
+    if key not in _cache:
+        logB = K4_LEVEL_ROWS[level][0]
+        p = B.PbsParams(n=n, k=4, N=512, level=level, base_log=logB, ks_level=3, ks_base_log=4)
+        _cache[key] = Setup(B, oracle, torch, p, seed)
+    return _cache[key]
+
+
+@pytest.mark.parametrize("level", [3, 4, 5])
+def test_k4_levels_key_layout(B, oracle, torch_cuda, level):
+    """[n][limb][col][q][row][slot][lane]: level v = l - 1 - q of key polynomial (row, col)."""
+    S = k4_level_setup(B, oracle, torch_cuda, level, 3, 9600 + level)
+    p = S.p
+    K1, M, N = 5, 256, 512
+    assert B.bsk_format(p) == (5, 4, 16)
+    assert B.fourier_bsk_bytes(p) == p.n * level * 4 * 25 * M * 16
+    got = B.to_host(S.fbsk).view(np.float64).reshape(p.n, 4, K1, level, K1, 4, 64, 2)
+    bsk = S.bsk.reshape(p.n, level, K1, K1, N)
+    lane = np.arange(64)
+    K = (lane[None, :] >> 3) + 8 * (lane[None, :] & 7) + 64 * np.arange(4)[:, None]
+    tw = np.exp(1j * np.pi * np.arange(M) / N)
+    worst = 0.0
+    for i in (0, p.n - 1):
+        for li in (0, 3):
+            for col in (0, 4):
+                for q in range(level):
+                    for row in (0, 3):
+                        lv = signed_limb(bsk[i, level - 1 - q, row, col], li)
+                        ref = np.fft.fft((lv[:M] + 1j * lv[M:]) * tw)[K] / 1024.0
+                        gg = got[i, li, col, q, row]
+                        worst = max(worst, np.max(np.abs(gg[..., 0] + 1j * gg[..., 1] - ref)) / np.max(np.abs(ref)))
+    assert worst < 1e-13, worst
+
+
+@pytest.mark.parametrize("n", [1, 2, 9])
+@pytest.mark.parametrize("level", [3, 4, 5])
+def test_k4_levels_bit_exact(B, oracle, torch_cuda, level, n):
+    """Bit-exact vs the exact oracle over ring prologues / tails (n = 1, 2) and a longer rotation, odd
+    batch (the last workgroup's second ciphertext empty), residual under the certified bound."""
+    S = k4_level_setup(B, oracle, torch_cuda, level, n, 9700 + 10 * level + n)
+    width = 2
+    rng = np.random.RandomState(level * 10 + n)
+    msgs = rng.randint(0, 4, size=5)
+    cts = encrypt(B, S, msgs, width, 80 + n, std=2.0 ** -30)
+    acc = lut_acc(B, S, rng.randint(0, 4, size=4), width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    assert np.array_equal(got, run_oracle(oracle, S, cts, acc))
+    assert resid < bound(B, oracle, S) < 0.5
+
+
+@pytest.mark.parametrize("level", [3, 5])
+def test_k4_levels_full_row(B, oracle, torch_cuda, level):
+    """The full 3-bit rows (br 3/12 n = 700, br 5/8 n = 689): 256 samples decrypted, 2 bit-exact, residual
+    under the bound."""
+    S = k4_level_setup(B, oracle, torch_cuda, level, K4_LEVEL_ROWS[level][1], 9800 + level)
+    width = 3
+    rng = np.random.RandomState(level)
+    table = rng.randint(0, 8, size=8)
+    msgs = rng.randint(0, 8, size=256)
+    cts = encrypt(B, S, msgs, width, 90 + level)
+    acc = lut_acc(B, S, table, width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    b = bound(B, oracle, S)
+    assert resid < b < 0.5, (resid, b)
+    dec = B.lwe_decrypt(S.glwe_sk, got, S.p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+    assert np.array_equal(got[:2], run_oracle(oracle, S, cts[:2], acc))
+
+
+# ---- pbs_small.hip at l = 2, 3 (whole digits; the rows at br 2/10, 2/12, 3/9) ---------------------
+SM_LEVEL_ROWS = {  # label -> (k, N, l, logB, an optimizer row's n, its message bits)
+    "k5_N256_l2": (5, 256, 2, 10, 594, 1), "k6_N256_l2": (6, 256, 2, 12, 614, 1),
+    "k6_N256_l3": (6, 256, 3, 9, 601, 1), "k3_N512_l2": (3, 512, 2, 12, 739, 3),
+    "k3_N512_l3": (3, 512, 3, 9, 700, 3)}
+
+
+def sm_level_setup(B, oracle, torch, label, n, seed):
+    key = ("sml", label, n, seed)
+    if key not in _cache:
+        k, N, level, logB = SM_LEVEL_ROWS[label][:4]
+        p = B.PbsParams(n=n, k=k, N=N, level=level, base_log=logB, ks_level=3, ks_base_log=4)
+        _cache[key] = Setup(B, oracle, torch, p, seed)
+    return _cache[key]
+
+
+@pytest.mark.parametrize("label", ["k5_N256_l2", "k3_N512_l3"])
+def test_small_levels_key_layout(B, oracle, torch_cuda, label):
+    """[n][limb][cg][q][c2][row][slot][lane] (col = cg GC + c2; GC = 2 at N = 256, k = 5): level
+    v = l - 1 - q of key polynomial (row, col)."""
+    S = sm_level_setup(B, oracle, torch_cuda, label, 3, 9900)
+    p = S.p
+    N, K1, M, P, level = p.N, p.k + 1, p.N // 2, 1024 // p.N, p.level
+    GC = 2 if (N == 256 and K1 % 2 == 0) else 1
+    assert B.bsk_format(p) == (5, 4, 16)
+    got = B.to_host(S.fbsk).view(np.float64).reshape(p.n, 4, K1 // GC, level, GC, K1, M // 64, 64, 2)
+    bsk = S.bsk.reshape(p.n, level, K1, K1, N)
+    lane = np.arange(64)
+    K = (lane[None, :] >> 3) + 8 * (lane[None, :] & 7) + 64 * np.arange(M // 64)[:, None]
+    tw = np.exp(1j * np.pi * np.arange(M) / N)
+    worst = 0.0
+    for i in (0, p.n - 1):
+        for li in (0, 3):
+            for col in range(K1):
+                for q in range(level):
+                    for row in (0, K1 - 1):
+                        lv = signed_limb(bsk[i, level - 1 - q, row, col], li)
+                        ref = np.fft.fft((lv[:M] + 1j * lv[M:]) * tw)[K] / (512.0 * P)
+                        gg = got[i, li, col // GC, q, col % GC, row]
+                        worst = max(worst, np.max(np.abs(gg[..., 0] + 1j * gg[..., 1] - ref)) / np.max(np.abs(ref)))
+    assert worst < 1e-13, worst
+
+
+@pytest.mark.parametrize("n", [1, 2, 9])
+@pytest.mark.parametrize("label", list(SM_LEVEL_ROWS))
+def test_small_levels_bit_exact(B, oracle, torch_cuda, label, n):
+    """Bit-exact vs the exact oracle over ring prologues / tails and a longer rotation, a ragged batch
+    of 5 (four ciphertexts per workgroup), residual under the certified bound."""
+    S = sm_level_setup(B, oracle, torch_cuda, label, n, 9910 + n)
+    width = 2
+    rng = np.random.RandomState(n)
+    msgs = rng.randint(0, 4, size=5)
+    cts = encrypt(B, S, msgs, width, 85 + n, std=2.0 ** -30)
+    acc = lut_acc(B, S, rng.randint(0, 4, size=4), width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    assert np.array_equal(got, run_oracle(oracle, S, cts, acc))
+    assert resid < bound(B, oracle, S) < 0.5
+
+
+@pytest.mark.parametrize("label", ["k5_N256_l2", "k6_N256_l3", "k3_N512_l3"])
+def test_small_levels_full_row(B, oracle, torch_cuda, label):
+    """Full rows: 256 samples decrypted, 2 bit-exact, residual under the bound."""
+    S = sm_level_setup(B, oracle, torch_cuda, label, SM_LEVEL_ROWS[label][4], 9950)
+    width = SM_LEVEL_ROWS[label][5]
+    rng = np.random.RandomState(11)
+    table = rng.randint(0, 1 << width, size=1 << width)
+    msgs = rng.randint(0, 1 << width, size=256)
+    cts = encrypt(B, S, msgs, width, 95)
+    acc = lut_acc(B, S, table, width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    b = bound(B, oracle, S)
+    assert resid < b < 0.5, (resid, b)
+    dec = B.lwe_decrypt(S.glwe_sk, got, S.p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+    assert np.array_equal(got[:2], run_oracle(oracle, S, cts[:2], acc))

@@ -151,22 +151,26 @@ __global__ void __launch_bounds__(256) convert_bsk_kernel(cplx* __restrict__ des
 // polynomial g (row, col), limb `limb`, as an N = 1024 negacyclic polynomial: folded, twisted,
 // transformed exactly like the N = 1024 key.
 #if P2_PM
-// P2_PM: block = (i, limb, col, row); both parity spectra G_e, G_o in double-double, then the key at
-// the square roots of each evaluation point, K+-[f] = (G_e[f] +- s_f G_o[f]) / 2 with
+// P2_PM: block = (i, limb, col, q, row); both parity spectra G_e, G_o in double-double, then the key
+// at the square roots of each evaluation point, K+-[f] = (G_e[f] +- s_f G_o[f]) / 2 with
 // s_f = exp(i pi (1 - 4 f) / 2048) (s_f^2 = alpha_f), correctly rounded from double-double.  Layout
-// [n][limb][col][row][+-][slot][lane], scaled 1/512 like the even/odd key.
+// [n][limb][col][q][row][+-][slot][lane] (level v = l - 1 - q, q in digit order), scaled 1/512 like
+// the even/odd key.
 template <int LIMBS>
 __global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__ dest, const uint64_t* __restrict__ src,
                                                              const ddc* __restrict__ zeta_t,
                                                              const ddc* __restrict__ tw_t,
-                                                             const ddc* __restrict__ sroot_t) {
+                                                             const ddc* __restrict__ sroot_t, uint32_t level) {
   constexpr int M = 512, LOGM = 9;
   __shared__ ddc buf[2][M];
   const uint64_t blk = blockIdx.x;
-  const uint32_t row = (uint32_t)(blk & 1), col = (uint32_t)((blk >> 1) & 1);
-  const uint32_t limb = (uint32_t)((blk >> 2) % LIMBS);
-  const uint64_t i = (blk >> 2) / LIMBS;
-  const uint64_t* g = src + (i * 4 + row * 2 + col) * 2048;  // [n][l = 1][row][col][N]
+  const uint32_t row = (uint32_t)(blk & 1);
+  const uint32_t q = (uint32_t)((blk >> 1) % level);
+  const uint32_t col = (uint32_t)((blk >> 1) / level & 1);
+  const uint32_t limb = (uint32_t)(((blk >> 1) / level >> 1) % LIMBS);
+  const uint64_t i = ((blk >> 1) / level >> 1) / LIMBS;
+  const uint32_t v = level - 1 - q;
+  const uint64_t* g = src + ((i * level + v) * 4 + row * 2 + col) * 2048;  // [n][l][row][col][N]
   for (int e = threadIdx.x; e < 2 * M; e += blockDim.x) {
     const int par = e / M, j = e % M;
     ddc z{dd_from(limb_value<LIMBS>(g[2 * j + par], limb)), dd_from(limb_value<LIMBS>(g[2 * (j + M) + par], limb))};
@@ -193,15 +197,19 @@ __global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__
 template <int LIMBS>
 __global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__ dest, const uint64_t* __restrict__ src,
                                                              const ddc* __restrict__ zeta_t,
-                                                             const ddc* __restrict__ tw_t, const ddc* __restrict__) {
+                                                             const ddc* __restrict__ tw_t, const ddc* __restrict__,
+                                                             uint32_t level) {
   constexpr int M = 512, LOGM = 9;
   __shared__ ddc buf[M];
   const uint64_t blk = blockIdx.x;
   const uint32_t par = (uint32_t)(blk & 1);
-  const uint32_t row = (uint32_t)((blk >> 1) & 1), col = (uint32_t)((blk >> 2) & 1);
-  const uint32_t limb = (uint32_t)((blk >> 3) % LIMBS);
-  const uint64_t i = (blk >> 3) / LIMBS;
-  const uint64_t* g = src + (i * 4 + row * 2 + col) * 2048;  // [n][l = 1][row][col][N]
+  const uint32_t row = (uint32_t)((blk >> 1) & 1);
+  const uint32_t q = (uint32_t)((blk >> 2) % level);
+  const uint32_t col = (uint32_t)((blk >> 2) / level & 1);
+  const uint32_t limb = (uint32_t)(((blk >> 2) / level >> 1) % LIMBS);
+  const uint64_t i = ((blk >> 2) / level >> 1) / LIMBS;
+  const uint32_t v = level - 1 - q;
+  const uint64_t* g = src + ((i * level + v) * 4 + row * 2 + col) * 2048;  // [n][l][row][col][N]
   for (int j = threadIdx.x; j < M; j += blockDim.x) {
     ddc z{dd_from(limb_value<LIMBS>(g[2 * j + par], limb)), dd_from(limb_value<LIMBS>(g[2 * (j + M) + par], limb))};
     z = ddc_mul(z, zeta_t[j]);
@@ -213,7 +221,7 @@ __global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__
 }
 #endif
 
-// N = 1024, k = 2, l = 1 or 2 (pbs1024k2.hip).  Block = (i, limb, col, q, row), in the order of the
+// N = 1024, k = 2, l <= 3 (pbs1024k2.hip).  Block = (i, limb, col, q, row), in the order of the
 // output layout [n][limb][col][q][row][512]: limb `limb` of key polynomial (row, col) of level
 // v = l - 1 - q (q in digit order), folded, twisted and transformed like the k = 1 key.
 __global__ void __launch_bounds__(256) convert_bsk1024k2_kernel(cplx* __restrict__ dest,
@@ -337,8 +345,9 @@ static void make_sroots(std::vector<ddc>& sr) {
 int convert_bsk_launch(const ConvertArgs& a) {
   if (key_format(a.k, a.N, a.level).kind == KeyKind::GENERIC) return convert_bsk_generic_launch(a);
   const bool n1024 = a.N == 1024 && a.k == 1 && a.limbs == 3 && a.level >= 1 && a.level <= 3;
-  const bool n2048 = a.N == 2048 && a.k == 1 && a.limbs == (uint32_t)PBS2_LIMBS && a.level == 1;
-  const bool k2 = a.N == 1024 && a.k == 2 && a.limbs == (uint32_t)K2_LIMBS && (a.level == 1 || a.level == 2);
+  const bool n2048 =
+      a.N == 2048 && a.k == 1 && a.limbs == (uint32_t)PBS2_LIMBS && a.level >= 1 && a.level <= PBS2_MAX_LEVEL;
+  const bool k2 = a.N == 1024 && a.k == 2 && a.limbs == (uint32_t)K2_LIMBS && a.level >= 1 && a.level <= K2_MAX_LEVEL;
   const bool small = pbs_small_shape(a.k, a.N, a.level) && a.limbs == (uint32_t)SM_LIMBS;
   if (!n1024 && !n2048 && !k2 && !small) {
     set_error("unsupported BSK conversion parameters: N=%u k=%u level=%u limbs=%u", a.N, a.k, a.level, a.limbs);
@@ -359,9 +368,9 @@ int convert_bsk_launch(const ConvertArgs& a) {
     make_sroots(sr);
     CHIP_CHECK(hipMallocAsync((void**)&ds, sr.size() * sizeof(ddc), a.stream));
     CHIP_CHECK(hipMemcpyAsync(ds, sr.data(), sr.size() * sizeof(ddc), hipMemcpyHostToDevice, a.stream));
-    const uint64_t blocks = (uint64_t)a.n * PBS2_LIMBS * 4 * (P2_PM ? 1 : 2);
+    const uint64_t blocks = (uint64_t)a.n * PBS2_LIMBS * 4 * a.level * (P2_PM ? 1 : 2);
     hipLaunchKernelGGL((convert_bsk2048_kernel<PBS2_LIMBS>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
-                       reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, ds);
+                       reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, ds, a.level);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       set_error("convert launch failed: %s", hipGetErrorString(e));

@@ -18,9 +18,9 @@ KeyFormat generic_key_format(uint32_t k, uint32_t N, uint32_t level);  // pbs_ge
 inline bool pbs_needs_generic_key(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
   const KeyFormat f = key_format(k, N, level);
   if (f.kind == KeyKind::N1024 && !pbs1024_exact(k, level, base_log)) return generic_pbs_ok(k, N, level, base_log);
-  if (f.kind == KeyKind::N2048 && !(base_log >= 1 && base_log <= PBS2_MAX_LOGB))
+  if (f.kind == KeyKind::N2048 && !pbs2048_ok(level, base_log))
     return generic_pbs_ok(k, N, level, base_log);
-  if (f.kind == KeyKind::K2N1024 && !(base_log >= 1 && base_log <= k2_max_logb(level)))
+  if (f.kind == KeyKind::K2N1024 && !k2_ok(level, base_log))
     return generic_pbs_ok(k, N, level, base_log);
   if (f.kind == KeyKind::SMALL && !pbs_small_ok(k, N, level, base_log))
     return generic_pbs_ok(k, N, level, base_log);

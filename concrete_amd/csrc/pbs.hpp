@@ -35,6 +35,14 @@ constexpr int PBS2_LIMBS = 4;     // 16-bit key limbs
 constexpr int PBS2_SUBS = 2;      // sub-digits per decomposition digit: balanced 16-bit d_lo, d_hi
 constexpr int PBS2_SUB_BITS = 16; // on the key-limb grid (pbs2048.hip)
 constexpr int PBS2_MAX_LOGB = 24; // |d_hi| <= 2^(logB-17) + 1 keeps the certified bound < 1/2
+// l = 2 .. PBS2_MAX_LEVEL: whole digits with l 2^(logB-1) <= 2^15 (the l = 1 digit's magnitude), the
+// levels' products summed into the same slot (the optimizer's 5-bit rows at br 2/15, 3/11, 4/9)
+constexpr uint32_t PBS2_MAX_LEVEL = 4;
+inline bool pbs2048_ok(uint32_t level, uint32_t base_log) {
+  if (level == 1) return base_log >= 1 && base_log <= (uint32_t)PBS2_MAX_LOGB;
+  return level >= 2 && level <= PBS2_MAX_LEVEL && base_log >= 1 && base_log <= 15 &&
+         ((uint64_t)level << (base_log - 1)) <= (1ull << 15);
+}
 // P2_PM = 1: the key holds the spectra at the two square roots +-s_k of each evaluation point
 // alpha_k, K+- = (G_e +- s G_o) / 2 (the N = 2048 polynomial evaluated at +-s_k, i.e. its
 // 1024-point negacyclic spectrum), so a product costs 2 complex multiplies per frequency instead
@@ -57,8 +65,15 @@ constexpr int K2_LIMBS = 4;
 constexpr int K2_SUBS = 2;
 constexpr int K2_SUB_BITS = 16;
 constexpr int K2_MAX_LOGB = 24;  // certified bound < 1/2 (oracle/pyoracle.py:gpu1024k2_error_bound)
-// l = 1: one digit split into two sub-digits (logB <= 24); l = 2: two whole digits (logB <= 15)
-inline uint32_t k2_max_logb(uint32_t level) { return level == 1 ? (uint32_t)K2_MAX_LOGB : level == 2 ? 15u : 0u; }
+// l = 1: one digit split into two sub-digits (logB <= 24); l = 2 .. K2_MAX_LEVEL: whole digits with
+// l 2^(logB-1) <= 2^15 (the l = 1 digit's magnitude; the optimizer's br 2/15, 3/12 rows; l = 4 would
+// hold 36 digit spectra per wave: 66-78 spilled VGPRs)
+constexpr uint32_t K2_MAX_LEVEL = 3;
+inline bool k2_ok(uint32_t level, uint32_t base_log) {
+  if (level == 1) return base_log >= 1 && base_log <= (uint32_t)K2_MAX_LOGB;
+  return level >= 2 && level <= K2_MAX_LEVEL && base_log >= 1 && base_log <= 15 &&
+         ((uint64_t)level << (base_log - 1)) <= (1ull << 15);
+}
 constexpr size_t pbs1024k2_lds_bytes() {
   return PBS1024_TABLE_BYTES + 3 * K2_CTS * PBS1024_XCH_SLOTS * 16 + (size_t)K2_RING_SLOTS * 3 * 512 * 16 +
          3 * K2_CTS * 4;  // + per-wave sync counters
@@ -115,7 +130,7 @@ inline bool pbs_small_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_l
 // GENERIC: pbs_generic.hip, L balanced limbs of `bits` bits for any k <= GEN_MAX_K and
 // N = 256 .. 16384.  The format depends on (k, N, l) only: the runtime's key conversion call
 // carries no base_log (context.h:106-109).
-// K2N1024: pbs1024k2.hip (k = 2, N = 1024, l = 1 or 2); SMALL: pbs_small.hip (N = 512, k = 3 and
+// K2N1024: pbs1024k2.hip (k = 2, N = 1024, l <= 3); SMALL: pbs_small.hip (N = 512, k = 3 and
 // N = 256, k = 5 / 6, l <= 3) and pbs512k4.hip (N = 512, k = 4, l = 1, 3 .. 5).  The values are the ABI's format codes
 // (concrete_hip_bsk_format).
 enum class KeyKind { NONE, N1024, N2048, GENERIC, K2N1024, SMALL };
@@ -151,9 +166,9 @@ inline bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_
   switch (f.kind) {
     case KeyKind::N1024: return pbs1024_exact(k, level, base_log);
     // one level whose digit splits into d_lo + 2^16 d_hi (pbs2048.hip)
-    case KeyKind::N2048: return base_log >= 1 && base_log <= PBS2_MAX_LOGB;
+    case KeyKind::N2048: return pbs2048_ok(level, base_log);
     case KeyKind::GENERIC: return generic_pbs_ok(k, N, level, base_log);
-    case KeyKind::K2N1024: return base_log >= 1 && base_log <= k2_max_logb(level);
+    case KeyKind::K2N1024: return k2_ok(level, base_log);
     case KeyKind::SMALL: return pbs_small_ok(k, N, level, base_log);
     default: return false;
   }
@@ -161,9 +176,9 @@ inline bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_
 
 // Size in bytes of the device Fourier bootstrapping key.
 //   N1024:   [n][col][limb][row*l + q][512] complex f64
-//   N2048:   [n][limb][col][row][parity][512] complex f64 (pbs2048.hip)
+//   N2048:   [n][limb][col][q][row][+-][512] complex f64 (pbs2048.hip; l <= 4)
 //   GENERIC: [n][col][limb][row][q][N/2] complex f64 (pbs_generic.hip)
-//   K2N1024: [n][limb][col][q][row][512] complex f64 (pbs1024k2.hip; l = 1 or 2)
+//   K2N1024: [n][limb][col][q][row][512] complex f64 (pbs1024k2.hip; l <= 3)
 //   SMALL:   [n][limb][cg][q][c2][row][N/2] complex f64, col = cg GC + c2 (pbs_small.hip, pbs512k4.hip;
 //            GC = sm_gc(N, k + 1))
 inline uint64_t fourier_bsk_bytes(uint32_t n, uint32_t k, uint32_t level, uint32_t N) {

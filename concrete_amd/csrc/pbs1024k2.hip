@@ -32,6 +32,8 @@
 #include "kernel_util.hpp"
 #include "pbs.hpp"
 
+#include <type_traits>
+
 namespace chip {
 
 namespace {
@@ -103,10 +105,10 @@ __device__ __forceinline__ void tri_wait(uint32_t* flags, int ctl, int v, uint32
 
 }  // namespace
 
-// LEVELS = false: l = 1, the two sub-digits of one digit (d_hi carried into the next slot);
-// LEVELS = true: l = 2 at logB <= 15, the two levels' digits whole (both in the same slot; the key
+// NQ = 1: l = 1, the two sub-digits of one digit (d_hi carried into the next slot); NQ = l = 2, 3:
+// whole digits (l 2^(logB-1) <= 2^15), the levels' products in the same slot (the key
 // holds both levels, [n][limb][col][q][row][512], one ring group per level).
-template <bool RESID, bool LEVELS>
+template <bool RESID, int NQ>
 __global__ void __launch_bounds__(K2_CTS * 192, 1)
 pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx,
                  const uint64_t* __restrict__ luts, const uint64_t* __restrict__ lut_idx,
@@ -115,7 +117,9 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
                  unsigned long long* __restrict__ resid_out, SyncGuard guard) {
   constexpr int N = 1024, LOG2_2N = 11, K1 = 3;
   constexpr int NW = 3 * K2_CTS;              // waves per workgroup
-  constexpr int NQ = LEVELS ? 2 : 1;          // key levels per (limb, column)
+  constexpr bool LEVELS = NQ > 1;             // key levels per (limb, column): NQ
+  constexpr int NF = LEVELS ? NQ : K2_SUBS;   // digit polynomials (sub-digits or levels) per step
+  using StT = std::conditional_t<(NQ > 2), uint64_t, uint32_t>;  // decomposition state (l logB bits)
   constexpr int GROUP = K1 * 512;             // (limb, column[, level]): the three row spectra
   constexpr int NGRP = K2_LIMBS * K1 * NQ;    // ring groups per CMUX step
   constexpr int PER_I = NGRP * GROUP;         // complex values per Fourier GGSW
@@ -213,7 +217,7 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
 
     // ---- ct1 = X^{at} acc - acc within my own scratch (nobody else reads or writes it between
     //      the last limb's mailbox read and this step's first spectrum exchange)
-    uint32_t st[16];
+    StT st[16];
     {
 #pragma unroll
       for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = A[m];
@@ -225,17 +229,17 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const uint32_t sp = (uint32_t)(lane + 64 * m - (int)at) & (2 * N - 1);
-        st[m] = (uint32_t)decomp_init((sp < N ? rv[m] : 0ull - rv[m]) - A[m], nrep);
+        st[m] = (StT)decomp_init((sp < N ? rv[m] : 0ull - rv[m]) - A[m], nrep);
       }
       wave_lds_fence();
     }
 
     // ---- one level, two sub-digit polynomials, forward transforms ------------------------
     // X[row][sub][jj]: spectrum of row `row`'s sub-digit polynomial at my slot sb + jj
-    cplx X[K1][K2_SUBS][MS];
+    cplx X[K1][NF][MS];
     int32_t dlo[16], dhi[16];
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
+    for (int m = 0; m < (NQ <= 2 ? 16 : 0); ++m) {  // NQ > 2: each level's digits before its transform
       const int32_t d = decomp_next_t(st[m], logB);
       if constexpr (LEVELS) {
         dlo[m] = d;                           // level q = 0 (least significant first)
@@ -247,12 +251,16 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
       }
     }
 #pragma unroll
-    for (int sub = 0; sub < K2_SUBS; ++sub) {
+    for (int sub = 0; sub < NF; ++sub) {
       {
+        if constexpr (NQ > 2) {
+#pragma unroll
+          for (int m = 0; m < 16; ++m) dlo[m] = decomp_next_t(st[m], logB);  // level q = sub
+        }
         cplx vv8[8];
 #pragma unroll
         for (int m = 0; m < 8; ++m)
-          vv8[m] = sub == 0 ? cplx{(double)dlo[m], (double)dlo[m + 8]} : cplx{(double)dhi[m], (double)dhi[m + 8]};
+          vv8[m] = sub == 0 || NQ > 2 ? cplx{(double)dlo[m], (double)dlo[m + 8]} : cplx{(double)dhi[m], (double)dhi[m + 8]};
         cplx tw2[4], tw3[4];
         fwd_p2_tw(tw2, T, lane >> 3);
         fwd_p3_tw(tw3, T, lane);
@@ -267,7 +275,7 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
       }
       // The last sub-digit's spectra need no sync: the first key window's workgroup barrier
       // (which drains every wave's LDS writes) publishes them; they are read right after it.
-      if (sub + 1 < K2_SUBS) {
+      if (sub + 1 < NF) {
         tri_sync(tflags, ctl, v, tcnt, guard);
 #pragma unroll
         for (int row = 0; row < K1; ++row)
@@ -316,7 +324,7 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
               for (int row = 0; row < K1; ++row)
 #pragma unroll
                 for (int jj = 0; jj < MS; ++jj)
-                  if (has(jj)) X[row][K2_SUBS - 1][jj] = ctx[(K2D_NOXRD ? v : row) * XS + (sb + jj) * 64 + lane];
+                  if (has(jj)) X[row][NF - 1][jj] = ctx[(K2D_NOXRD ? v : row) * XS + (sb + jj) * 64 + lane];
             }
           }
           cplx Ya[MS];
@@ -382,7 +390,7 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
                 for (int row = 0; row < K1; ++row)
 #pragma unroll
                   for (int jj = 0; jj < MS; ++jj)
-                    if (has(jj)) X[row][K2_SUBS - 1][jj] = ctx[row * XS + (sb + jj) * 64 + lane];
+                    if (has(jj)) X[row][NF - 1][jj] = ctx[row * XS + (sb + jj) * 64 + lane];
               }
             }
             const cplx* G = ring + (r % RS) * GROUP + sb * 64 + lane;
@@ -464,10 +472,10 @@ pbs1024k2_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_id
   }
 }
 
-template <bool RESID, bool LEVELS>
+template <bool RESID, int NQ>
 static int launch_k2_t(const PbsArgs& a) {
   const size_t lds = pbs1024k2_lds_bytes();
-  auto kern = pbs1024k2_kernel<RESID, LEVELS>;
+  auto kern = pbs1024k2_kernel<RESID, NQ>;
   CHIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const uint32_t blocks = (a.num_samples + K2_CTS - 1) / K2_CTS;
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(K2_CTS * 192), lds, a.stream, a.out, a.out_idx, a.luts, a.lut_idx,
@@ -482,15 +490,17 @@ static int launch_k2_t(const PbsArgs& a) {
 }
 
 int pbs1024k2_launch(const PbsArgs& a) {
-  if (!(a.N == 1024 && a.k == 2 && a.limbs == (uint32_t)K2_LIMBS && a.base_log >= 1 &&
-        a.base_log <= k2_max_logb(a.level))) {
+  if (!(a.N == 1024 && a.k == 2 && a.limbs == (uint32_t)K2_LIMBS && k2_ok(a.level, a.base_log))) {
     set_error("unsupported PBS parameters: N=%u k=%u level=%u base_log=%u limbs=%u", a.N, a.k, a.level, a.base_log,
               a.limbs);
     return -2;
   }
   if (a.num_samples == 0) return 0;
-  if (a.level == 2) return a.resid ? launch_k2_t<true, true>(a) : launch_k2_t<false, true>(a);
-  return a.resid ? launch_k2_t<true, false>(a) : launch_k2_t<false, false>(a);
+  switch (a.level) {
+    case 1: return a.resid ? launch_k2_t<true, 1>(a) : launch_k2_t<false, 1>(a);
+    case 2: return a.resid ? launch_k2_t<true, 2>(a) : launch_k2_t<false, 2>(a);
+    default: return a.resid ? launch_k2_t<true, 3>(a) : launch_k2_t<false, 3>(a);
+  }
 }
 
 }  // namespace chip

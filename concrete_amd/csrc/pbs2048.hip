@@ -38,6 +38,8 @@
 #include "kernel_util.hpp"
 #include "pbs.hpp"
 
+#include <type_traits>
+
 namespace chip {
 
 constexpr uint64_t P2_MAGIC_ALL =
@@ -102,7 +104,10 @@ __device__ __forceinline__ void pair_sync2048(uint32_t* flags, int ctl, int v, u
   spin_until_ge(&flags[ctl * 4 + (v ^ 1)], cnt, guard);
 }
 
-template <bool RESID>
+// NQ = 1: one digit split into d_lo + 2^16 d_hi (logB <= 24); NQ = l = 2 .. 4: whole digits
+// (l 2^(logB-1) <= 2^15), each level's products landing in the same slot (the key holds the levels,
+// [n][limb][col][q][row][+-][512], one ring group per (column, level, row)).
+template <bool RESID, int NQ>
 __global__ void __launch_bounds__(PBS2_CTS * 256, 2)
 pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx,
                     const uint64_t* __restrict__ luts, const uint64_t* __restrict__ lut_idx,
@@ -112,7 +117,9 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   constexpr int N = 2048, LOG2_2N = 12, K1 = 2;
   constexpr int NW = 4 * PBS2_CTS;                          // waves per workgroup
   constexpr int GROUP = 2 * 512;                            // (limb, col, row): parity e and o spectra
-  constexpr int NGRP = PBS2_LIMBS * K1 * K1;                // ring groups per CMUX step
+  constexpr int NGRP = PBS2_LIMBS * K1 * K1 * NQ;           // ring groups per CMUX step
+  constexpr int NF = NQ == 1 ? PBS2_SUBS : NQ;              // forward transforms per step
+  using StT = std::conditional_t<(NQ > 1), uint64_t, uint32_t>;  // decomposition state (l logB bits)
   constexpr int PER_I = NGRP * GROUP;                       // complex values per Fourier GGSW
   constexpr int RS = PBS2_RING_SLOTS, DIST = PBS2_RING_DIST;
   constexpr int GLDS = GROUP / 64 / NW;                     // 1 KB LDS-DMA pieces per wave per group
@@ -190,7 +197,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     sroot[jj] = {cs, sn};
   }
   // X[2 row][sub] / X[2 row + 1][sub] (parity e / o spectra of one row) -> A+ / A- in place
-  auto to_pm = [&](cplx (&X)[4][PBS2_SUBS][2], int sub) __attribute__((always_inline)) {
+  auto to_pm = [&](cplx (&X)[4][NF][2], int sub) __attribute__((always_inline)) {
 #pragma unroll
     for (int row = 0; row < 2; ++row)
 #pragma unroll
@@ -214,7 +221,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   }
 #endif
 
-  const int nrep = 64 - (int)base_log;
+  const int nrep = 64 - NQ * (int)base_log;
   const int logB = (int)base_log;
   double max_resid = 0.0;
 
@@ -231,7 +238,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     // compiler from hoisting undefined values of skipped-step arrays out of the loop.
 
     // ---- ct1 = X^{at} acc - acc: the source coefficient may sit in the other parity's wave --
-    uint32_t st[16];
+    StT st[16];
     {
 #pragma unroll
       for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = A[m];
@@ -251,17 +258,17 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
         const uint32_t sj = sp & (N - 1);
         const uint64_t* box = reinterpret_cast<const uint64_t*>(ctx + (c * 2 + (int)(sj & 1)) * XS);
         const uint64_t rv = box[sj >> 1];
-        st[m] = (uint32_t)decomp_init((sp < N ? rv : 0ull - rv) - A[m], nrep);
+        st[m] = (StT)decomp_init((sp < N ? rv : 0ull - rv) - A[m], nrep);
       }
     }
     if (odd) pair_sync2048(qflags, ctl, v, qcnt, guard);  // my partner has read my scratch
 
-    // ---- one decomposition level, two sub-digit polynomials, forward transforms ----------
-    // X[vv][sub][jj]: spectrum of sub-digit polynomial (virtual poly vv = 2 row + parity) at
+    // ---- digit polynomials (two sub-digits of one level, or NQ levels), forward transforms --
+    // X[vv][f][jj]: spectrum of digit polynomial f (virtual poly vv = 2 row + parity) at
     // frequency slot 2v + jj
-    cplx X[4][PBS2_SUBS][2];
+    cplx X[4][NF][2];
     int32_t dlo[16], dhi[16];
-    {
+    if constexpr (NQ == 1) {
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int32_t d = decomp_next_t(st[m], logB);
@@ -271,12 +278,16 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
       }
     }
 #pragma unroll
-    for (int sub = 0; sub < PBS2_SUBS; ++sub) {
+    for (int sub = 0; sub < NF; ++sub) {
       {
+        if constexpr (NQ > 1) {
+#pragma unroll
+          for (int m = 0; m < 16; ++m) dlo[m] = decomp_next_t(st[m], logB);  // level q = sub
+        }
         cplx vv8[8];
 #pragma unroll
         for (int m = 0; m < 8; ++m)
-          vv8[m] = sub == 0 ? cplx{(double)dlo[m], (double)dlo[m + 8]} : cplx{(double)dhi[m], (double)dhi[m + 8]};
+          vv8[m] = sub == 0 || NQ > 1 ? cplx{(double)dlo[m], (double)dlo[m + 8]} : cplx{(double)dhi[m], (double)dhi[m + 8]};
 #if P2_SPLIT_XSYNC
         if (!D4_NOFWD) {
           cplx tw2[4], tw3[4];
@@ -297,7 +308,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
       // The last sub-digit's spectra need no quad sync: the first key window's workgroup barrier
       // (which drains every wave's LDS writes) publishes them, and they are first used in the
       // second window (sub 1); they are read right after that barrier.
-      if (sub + 1 < PBS2_SUBS) {
+      if (sub + 1 < NF) {
         quad_sync(qflags, ctl, v, qcnt, guard);
 #pragma unroll
         for (int vv = 0; vv < 4; ++vv)
@@ -314,9 +325,9 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
       // everyone has read my spectrum before my next transform writes the scratch; after the
       // last sub-digit the scratches are next written behind the key windows' barriers
 #if P2_SPLIT_XSYNC
-      if (sub + 1 < PBS2_SUBS) quad_signal(qflags, ctl, v, qcnt);
+      if (sub + 1 < NF) quad_signal(qflags, ctl, v, qcnt);
 #else
-      if (sub + 1 < PBS2_SUBS) quad_sync(qflags, ctl, v, qcnt, guard);
+      if (sub + 1 < NF) quad_sync(qflags, ctl, v, qcnt, guard);
 #endif
     }
 
@@ -332,7 +343,13 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
       for (int jj = 0; jj < 2; ++jj) Ya[cc][0][jj] = Ya[cc][1][jj] = Pa[cc][jj] = {0.0, 0.0};
     static_for<0, PBS2_LIMBS>([&](auto LI) __attribute__((always_inline)) {
       constexpr int li = decltype(LI)::value;
-      constexpr bool HI = li + 1 < PBS2_LIMBS;  // d_hi * g_3 lands at 2^64: vanishes
+      constexpr bool HI = NQ == 1 && li + 1 < PBS2_LIMBS;  // d_hi * g_3 lands at 2^64: vanishes
+      if constexpr (NQ > 1 && li > 0) {  // levels: no carry, every slot starts from zero
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) Ya[cc][0][jj] = Ya[cc][1][jj] = Pa[cc][jj] = {0.0, 0.0};
+      }
       cplx Yb[2][2][2], Pb[2][2];
 #pragma unroll
       for (int cc = 0; cc < 2; ++cc)
@@ -365,8 +382,9 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
 #pragma unroll
       for (int cc = 0; cc < K1; ++cc) {
 #pragma unroll
-        for (int row = 0; row < K1; ++row) {
-          const int r = (li * K1 + cc) * K1 + row;  // group within the step
+        for (int rq = 0; rq < K1 * NQ; ++rq) {
+          const int q = rq / K1, row = rq % K1;  // level (NQ > 1), row
+          const int r = (li * K1 + cc) * K1 * NQ + rq;  // group within the step
           // group r landed for this wave's pieces (the next DIST - 1 may stay in flight) ...
           if (r + DIST - 1 < NGRP || !last_step) wait_vmcnt<GLDS * (DIST - 1)>();
           else if (r + 1 == NGRP) wait_vmcnt<0>();
@@ -377,14 +395,14 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
           if (r + DIST < NGRP) issue_group(key_step, r + DIST);
           else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
           if constexpr (li == 0) {
-            if (cc == 0 && row == 0) {  // the last sub-digit's spectra (see above)
+            if (cc == 0 && rq == 0) {  // the last digit polynomial's spectra (see above)
 #pragma unroll
               for (int vv = 0; vv < 4; ++vv)
 #pragma unroll
                 for (int jj = 0; jj < 2; ++jj)
-                  X[vv][PBS2_SUBS - 1][jj] = ctx[vv * XS + (2 * v + jj) * 64 + lane];
+                  X[vv][NF - 1][jj] = ctx[vv * XS + (2 * v + jj) * 64 + lane];
 #if P2_PM
-              to_pm(X, PBS2_SUBS - 1);
+              to_pm(X, NF - 1);
 #endif
             }
           }
@@ -397,7 +415,7 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             // them one at a time, each behind its own LDS round trip): +1.1 %, 255 VGPRs
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int jj = 0; jj < (D4_NOMAC ? 0 : 2); ++jj) mac(Ya[cc], Pa[cc], X[2 * row][0][jj], X[2 * row + 1][0][jj], ge[jj], go[jj], jj);
+            for (int jj = 0; jj < (D4_NOMAC ? 0 : 2); ++jj) mac(Ya[cc], Pa[cc], X[2 * row][q][jj], X[2 * row + 1][q][jj], ge[jj], go[jj], jj);
             if constexpr (HI) {
 #pragma unroll
               for (int jj = 0; jj < (D4_NOMAC ? 0 : 2); ++jj)
@@ -511,10 +529,10 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
   }
 }
 
-template <bool RESID>
+template <bool RESID, int NQ>
 static int launch2048_t(const PbsArgs& a) {
   const size_t lds = pbs2048_lds_bytes();
-  auto kern = pbs2048_quad_kernel<RESID>;
+  auto kern = pbs2048_quad_kernel<RESID, NQ>;
   CHIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const uint32_t blocks = (a.num_samples + PBS2_CTS - 1) / PBS2_CTS;
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(PBS2_CTS * 256), lds, a.stream, a.out, a.out_idx, a.luts, a.lut_idx,
@@ -529,14 +547,18 @@ static int launch2048_t(const PbsArgs& a) {
 }
 
 int pbs2048_launch(const PbsArgs& a) {
-  if (!(a.N == 2048 && a.k == 1 && a.level == 1 && a.limbs == (uint32_t)PBS2_LIMBS && a.base_log >= 1 &&
-        a.base_log <= (uint32_t)PBS2_MAX_LOGB)) {
+  if (!(a.N == 2048 && a.k == 1 && a.limbs == (uint32_t)PBS2_LIMBS && pbs2048_ok(a.level, a.base_log))) {
     set_error("unsupported PBS parameters: N=%u k=%u level=%u base_log=%u limbs=%u", a.N, a.k, a.level, a.base_log,
               a.limbs);
     return -2;
   }
   if (a.num_samples == 0) return 0;
-  return a.resid ? launch2048_t<true>(a) : launch2048_t<false>(a);
+  switch (a.level) {
+    case 1: return a.resid ? launch2048_t<true, 1>(a) : launch2048_t<false, 1>(a);
+    case 2: return a.resid ? launch2048_t<true, 2>(a) : launch2048_t<false, 2>(a);
+    case 3: return a.resid ? launch2048_t<true, 3>(a) : launch2048_t<false, 3>(a);
+    default: return a.resid ? launch2048_t<true, 4>(a) : launch2048_t<false, 4>(a);
+  }
 }
 
 }  // namespace chip

@@ -103,7 +103,7 @@ def limbs_for(N: int) -> int:
     return 3 if N <= 1024 else 8
 
 
-def gpu2048_error_bound(fbsk_gpu: np.ndarray, logB: int = 23) -> float:
+def gpu2048_error_bound(fbsk_gpu: np.ndarray, logB: int = 23, level: int = 1) -> float:
     """Certified bound on |x - round(x)| for the GPU's N = 2048 scheme (concrete_amd/csrc/
     pbs2048.hip).  The products are taken at the square roots +-s_k of the
     N = 1024 evaluation points (P2_PM): each digit polynomial's 1024-point negacyclic spectrum is
@@ -113,7 +113,8 @@ def gpu2048_error_bound(fbsk_gpu: np.ndarray, logB: int = 23) -> float:
     twiddle error mu = 2u (s_k from sincospi, <= 1 ulp per component; the tables are correctly
     rounded).  The digit split on the 16-bit key-limb grid, d = d_lo + 2^16 d_hi (|d_lo| <= 2^15,
     |d_hi| <= 2^(logB-17) + 1), makes output slot m the sum of d_lo g_m + d_hi g_{m-1} over both
-    rows: 4 full N = 2048 products.  fbsk_gpu: the device key (f64 view; K+- = G(+-s) / 1024)."""
+    rows: 4 full N = 2048 products.  level > 1 (logB <= 15): the l levels' whole digits sum into the
+    same slot, dsum = 2 l 2^(logB-1).  fbsk_gpu: the device key (f64 view; K+- = G(+-s) / 1024)."""
     u = 2.0 ** -53
     logM = 10.0
     mu = 2.0 * u
@@ -121,9 +122,12 @@ def gpu2048_error_bound(fbsk_gpu: np.ndarray, logB: int = 23) -> float:
     gamma = logM * eta / (1.0 - logM * eta)
     f = np.asarray(fbsk_gpu, dtype=np.float64).reshape(-1, 2)
     maxG = float(np.max(np.hypot(f[:, 0], f[:, 1]))) * 1024.0
-    dlo = 2.0 ** 15
-    dhi = 2.0 ** max(logB - 17, 0) + 1.0
-    dsum = 2.0 * (dlo + dhi)                    # sum over the 4 products of max |digit|
+    if level > 1:
+        dsum = 2.0 * level * 2.0 ** (logB - 1)  # whole digits of every level, both rows
+    else:
+        dlo = 2.0 ** 15
+        dhi = 2.0 ** max(logB - 17, 0) + 1.0
+        dsum = 2.0 * (dlo + dhi)                # sum over the 4 products of max |digit|
     # forward transform, key rounding, pointwise product and inverse of each product, plus the
     # accumulation and unfold additions: (4 gamma + 5 u), as for the N = 1024 products
     main = np.sqrt(2048.0) * dsum * maxG * (4.0 * gamma + 5.0 * u) * 1.0001

@@ -208,12 +208,12 @@ def test_opt4_full_bit_exact_and_bound(B, oracle, opt4, torch_cuda):
     assert np.array_equal(got[pick], run_oracle(oracle, opt4, cts[pick], acc))
 
 
-@pytest.mark.parametrize("level", [1, 2])
+@pytest.mark.parametrize("level", [1, 2, 3])
 @pytest.mark.parametrize("n", [1, 2, 3])
 def test_tiny_n(B, oracle, torch_cuda, n, level):
     """Blind rotations of 1-3 steps: the key ring's prologue and tail (the last step issues no
     further groups and waits for fewer in flight) meet within one or two steps."""
-    p = replace(B.OPTIMIZER_SETS[4], n=n, level=level, base_log=23 if level == 1 else 15)
+    p = replace(B.OPTIMIZER_SETS[4], n=n, level=level, base_log={1: 23, 2: 15, 3: 12}[level])
     S = Setup(B, oracle, torch_cuda, p, 8400 + 10 * level + n)
     width = 3
     rng = np.random.RandomState(n)
@@ -276,6 +276,39 @@ def test_two_levels_full_row(B, oracle, torch_cuda):
     acc = lut_acc(B, S, table, width)
     got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
     bound = oracle.gpu1024k2_error_bound(B.to_host(S.fbsk).view(np.float64), 15, 2)
+    assert resid < bound < 0.5, (resid, bound)
+    dec = B.lwe_decrypt(S.glwe_sk, got, S.p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+    assert np.array_equal(got[:2], run_oracle(oracle, S, cts[:2], acc))
+
+
+# ---- l = 3 (the rows at log norm2 14-17: br 3/12, n = 742-769) -------------------------------------
+@pytest.mark.parametrize("logB,batch", [(12, 5), (5, 2)])
+def test_three_levels_bit_exact(B, oracle, torch_cuda, logB, batch):
+    S = Setup(B, oracle, torch_cuda, replace(B.OPTIMIZER_SETS[4], n=10, level=3, base_log=logB), 8800 + logB)
+    width = 3
+    rng = np.random.RandomState(logB)
+    msgs = rng.randint(0, 8, size=batch)
+    cts = encrypt(B, S, msgs, width, 75 + logB, std=2.0 ** -30)
+    acc = lut_acc(B, S, rng.randint(0, 8, size=8), width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    assert np.array_equal(got, run_oracle(oracle, S, cts, acc))
+    assert resid < oracle.gpu1024k2_error_bound(B.to_host(S.fbsk).view(np.float64), logB, 3) < 0.5
+
+
+def test_three_levels_full_row(B, oracle, torch_cuda):
+    """The 4-bit row at log norm2 14 (n = 742, br 3/12): 256 samples decrypted, 2 bit-exact, residual
+    under the bound."""
+    S = Setup(B, oracle, torch_cuda, B.PbsParams(n=742, k=2, N=1024, level=3, base_log=12, ks_level=3,
+                                                ks_base_log=4), 8900)
+    width = 4
+    rng = np.random.RandomState(14)
+    table = rng.randint(0, 16, size=16)
+    msgs = rng.randint(0, 16, size=256)
+    cts = encrypt(B, S, msgs, width, 98)
+    acc = lut_acc(B, S, table, width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    bound = oracle.gpu1024k2_error_bound(B.to_host(S.fbsk).view(np.float64), 12, 3)
     assert resid < bound < 0.5, (resid, bound)
     dec = B.lwe_decrypt(S.glwe_sk, got, S.p.big_n)
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]

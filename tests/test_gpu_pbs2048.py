@@ -252,3 +252,74 @@ def test_pbs2048_batch_properties(B, oracle, cfg4, torch_cuda):
     pick = rng.choice(nb, size=8, replace=False)
     ref = run_oracle(oracle, cfg4, cts[pick], acc)
     assert np.array_equal(got[pick], ref)
+
+
+# ---- l = 2 .. 4 (whole digits; the optimizer's 5-bit rows at br 2/15, 3/11, 4/9) -----------------
+LEVEL_ROWS = {2: (15, 783), 3: (11, 784), 4: (9, 761)}  # level -> (logB, an optimizer row's n)
+
+
+def test_fourier_key_2048_levels_layout(B, torch_cuda, oracle):
+    """[n][limb][col][q][row][+-][slot][lane]: level v = l - 1 - q of key polynomial (row, col)."""
+    level = 3
+    S = Setup(B, oracle, torch_cuda, replace(B.CFG4, n=2, level=level, base_log=11), 6500)
+    p = S.p
+    assert B.bsk_format(p) == (2, 4, 16)
+    assert B.fourier_bsk_bytes(p) == p.n * level * 4 * 4 * 2 * 512 * 16
+    got = B.to_host(S.fbsk).view(np.float64).reshape(p.n, 4, 2, level, 2, 2, 8, 64, 2)
+    bsk = S.bsk.reshape(p.n, level, 2, 2, 2048)
+    lane = np.arange(64)
+    K = (lane[None, :] >> 3) + 8 * (lane[None, :] & 7) + 64 * np.arange(8)[:, None]
+    tw = np.exp(1j * np.pi * np.arange(512) / 1024.0)
+    sroot = np.exp(1j * np.pi * (1.0 - 4.0 * K) / 2048.0)
+    worst = 0.0
+    for i in (0, p.n - 1):
+        for li in (0, 3):
+            for col in range(2):
+                for q in range(level):
+                    for row in range(2):
+                        spec = []
+                        for par in range(2):
+                            lv = signed_limb(bsk[i, level - 1 - q, row, col, par::2], li)
+                            spec.append(np.fft.fft((lv[:512] + 1j * lv[512:]) * tw)[K])
+                        for pm, sign in ((0, 1.0), (1, -1.0)):
+                            ref = (spec[0] + sign * sroot * spec[1]) / 1024.0
+                            gg = got[i, li, col, q, row, pm]
+                            worst = max(worst, np.max(np.abs(gg[..., 0] + 1j * gg[..., 1] - ref)) / np.max(np.abs(ref)))
+    assert worst < 1e-13, worst
+
+
+@pytest.mark.parametrize("n", [1, 2, 9])
+@pytest.mark.parametrize("level", [2, 3, 4])
+def test_pbs2048_levels_bit_exact(B, oracle, torch_cuda, level, n):
+    """Bit-exact vs the exact oracle at each level count over ring prologues / tails (n = 1, 2) and a
+    longer rotation, an odd batch, residual under the certified bound."""
+    logB = LEVEL_ROWS[level][0]
+    S = Setup(B, oracle, torch_cuda, replace(B.CFG4, n=n, level=level, base_log=logB), 6600 + 10 * level + n)
+    width = 3
+    rng = np.random.RandomState(level * 10 + n)
+    msgs = rng.randint(0, 8, size=5)
+    cts = encrypt(B, S, msgs, width, 70 + n, std=2.0 ** -30)
+    acc = lut_acc(B, S, rng.randint(0, 8, size=8), width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    assert np.array_equal(got, run_oracle(oracle, S, cts, acc))
+    assert resid < oracle.gpu2048_error_bound(B.to_host(S.fbsk).view(np.float64), logB, level) < 0.5
+
+
+@pytest.mark.parametrize("level", [2, 4])
+def test_pbs2048_levels_full_row(B, oracle, torch_cuda, level):
+    """The 5-bit rows at br 2/15 (n = 783) and 4/9 (n = 761): 256 samples decrypted, 2 bit-exact,
+    residual under the bound."""
+    logB, n = LEVEL_ROWS[level]
+    S = Setup(B, oracle, torch_cuda, replace(B.CFG4, n=n, level=level, base_log=logB), 6700 + level)
+    width = 5
+    rng = np.random.RandomState(level)
+    table = rng.randint(0, 32, size=32)
+    msgs = rng.randint(0, 32, size=256)
+    cts = encrypt(B, S, msgs, width, 90 + level)
+    acc = lut_acc(B, S, table, width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    bound = oracle.gpu2048_error_bound(B.to_host(S.fbsk).view(np.float64), logB, level)
+    assert resid < bound < 0.5, (resid, bound)
+    dec = B.lwe_decrypt(S.glwe_sk, got, S.p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+    assert np.array_equal(got[:2], run_oracle(oracle, S, cts[:2], acc))

@@ -36,7 +36,7 @@ CASES = [
     ("2bit_k6_N256", 6, 256, 16, 1, 18, 2),  # the small-ring kernel since round 4
     ("3bit_k3_N512", 3, 512, 16, 1, 18, 3),
     ("4bit_k2_N1024", 2, 1024, 12, 1, 23, 4),
-    ("k1_N2048_l2", 1, 2048, 12, 2, 10, 3),
+    ("k1_N2048_l2", 1, 2048, 12, 2, 10, 3),  # the N = 2048 kernel's levels since round 4
     ("6bit_k1_N4096", 1, 4096, 6, 1, 22, 6),
     ("7bit_k1_N8192", 1, 8192, 4, 1, 22, 7),
     ("8bit_k1_N16384", 1, 16384, 3, 2, 15, 8),
@@ -62,10 +62,11 @@ CASES = [
     ("1bit_k6_N256_l2", 6, 256, 12, 2, 12, 1),
     ("3bit_k4_N512", 4, 512, 14, 1, 23, 3),  # pbs512k4.hip since round 4 (test_gpu_pbs_small.py)
     # shapes that stay on the general path's two-launch kernels: l = 4 at N = 256 (no table row) and
-    # k = 2, N = 1024, l = 3 (br 3/12)
+    # k = 2, N = 1024, l = 4 (br 4/9)
     ("k5_N256_l4", 5, 256, 12, 4, 7, 2),
-    ("k2_N1024_l3", 2, 1024, 10, 3, 12, 3),
+    ("k2_N1024_l4", 2, 1024, 10, 4, 9, 3),
     ("k6_N256_l4", 6, 256, 10, 4, 8, 1),
+    ("k1_N2048_l5", 1, 2048, 6, 5, 8, 3),  # the general path's N = 2048 four-step kernels
 ]
 
 
@@ -106,7 +107,9 @@ def test_generic_pbs_bit_exact(B, oracle, torch_cuda, case):
     ref, _ = oracle.pbs_batch(op, cts, acc[None, :], bsk=bsk, mode=oracle.MODE_KARATSUBA)
     assert np.array_equal(got, ref), f"{case[0]}: GPU differs from the exact oracle"
     kind, limbs, bits = B.bsk_format(p)
-    if kind == 4:  # k = 2, N = 1024, l = 1 / 2: its own kernel since round 4 (test_gpu_pbs1024k2.py)
+    if kind == 2:  # N = 2048: pbs2048.hip (test_gpu_pbs2048.py)
+        bound = oracle.gpu2048_error_bound(B.to_host(fbsk).view(np.float64), p.base_log, p.level)
+    elif kind == 4:  # k = 2, N = 1024, l = 1 / 2: its own kernel since round 4 (test_gpu_pbs1024k2.py)
         bound = oracle.gpu1024k2_error_bound(B.to_host(fbsk).view(np.float64), p.base_log, p.level)
     elif kind == 5:  # N = 512, k = 3 / 4, N = 256, k = 5 / 6, l = 1: pbs_small.hip, pbs512k4.hip
         bound = oracle.gpu_small_error_bound(B.to_host(fbsk).view(np.float64), p.N, p.k, p.base_log, p.level)

@@ -104,6 +104,11 @@ def test_key_formats_and_exact_range():
     assert L.concrete_hip_fourier_bsk_size_bytes(742, 1, 1, 2048) == 742 * 4 * 4 * 1024 * 16
     assert L.concrete_hip_pbs_supported(1, 2048, 1, 24) == 1
     assert L.concrete_hip_pbs_supported(1, 2048, 1, 25) == 1  # past the cfg4 kernel: the general path
+    # l = 2 .. 4: the same kernel with whole-digit levels (l 2^(logB-1) <= 2^15), format code 2
+    assert fmt(1, 2048, 2) == (2, 4, 16) and fmt(1, 2048, 4) == (2, 4, 16) and fmt(1, 2048, 5)[0] == 3
+    assert L.concrete_hip_fourier_bsk_size_bytes(783, 1, 2, 2048) == 783 * 2 * 4 * 4 * 1024 * 16
+    assert L.concrete_hip_pbs_supported(1, 2048, 2, 15) == 1 and L.concrete_hip_pbs_supported(1, 2048, 4, 9) == 1
+    assert L.concrete_hip_pbs_supported(1, 2048, 2, 16) == 1  # past the levels gate: the companion key
     # the general-format key of the hand-tuned shapes (wide digits): its own limbs
     assert L.concrete_hip_generic_bsk_size_bytes(10, 1, 1, 2048) > 0
     assert L.concrete_hip_generic_bsk_size_bytes(10, 1, 1, 32768) > 0  # N = 2^15: the split path (round 4)
@@ -112,6 +117,8 @@ def test_key_formats_and_exact_range():
     # 4 limbs of 16 bits, the digit split on the limb grid as at N = 2048
     assert fmt(2, 1024, 1) == (4, 4, 16) and fmt(2, 1024, 2) == (4, 4, 16)
     assert L.concrete_hip_pbs_supported(2, 1024, 2, 15) == 1  # two levels: whole digits up to 15 bits
+    assert fmt(2, 1024, 3) == (4, 4, 16) and fmt(2, 1024, 4)[0] == 3  # l = 3 (br 3/12); l = 4: general
+    assert L.concrete_hip_pbs_supported(2, 1024, 3, 12) == 1
     assert L.concrete_hip_fourier_bsk_size_bytes(801, 2, 1, 1024) == 801 * 4 * 9 * 512 * 16
     assert L.concrete_hip_pbs_supported(2, 1024, 1, 24) == 1
     assert L.concrete_hip_generic_error_bound(2, 1024, 1, 23, 0.0) == -1.0
@@ -131,8 +138,8 @@ def test_key_formats_and_exact_range():
     assert L.concrete_hip_fourier_bsk_size_bytes(722, 3, 1, 512) == 722 * 4 * 16 * 256 * 16
     assert L.concrete_hip_pbs_supported(3, 512, 1, 24) == 1 and L.concrete_hip_pbs_supported(5, 256, 1, 15) == 1
     assert L.concrete_hip_pbs_supported(5, 256, 1, 25) == 1  # past the small-ring gate: the general path
-    for k, N, l, logB in [(6, 256, 4, 8), (4, 512, 2, 16), (2, 1024, 3, 12), (1, 4096, 1, 22),
-                          (1, 8192, 1, 22), (1, 16384, 2, 15), (1, 2048, 2, 10)]:
+    for k, N, l, logB in [(6, 256, 4, 8), (4, 512, 2, 16), (2, 1024, 4, 9), (1, 4096, 1, 22),
+                          (1, 8192, 1, 22), (1, 16384, 2, 15), (1, 2048, 5, 8)]:
         kind, limbs, bits = fmt(k, N, l)
         assert kind == 3 and limbs * bits >= 64, (k, N, l)
         assert L.concrete_hip_pbs_supported(k, N, l, logB) == 1, (k, N, l, logB)

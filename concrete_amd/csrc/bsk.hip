@@ -255,7 +255,7 @@ __global__ void __launch_bounds__(256) convert_bsk1024k2_kernel(cplx* __restrict
 // order), folded, twisted by zeta_2N^j and transformed (M = N / 2 points), scaled 1 / (512 P) with
 // P = 1024 / N (the kernels' unnormalised unzip and zip), element e = (slot, lane) at frequency
 // fft512_freq(lane, slot).
-template <int N, int K1>
+template <int N, int K1, int LIMBS = SM_LIMBS>
 __global__ void __launch_bounds__(256) convert_bsk_small_kernel(cplx* __restrict__ dest,
                                                                const uint64_t* __restrict__ src,
                                                                const ddc* __restrict__ zeta_t,
@@ -273,12 +273,12 @@ __global__ void __launch_bounds__(256) convert_bsk_small_kernel(cplx* __restrict
   t /= level;
   const uint32_t cg = (uint32_t)(t % NCG);
   t /= NCG;
-  const uint32_t limb = (uint32_t)(t % SM_LIMBS);
-  const uint64_t i = t / SM_LIMBS;
+  const uint32_t limb = (uint32_t)(t % LIMBS);
+  const uint64_t i = t / LIMBS;
   const uint32_t col = cg * GC + c2, v = level - 1 - q;
   const uint64_t* g = src + (((i * level + v) * K1 + row) * K1 + col) * N;  // [n][l][row][col][N]
   for (int j = threadIdx.x; j < M; j += blockDim.x) {
-    ddc z{dd_from(limb_value<SM_LIMBS>(g[j], limb)), dd_from(limb_value<SM_LIMBS>(g[j + M], limb))};
+    ddc z{dd_from(limb_value<LIMBS>(g[j], limb)), dd_from(limb_value<LIMBS>(g[j + M], limb))};
     z = ddc_mul(z, zeta_t[j]);
     const int r = (int)(__builtin_bitreverse32((uint32_t)j) >> (32 - LOGM));
     buf[r] = z;
@@ -348,7 +348,7 @@ int convert_bsk_launch(const ConvertArgs& a) {
   const bool n2048 =
       a.N == 2048 && a.k == 1 && a.limbs == (uint32_t)PBS2_LIMBS && a.level >= 1 && a.level <= PBS2_MAX_LEVEL;
   const bool k2 = a.N == 1024 && a.k == 2 && a.limbs == (uint32_t)K2_LIMBS && a.level >= 1 && a.level <= K2_MAX_LEVEL;
-  const bool small = pbs_small_shape(a.k, a.N, a.level) && a.limbs == (uint32_t)SM_LIMBS;
+  const bool small = pbs_small_shape(a.k, a.N, a.level) && a.limbs == small_limbs(a.k, a.N, a.level);
   if (!n1024 && !n2048 && !k2 && !small) {
     set_error("unsupported BSK conversion parameters: N=%u k=%u level=%u limbs=%u", a.N, a.k, a.level, a.limbs);
     return -2;
@@ -377,10 +377,13 @@ int convert_bsk_launch(const ConvertArgs& a) {
       rc = -1;
     }
   } else if (small) {
-    const uint64_t blocks = (uint64_t)a.n * SM_LIMBS * (a.k + 1) * (a.k + 1) * a.level;
+    const uint64_t blocks = (uint64_t)a.n * a.limbs * (a.k + 1) * (a.k + 1) * a.level;
     if (a.N == 512 && a.k == 3)
       hipLaunchKernelGGL((convert_bsk_small_kernel<512, 4>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
                          reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level);
+    else if (a.N == 512 && a.limbs == K4_L2_LIMBS)
+      hipLaunchKernelGGL((convert_bsk_small_kernel<512, 5, K4_L2_LIMBS>), dim3((uint32_t)blocks), dim3(256), 0,
+                         a.stream, reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level);
     else if (a.N == 512)
       hipLaunchKernelGGL((convert_bsk_small_kernel<512, 5>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
                          reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level);

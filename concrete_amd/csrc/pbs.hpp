@@ -106,9 +106,10 @@ constexpr size_t pbs_small_lds_bytes(int N, int K1) {
 // N = 512, k = 4 (pbs512k4.hip): the same key format and packing; five polynomials make three packed
 // transforms: four waves per ciphertext (three transform owners, one slot each), K4_CTS ciphertexts per
 // workgroup and a ring of K4_RING_SLOTS 20 KB key groups.  l = 1 (logB <= 24) or l = 3 .. K4_MAX_LEVEL
-// whole digits with l 2^(logB-1) <= 2^15 (the l = 1, logB = 16 magnitude: certified bound 0.35).  Not
-// l = 2: the optimizer's k = 4, N = 512, l = 2 rows have logB = 16 (bound 0.69), and the key format
-// depends on (k, N, l) only, so that shape keeps the general path's format.
+// whole digits with l 2^(logB-1) <= 2^15 (the l = 1, logB = 16 magnitude: certified bound 0.35).
+// l = 2: the optimizer's rows have logB = 16, where two whole digits against 16-bit limbs would put the
+// bound at 0.69, so that shape's key has five 13-bit limbs (bound 0.09; the format depends on (k, N, l)
+// only, so the whole shape takes it).
 constexpr int K4_CTS = 2;
 constexpr int K4_RING_SLOTS = 4;
 constexpr uint32_t K4_MAX_LEVEL = 5;
@@ -117,12 +118,19 @@ constexpr size_t pbs512k4_lds_bytes() {
          3 * K4_CTS * 4;
 }
 inline bool pbs_small_shape(uint32_t k, uint32_t N, uint32_t level) {
-  if (N == 512 && k == 4) return level == 1 || (level >= 3 && level <= K4_MAX_LEVEL);
+  if (N == 512 && k == 4) return level >= 1 && level <= K4_MAX_LEVEL;
   return level >= 1 && level <= SM_MAX_LEVEL && ((N == 512 && k == 3) || (N == 256 && (k == 5 || k == 6)));
+}
+// key limbs of a small-ring key: 4 of 16 bits, 5 of 13 bits at k = 4, N = 512, l = 2 (K4_L2_LIMBS)
+constexpr uint32_t K4_L2_LIMBS = 5;
+inline uint32_t small_limbs(uint32_t k, uint32_t N, uint32_t level) {
+  return N == 512 && k == 4 && level == 2 ? K4_L2_LIMBS : (uint32_t)SM_LIMBS;
 }
 inline bool pbs_small_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
   if (!pbs_small_shape(k, N, level) || base_log < 1) return false;
   if (level == 1) return base_log <= pbs_small_max_logb(N);
+  // 13-bit limbs: two whole digits up to 16 bits (certified bound 0.09 on the table rows' keys)
+  if (small_limbs(k, N, level) == K4_L2_LIMBS) return base_log <= 16;
   return base_log <= 15 && ((uint64_t)level << (base_log - 1)) <= (1ull << 15);
 }
 

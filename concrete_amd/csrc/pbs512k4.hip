@@ -29,8 +29,12 @@ namespace chip {
 
 namespace {
 
-constexpr uint64_t K4_MAGIC_ALL =
-    RND_MAGIC_BITS + (RND_MAGIC_BITS << 16) + (RND_MAGIC_BITS << 32) + (RND_MAGIC_BITS << 48);
+// sum over the key limbs of the rounding constant at each limb's shift (LB bits per limb)
+constexpr uint64_t k4_magic_all(int limbs, int lb) {
+  uint64_t m = 0;
+  for (int li = 0; li < limbs; ++li) m += RND_MAGIC_BITS << (lb * li);
+  return m;
+}
 
 // the four waves of one ciphertext (counters f[ct * 4 + role]): publish how many sync points this
 // wave has passed; wait until the other three have reached a count.  LDS traffic is drained, the key
@@ -56,7 +60,9 @@ __device__ __forceinline__ void k4_sync(uint32_t* f, int ctl, int role, uint32_t
 // SUBS = 2, NQ = 1: one digit split into d_lo + 2^16 d_hi (16 < logB <= 24); SUBS = 1: NQ = l whole
 // digits (logB <= 15; l = 1, 3, 4, 5: pbs.hpp K4_MAX_LEVEL), each level's products landing in the same slot (the key holds the levels,
 // [n][limb][col][q][row][M], one ring group per level).
-template <int SUBS, int NQ, bool RESID>
+// LIMBS = 4 balanced 16-bit key limbs, or 5 of 13 bits (l = 2 at logB = 16: two whole 16-bit digits
+// against 16-bit limbs would put the certified bound at 0.69; 13-bit limbs cut the key spectra 8x).
+template <int SUBS, int NQ, int LIMBS, bool RESID>
 __global__ void __launch_bounds__(K4_CTS * 256, 1)
 pbs512k4_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx,
                 const uint64_t* __restrict__ luts, const uint64_t* __restrict__ lut_idx,
@@ -68,7 +74,10 @@ pbs512k4_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx
   constexpr int SL = 4;                     // spectrum slots per polynomial (two per transform)
   constexpr int NW = 4 * K4_CTS;            // waves per workgroup
   constexpr int GROUP = K1 * M;             // (limb, column): the five row spectra
-  constexpr int NGRP = SM_LIMBS * K1 * NQ;  // ring groups per CMUX step
+  constexpr int LB = LIMBS == 4 ? 16 : 13;  // limb grid: limb li at 2^{LB li} (the last of 5: 12 bits)
+  static_assert(LIMBS == 4 || (LIMBS == 5 && SUBS == 1), "sub-digits need the 16-bit grid");
+  constexpr uint64_t MAGIC_ALL = k4_magic_all(LIMBS, LB);
+  constexpr int NGRP = LIMBS * K1 * NQ;     // ring groups per CMUX step
   constexpr int NF = SUBS * NQ;             // forward transforms per step (sub-digits or levels)
   static_assert(SUBS == 1 || NQ == 1, "sub-digits or levels");
   using StT = std::conditional_t<(NQ > 1), uint64_t, uint32_t>;  // decomposition state (l logB bits)
@@ -77,7 +86,7 @@ pbs512k4_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx
   constexpr int GLDS = 4;                   // 1 KB LDS-DMA pieces per issuing wave per group
   constexpr int NISS = GROUP / 64 / GLDS;   // waves 0 .. NISS - 1 issue a group's pieces
   static_assert(GROUP / 64 == GLDS * NISS && NISS <= NW, "ring geometry");
-  static_assert(NGRP % RS == 0 && DIST <= 3, "ring geometry");
+  static_assert(NGRP % 2 == 0 && RS == 4 && DIST <= 3, "ring geometry");
   constexpr int XS = (int)PBS1024_XCH_SLOTS;
   static_assert(XCH_SLOTS <= XS && 2 * N * 8 <= XS * 16, "scratch");
 
@@ -107,10 +116,15 @@ pbs512k4_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx
   const cplx* key_w = fbsk + (uint64_t)(issuer ? w : 0) * GLDS * 64;
   cplx* ring_w = ring + (issuer ? w : 0) * GLDS * 64;
   const uint32_t lane_b = (uint32_t)lane * (uint32_t)sizeof(cplx);
-  auto issue_group = [&](const cplx* key_step, int r) __attribute__((always_inline)) {
+  // group r of step i (r may run past NGRP into step i + 1) sits in ring slot (i NGRP + r) % RS:
+  // with NGRP % RS == 0 a compile-time constant, else (NGRP even, RS = 4) the step's parity adds 2
+  auto slot_of = [&](uint32_t i, int r) __attribute__((always_inline)) {
+    return NGRP % RS == 0 ? r % RS : (int)((i * (uint32_t)NGRP + (uint32_t)r) & (RS - 1));
+  };
+  auto issue_group = [&](const cplx* key_step, uint32_t i, int r) __attribute__((always_inline)) {
     if (!issuer) return;
     const char* src = reinterpret_cast<const char*>(key_step + r * GROUP);
-    cplx* dst = ring_w + (r % RS) * GROUP;
+    cplx* dst = ring_w + slot_of(i, r) * GROUP;
 #pragma unroll
     for (int j = 0; j < GLDS; ++j)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const cplx*>(src + j * 1024 + lane_b),
@@ -118,7 +132,7 @@ pbs512k4_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx
   };
   if (n > 0) {
 #pragma unroll
-    for (int g = 0; g < DIST; ++g) issue_group(key_w, g);
+    for (int g = 0; g < DIST; ++g) issue_group(key_w, 0u, g);
   }
 
   build_fft512_tables(tbl, threadIdx.x, NW * 64);
@@ -255,10 +269,10 @@ pbs512k4_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx
     cplx Yc[K1];
 #pragma unroll
     for (int cc = 0; cc < K1; ++cc) Yc[cc] = {0.0, 0.0};
-    static_for<0, SM_LIMBS>([&](auto LI) __attribute__((always_inline)) {
+    static_for<0, LIMBS>([&](auto LI) __attribute__((always_inline)) {
       constexpr int li = decltype(LI)::value;
       if constexpr (NQ == 1) {
-        constexpr bool HI = SUBS == 2 && li + 1 < SM_LIMBS;  // d_hi g_3 lands at 2^64: vanishes
+        constexpr bool HI = SUBS == 2 && li + 1 < LIMBS;  // d_hi g_3 lands at 2^64: vanishes
         cplx Yn[K1];
 #pragma unroll
         for (int cc = 0; cc < K1; ++cc) Yn[cc] = {0.0, 0.0};
@@ -273,8 +287,7 @@ pbs512k4_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx
             else wait_vmcnt<GLDS * 2>();
           }
           pair_barrier();  // ... for every wave; everyone is done with group r - 1
-          if (r + DIST < NGRP) issue_group(key_step, r + DIST);
-          else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
+          if (r + DIST < NGRP || !last_step) issue_group(key_step, i, r + DIST);
           if constexpr (li == 0) {
             if (cc == 0) {
 #pragma unroll
@@ -282,7 +295,7 @@ pbs512k4_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx
             }
           }
           cplx Ya = Yc[cc];
-          const cplx* G = ring + (r % RS) * GROUP + role * 64 + lane;
+          const cplx* G = ring + slot_of(i, r) * GROUP + role * 64 + lane;
 #pragma unroll
           for (int row = 0; row < K1; ++row) {
             const cplx g = G[row * M];
@@ -320,15 +333,14 @@ pbs512k4_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx
               else wait_vmcnt<GLDS * 2>();
             }
             pair_barrier();
-            if (r + DIST < NGRP) issue_group(key_step, r + DIST);
-            else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
+            if (r + DIST < NGRP || !last_step) issue_group(key_step, i, r + DIST);
             if constexpr (li == 0) {
               if (cc == 0 && q == 0) {  // the last level's spectra (published by this barrier)
 #pragma unroll
                 for (int row = 0; row < K1; ++row) X[row][NF - 1] = myslot[(row >> 1) * XS + (row & 1) * SL * 64];
               }
             }
-            const cplx* G = ring + (r % RS) * GROUP + role * 64 + lane;
+            const cplx* G = ring + slot_of(i, r) * GROUP + role * 64 + lane;
 #pragma unroll
             for (int row = 0; row < K1; ++row) {
               const cplx g = G[row * M];
@@ -371,11 +383,11 @@ pbs512k4_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx
           max_resid = fmax(max_resid, fabs(V[m].im - (ti - RND_MAGIC)));
         }
         if constexpr (li == 0) {
-          A[m] += (uint64_t)__double_as_longlong(tr) - K4_MAGIC_ALL;
-          A[m + 8] += (uint64_t)__double_as_longlong(ti) - K4_MAGIC_ALL;
+          A[m] += (uint64_t)__double_as_longlong(tr) - MAGIC_ALL;
+          A[m + 8] += (uint64_t)__double_as_longlong(ti) - MAGIC_ALL;
         } else {
-          A[m] += (uint64_t)__double_as_longlong(tr) << (16 * li);
-          A[m + 8] += (uint64_t)__double_as_longlong(ti) << (16 * li);
+          A[m] += (uint64_t)__double_as_longlong(tr) << (LB * li);
+          A[m + 8] += (uint64_t)__double_as_longlong(ti) << (LB * li);
         }
       }
 #pragma unroll
@@ -409,10 +421,10 @@ pbs512k4_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx
   }
 }
 
-template <int SUBS, int NQ, bool RESID>
+template <int SUBS, int NQ, int LIMBS, bool RESID>
 static int launch_k4_t(const PbsArgs& a) {
   const size_t lds = pbs512k4_lds_bytes();
-  auto kern = pbs512k4_kernel<SUBS, NQ, RESID>;
+  auto kern = pbs512k4_kernel<SUBS, NQ, LIMBS, RESID>;
   CHIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const uint32_t blocks = (a.num_samples + K4_CTS - 1) / K4_CTS;
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(K4_CTS * 256), lds, a.stream, a.out, a.out_idx, a.luts, a.lut_idx,
@@ -426,13 +438,14 @@ static int launch_k4_t(const PbsArgs& a) {
   return 0;
 }
 
-template <int SUBS, int NQ>
+template <int SUBS, int NQ, int LIMBS = 4>
 static int launch_k4_r(const PbsArgs& a) {
-  return a.resid ? launch_k4_t<SUBS, NQ, true>(a) : launch_k4_t<SUBS, NQ, false>(a);
+  return a.resid ? launch_k4_t<SUBS, NQ, LIMBS, true>(a) : launch_k4_t<SUBS, NQ, LIMBS, false>(a);
 }
 
 int pbs512k4_launch(const PbsArgs& a) {
-  if (!(a.N == 512 && a.k == 4 && a.limbs == (uint32_t)SM_LIMBS && pbs_small_ok(a.k, a.N, a.level, a.base_log))) {
+  if (!(a.N == 512 && a.k == 4 && a.limbs == small_limbs(a.k, a.N, a.level) &&
+        pbs_small_ok(a.k, a.N, a.level, a.base_log))) {
     set_error("unsupported PBS parameters: N=%u k=%u level=%u base_log=%u limbs=%u", a.N, a.k, a.level, a.base_log,
               a.limbs);
     return -2;
@@ -441,6 +454,7 @@ int pbs512k4_launch(const PbsArgs& a) {
   switch (a.level) {
     // logB <= 15: |digit| <= 2^14 fits the 16-bit grid whole (one sub-digit)
     case 1: return a.base_log <= 15 ? launch_k4_r<1, 1>(a) : launch_k4_r<2, 1>(a);
+    case 2: return launch_k4_r<1, 2, 5>(a);  // 13-bit key limbs
     case 3: return launch_k4_r<1, 3>(a);
     case 4: return launch_k4_r<1, 4>(a);
     default: return launch_k4_r<1, 5>(a);

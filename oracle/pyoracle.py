@@ -170,8 +170,9 @@ def gpu_small_error_bound(fbsk_gpu: np.ndarray, N: int, k: int, logB: int, level
     stages, and its error is relative to the norm of all P polynomials together: the 2-norm factor
     is sqrt(P N) = 32 instead of sqrt(N).  Digits on the 16-bit limb grid as in pbs1024k2.hip
     (logB <= 15: one sub-digit, |d| <= 2^(logB-1)); level > 1 (pbs512k4.hip, logB <= 15): the l
-    levels' whole digits sum into the same slot, dsum = (k + 1) l 2^(logB-1).  fbsk_gpu: the device
-    key (f64 view; spectra scaled by 1 / (512 P))."""
+    levels' whole digits sum into the same slot, dsum = (k + 1) l 2^(logB-1) (k = 4, l = 2: 13-bit key
+    limbs, which the measured key spectrum carries).  fbsk_gpu: the device key (f64 view; spectra
+    scaled by 1 / (512 P))."""
     u = 2.0 ** -53
     P = 1024 // N
     logM = 9.0 + np.log2(P) + 1.0
@@ -180,10 +181,9 @@ def gpu_small_error_bound(fbsk_gpu: np.ndarray, N: int, k: int, logB: int, level
     gamma = logM * eta / (1.0 - logM * eta)
     f = np.asarray(fbsk_gpu, dtype=np.float64).reshape(-1, 2)
     maxG = float(np.max(np.hypot(f[:, 0], f[:, 1]))) * 512.0 * P
-    if logB <= 15:
+    if logB <= 15 or level > 1:  # whole digits (level > 1: pbs512k4.hip's l = 2 reaches logB 16)
         dmax = 2.0 ** (logB - 1) * level
     else:
-        assert level == 1
         dmax = 2.0 ** 15 + 2.0 ** max(logB - 17, 0) + 1.0
     dsum = (k + 1) * dmax
     main = np.sqrt(1024.0) * dsum * maxG * (4.0 * gamma + 5.0 * u) * 1.0001

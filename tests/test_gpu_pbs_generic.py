@@ -53,10 +53,9 @@ CASES = [
     ("9bit_k1_N32768", 1, 32768, 2, 2, 15, 9),
     ("10bit_k1_N65536", 1, 65536, 2, 2, 14, 10),
     # round 4: the 1- to 4-bit log-norm2-0 rows above run on their own kernels (pbs_small.hip,
-    # pbs1024k2.hip), and so do the small-ring rows at l = 2, 3 whose digits fit whole (the next two);
-    # k = 4, N = 512, l = 2 (logB = 16) stays on the general path (its two-launch kernels; the tile
-    # kernels serve the general-format key of the shapes above,
-    # test_generic_tile_kernels_on_the_general_format_key)
+    # pbs1024k2.hip), and so do the small-ring rows at l = 2, 3 whose digits fit whole and k = 4,
+    # N = 512, l = 2 on 13-bit key limbs (the next three; the tile kernels serve the general-format
+    # key of the shapes above, test_generic_tile_kernels_on_the_general_format_key)
     ("3bit_k4_N512_l2", 4, 512, 12, 2, 16, 3),
     ("2bit_k5_N256_l2", 5, 256, 16, 2, 10, 2),
     ("1bit_k6_N256_l2", 6, 256, 12, 2, 12, 1),
@@ -67,6 +66,7 @@ CASES = [
     ("k2_N1024_l4", 2, 1024, 10, 4, 9, 3),
     ("k6_N256_l4", 6, 256, 10, 4, 8, 1),
     ("k1_N2048_l5", 1, 2048, 6, 5, 8, 3),  # the general path's N = 2048 four-step kernels
+    ("k4_N512_l6", 4, 512, 8, 6, 7, 2),  # the general path's two-launch kernels at N = 512
 ]
 
 
@@ -122,7 +122,7 @@ def test_generic_pbs_bit_exact(B, oracle, torch_cuda, case):
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
 
 
-@pytest.mark.parametrize("ci", [19, 15, 21, 5], ids=[CASES[i][0] for i in (19, 15, 21, 5)])
+@pytest.mark.parametrize("ci", [19, 23, 21, 5], ids=[CASES[i][0] for i in (19, 23, 21, 5)])
 def test_generic_tile_many_workgroups(B, oracle, torch_cuda, ci):
     """The general path over many ciphertexts (67: not a multiple of any workgroup's ciphertext
     count, so the last workgroup runs empty slots): small-ring shapes off the hand-tuned kernels and the
@@ -152,7 +152,7 @@ def test_generic_8bit_long_chain_decrypts(B, oracle, torch_cuda):
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
 
 
-@pytest.mark.parametrize("ci", [19, 15, 21, 20], ids=[CASES[i][0] for i in (19, 15, 21, 20)])
+@pytest.mark.parametrize("ci", [19, 23, 21, 20], ids=[CASES[i][0] for i in (19, 23, 21, 20)])
 def test_generic_index_arrays(B, oracle, torch_cuda, ci):
     """Mapped LUTs and permuted input/output rows (GPUDFG.cpp:1149-1205) on the general path:
     the one-launch tile kernels (N = 256: 4 ciphertexts per workgroup, the last one partly

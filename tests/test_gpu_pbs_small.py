@@ -275,7 +275,19 @@ def test_tiny_n(B, oracle, torch_cuda, shape, n):
 
 
 # ---- N = 512, k = 4 at l = 3 .. 5 (pbs512k4.hip's levels: the rows at br 3/12, 4/9, 5/8) ----------
-K4_LEVEL_ROWS = {3: (12, 700), 4: (9, 702), 5: (8, 689)}  # level -> (logB, a 3-bit optimizer row's n)
+K4_LEVEL_ROWS = {2: (16, 700), 3: (12, 700), 4: (9, 702), 5: (8, 689)}  # level -> (logB, a 3-bit row's n)
+
+
+def limb13(x, limb):
+    """Balanced limb of u64 values on the 5-limb grid (13, 13, 13, 13, 12 bits; bsk.hip limb_value)."""
+    rem = x.astype(np.uint64).copy()
+    val = None
+    for t in range(limb + 1):
+        w = 13 if t < 4 else 12
+        vv = (rem & np.uint64((1 << w) - 1)).astype(np.int64)
+        val = np.where(vv >= (1 << (w - 1)), vv - (1 << w), vv)
+        rem = (rem - val.astype(np.uint64)) >> np.uint64(w)
+    return val.astype(np.float64)
 
 
 def k4_level_setup(B, oracle, torch, level, n, seed):
@@ -287,26 +299,29 @@ def k4_level_setup(B, oracle, torch, level, n, seed):
     return _cache[key]
 
 
-@pytest.mark.parametrize("level", [3, 4, 5])
+@pytest.mark.parametrize("level", [2, 3, 4, 5])
 def test_k4_levels_key_layout(B, oracle, torch_cuda, level):
-    """[n][limb][col][q][row][slot][lane]: level v = l - 1 - q of key polynomial (row, col)."""
+    """[n][limb][col][q][row][slot][lane]: level v = l - 1 - q of key polynomial (row, col); at l = 2
+    five 13-bit limbs."""
     S = k4_level_setup(B, oracle, torch_cuda, level, 3, 9600 + level)
     p = S.p
     K1, M, N = 5, 256, 512
-    assert B.bsk_format(p) == (5, 4, 16)
-    assert B.fourier_bsk_bytes(p) == p.n * level * 4 * 25 * M * 16
-    got = B.to_host(S.fbsk).view(np.float64).reshape(p.n, 4, K1, level, K1, 4, 64, 2)
+    L = 5 if level == 2 else 4
+    assert B.bsk_format(p) == ((5, 5, 13) if level == 2 else (5, 4, 16))
+    assert B.fourier_bsk_bytes(p) == p.n * level * L * 25 * M * 16
+    got = B.to_host(S.fbsk).view(np.float64).reshape(p.n, L, K1, level, K1, 4, 64, 2)
     bsk = S.bsk.reshape(p.n, level, K1, K1, N)
     lane = np.arange(64)
     K = (lane[None, :] >> 3) + 8 * (lane[None, :] & 7) + 64 * np.arange(4)[:, None]
     tw = np.exp(1j * np.pi * np.arange(M) / N)
     worst = 0.0
     for i in (0, p.n - 1):
-        for li in (0, 3):
+        for li in (0, L - 1):
             for col in (0, 4):
                 for q in range(level):
                     for row in (0, 3):
-                        lv = signed_limb(bsk[i, level - 1 - q, row, col], li)
+                        src = bsk[i, level - 1 - q, row, col]
+                        lv = limb13(src, li) if L == 5 else signed_limb(src, li)
                         ref = np.fft.fft((lv[:M] + 1j * lv[M:]) * tw)[K] / 1024.0
                         gg = got[i, li, col, q, row]
                         worst = max(worst, np.max(np.abs(gg[..., 0] + 1j * gg[..., 1] - ref)) / np.max(np.abs(ref)))
@@ -314,7 +329,7 @@ def test_k4_levels_key_layout(B, oracle, torch_cuda, level):
 
 
 @pytest.mark.parametrize("n", [1, 2, 9])
-@pytest.mark.parametrize("level", [3, 4, 5])
+@pytest.mark.parametrize("level", [2, 3, 4, 5])
 def test_k4_levels_bit_exact(B, oracle, torch_cuda, level, n):
     """Bit-exact vs the exact oracle over ring prologues / tails (n = 1, 2) and a longer rotation, odd
     batch (the last workgroup's second ciphertext empty), residual under the certified bound."""
@@ -329,9 +344,9 @@ def test_k4_levels_bit_exact(B, oracle, torch_cuda, level, n):
     assert resid < bound(B, oracle, S) < 0.5
 
 
-@pytest.mark.parametrize("level", [3, 5])
+@pytest.mark.parametrize("level", [2, 3, 5])
 def test_k4_levels_full_row(B, oracle, torch_cuda, level):
-    """The full 3-bit rows (br 3/12 n = 700, br 5/8 n = 689): 256 samples decrypted, 2 bit-exact, residual
+    """The full 3-bit rows (br 2/16 n = 700, br 3/12 n = 700, br 5/8 n = 689): 256 samples decrypted, 2 bit-exact, residual
     under the bound."""
     S = k4_level_setup(B, oracle, torch_cuda, level, K4_LEVEL_ROWS[level][1], 9800 + level)
     width = 3

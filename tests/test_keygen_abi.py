@@ -128,17 +128,19 @@ def test_key_formats_and_exact_range():
     assert fmt(3, 512, 1) == (5, 4, 16) and fmt(5, 256, 1) == (5, 4, 16) and fmt(6, 256, 1) == (5, 4, 16)
     assert fmt(4, 512, 1) == (5, 4, 16) and L.concrete_hip_pbs_supported(4, 512, 1, 23) == 1
     # levels on the small-ring kernels: whole digits with l 2^(logB-1) <= 2^15 (pbs.hpp pbs_small_ok);
-    # k = 4, N = 512, l = 2 keeps the general format (its rows have logB = 16)
+    # k = 4, N = 512, l = 2 (logB = 16 rows): five 13-bit key limbs
     for k, N, l in [(5, 256, 2), (6, 256, 3), (3, 512, 3), (4, 512, 3), (4, 512, 5)]:
         assert fmt(k, N, l) == (5, 4, 16), (k, N, l)
-    assert fmt(4, 512, 2)[0] == 3 and fmt(5, 256, 4)[0] == 3 and fmt(4, 512, 6)[0] == 3
+    assert fmt(4, 512, 2) == (5, 5, 13) and fmt(5, 256, 4)[0] == 3 and fmt(4, 512, 6)[0] == 3
+    assert L.concrete_hip_fourier_bsk_size_bytes(700, 4, 2, 512) == 700 * 2 * 5 * 25 * 256 * 16
+    assert L.concrete_hip_pbs_supported(4, 512, 2, 16) == 1
     assert L.concrete_hip_fourier_bsk_size_bytes(700, 4, 3, 512) == 700 * 3 * 4 * 25 * 256 * 16
     assert L.concrete_hip_pbs_supported(6, 256, 3, 9) == 1 and L.concrete_hip_pbs_supported(4, 512, 5, 8) == 1
     assert L.concrete_hip_pbs_supported(6, 256, 3, 15) == 1  # past the levels gate: the companion key
     assert L.concrete_hip_fourier_bsk_size_bytes(722, 3, 1, 512) == 722 * 4 * 16 * 256 * 16
     assert L.concrete_hip_pbs_supported(3, 512, 1, 24) == 1 and L.concrete_hip_pbs_supported(5, 256, 1, 15) == 1
     assert L.concrete_hip_pbs_supported(5, 256, 1, 25) == 1  # past the small-ring gate: the general path
-    for k, N, l, logB in [(6, 256, 4, 8), (4, 512, 2, 16), (2, 1024, 4, 9), (1, 4096, 1, 22),
+    for k, N, l, logB in [(6, 256, 4, 8), (4, 512, 8, 5), (2, 1024, 4, 9), (1, 4096, 1, 22),
                           (1, 8192, 1, 22), (1, 16384, 2, 15), (1, 2048, 5, 8)]:
         kind, limbs, bits = fmt(k, N, l)
         assert kind == 3 and limbs * bits >= 64, (k, N, l)

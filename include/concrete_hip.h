@@ -141,9 +141,11 @@ uint64_t concrete_hip_fourier_bsk_size_bytes(uint32_t input_lwe_dim, uint32_t gl
 int concrete_hip_convert_bsk(void *stream, uint32_t gpu_index, void *dest_fourier, const void *src,
                              int src_is_device, uint32_t input_lwe_dim, uint32_t glwe_dim, uint32_t level_count,
                              uint32_t polynomial_size);
-/* Wide digits.  A (k, N, l) with a hand-tuned kernel (k = 1, N = 1024 / 2048) accepts only digits
- * that kernel keeps exact (N = 1024: (k+1) l 2^logB <= 4096; N = 2048: logB <= 24); wider ones run
- * on the general path (pbs_generic.hip), which needs the key in its own format.  Keys converted
+/* Wide digits.  A (k, N, l) with a hand-tuned kernel (concrete_hip_bsk_format code 1, 2, 4 or 5)
+ * accepts only digits that kernel keeps exact (k = 1, N = 1024: (k+1) l 2^logB <= 4096; l = 1 on the
+ * 16-bit-limb kernels: logB <= 24; whole-digit levels: l 2^(logB-1) <= 2^15, or logB <= 16 on the
+ * 13-bit-limb key of k = 4, N = 512, l = 2); wider ones run on the general path (pbs_generic.hip),
+ * which needs the key in its own format.  Keys converted
  * through a keyset or cuda_convert_lwe_programmable_bootstrap_key_64 get that companion built from
  * their standard key on first use (concrete_hip_pbs, the memref / stream-emulator routes); a
  * caller holding its own key converts it with these two and calls concrete_hip_pbs_generic. */

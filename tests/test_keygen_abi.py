@@ -184,3 +184,23 @@ def test_optimizer_table_coverage():
     big = [r for r in rows if r["bits"] > 8]
     assert len(big) == 31 and all(r["N"] >= 32768 for r in big)
     assert [r for r in big if not runs(r)] == []
+
+
+def test_optimizer_rows_on_hand_tuned_kernels():
+    """Round 4's dispatch census: 111 of the 235 table rows get a hand-tuned
+    key format (small-ring 74, k = 2 at N = 1024: 18, N = 2048: 19); the rows left to the general
+    path at N <= 2048 are the many-level ones (k = 4: l >= 6, k = 2: l >= 4, N = 2048: l >= 5)."""
+    import json
+    from collections import Counter
+
+    L = _native.lib()
+    rows = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "v0_last_128_rows.json")))["rows"]
+    fmt = lambda r: L.concrete_hip_bsk_format(r["k"], r["N"], r["br_l"], C.byref(C.c_uint32()),  # noqa: E731
+                                              C.byref(C.c_uint32()))
+    census = Counter(fmt(r) for r in rows)
+    assert census[5] == 74 and census[4] == 18 and census[2] == 19 and census[3] == 124, census
+    for r in rows:
+        if fmt(r) == 3 and r["N"] <= 2048:
+            assert r["br_l"] >= {512: 6, 1024: 4, 2048: 5}[r["N"]], r
+        if fmt(r) != 3:
+            assert L.concrete_hip_pbs_supported(r["k"], r["N"], r["br_l"], r["br_b"]) == 1, r

@@ -254,7 +254,7 @@ __global__ void __launch_bounds__(256) convert_bsk1024k2_kernel(cplx* __restrict
 // col = cg GC + c2): limb `limb` of key polynomial (row, col) of level v = l - 1 - q (q in digit
 // order), folded, twisted by zeta_2N^j and transformed (M = N / 2 points), scaled 1 / (512 P) with
 // P = 1024 / N (the kernels' unnormalised unzip and zip), element e = (slot, lane) at frequency
-// fft512_freq(lane, slot).
+// fft512_freq(lane, slot).  k = 4, N = 512, l >= K4_MANY_MIN: level-major, [n][q][limb][col][row][N/2].
 template <int N, int K1, int LIMBS = SM_LIMBS>
 __global__ void __launch_bounds__(256) convert_bsk_small_kernel(cplx* __restrict__ dest,
                                                                const uint64_t* __restrict__ src,
@@ -267,14 +267,26 @@ __global__ void __launch_bounds__(256) convert_bsk_small_kernel(cplx* __restrict
   uint64_t t = blk;
   const uint32_t row = (uint32_t)(t % K1);
   t /= K1;
-  const uint32_t c2 = (uint32_t)(t % GC);
-  t /= GC;
-  const uint32_t q = (uint32_t)(t % level);
-  t /= level;
-  const uint32_t cg = (uint32_t)(t % NCG);
-  t /= NCG;
-  const uint32_t limb = (uint32_t)(t % LIMBS);
-  const uint64_t i = t / LIMBS;
+  uint32_t c2, q, cg, limb;
+  uint64_t i;
+  if (N == 512 && K1 == 5 && level >= K4_MANY_MIN) {  // level-major: [n][q][limb][col][row] (GC = 1)
+    c2 = 0;
+    cg = (uint32_t)(t % K1);
+    t /= K1;
+    limb = (uint32_t)(t % LIMBS);
+    t /= LIMBS;
+    q = (uint32_t)(t % level);
+    i = t / level;
+  } else {
+    c2 = (uint32_t)(t % GC);
+    t /= GC;
+    q = (uint32_t)(t % level);
+    t /= level;
+    cg = (uint32_t)(t % NCG);
+    t /= NCG;
+    limb = (uint32_t)(t % LIMBS);
+    i = t / LIMBS;
+  }
   const uint32_t col = cg * GC + c2, v = level - 1 - q;
   const uint64_t* g = src + (((i * level + v) * K1 + row) * K1 + col) * N;  // [n][l][row][col][N]
   for (int j = threadIdx.x; j < M; j += blockDim.x) {

@@ -113,12 +113,15 @@ constexpr size_t pbs_small_lds_bytes(int N, int K1) {
 constexpr int K4_CTS = 2;
 constexpr int K4_RING_SLOTS = 4;
 constexpr uint32_t K4_MAX_LEVEL = 5;
+// l >= K4_MANY_MIN: one level at a time (pbs512k4_many_kernel), the key level-major
+// ([n][q][limb][col][row][M]); whole digits with l 2^(logB-1) <= 2^15 and l logB < 64
+constexpr uint32_t K4_MANY_MIN = 6;
 constexpr size_t pbs512k4_lds_bytes() {
   return PBS1024_TABLE_BYTES + 3 * K4_CTS * PBS1024_XCH_SLOTS * 16 + (size_t)K4_RING_SLOTS * 5 * 256 * 16 +
-         3 * K4_CTS * 4;
+         4 * K4_CTS * 4 * 2 + 4 * 64 * 16;  // + sync counters (padded to 16 B) + the many-level kernel's tz
 }
 inline bool pbs_small_shape(uint32_t k, uint32_t N, uint32_t level) {
-  if (N == 512 && k == 4) return level >= 1 && level <= K4_MAX_LEVEL;
+  if (N == 512 && k == 4) return level >= 1 && level <= 64;
   return level >= 1 && level <= SM_MAX_LEVEL && ((N == 512 && k == 3) || (N == 256 && (k == 5 || k == 6)));
 }
 // key limbs of a small-ring key: 4 of 16 bits, 5 of 13 bits at k = 4, N = 512, l = 2 (K4_L2_LIMBS)
@@ -131,6 +134,8 @@ inline bool pbs_small_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_l
   if (level == 1) return base_log <= pbs_small_max_logb(N);
   // 13-bit limbs: two whole digits up to 16 bits (certified bound 0.09 on the table rows' keys)
   if (small_limbs(k, N, level) == K4_L2_LIMBS) return base_log <= 16;
+  if (level > K4_MAX_LEVEL && level < K4_MANY_MIN) return false;
+  if ((uint64_t)level * base_log >= 64) return false;
   return base_log <= 15 && ((uint64_t)level << (base_log - 1)) <= (1ull << 15);
 }
 
@@ -188,7 +193,7 @@ inline bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_
 //   GENERIC: [n][col][limb][row][q][N/2] complex f64 (pbs_generic.hip)
 //   K2N1024: [n][limb][col][q][row][512] complex f64 (pbs1024k2.hip; l <= 3)
 //   SMALL:   [n][limb][cg][q][c2][row][N/2] complex f64, col = cg GC + c2 (pbs_small.hip, pbs512k4.hip;
-//            GC = sm_gc(N, k + 1))
+//            GC = sm_gc(N, k + 1)); k = 4, N = 512, l >= K4_MANY_MIN: [n][q][limb][col][row][N/2]
 inline uint64_t fourier_bsk_bytes(uint32_t n, uint32_t k, uint32_t level, uint32_t N) {
   const KeyFormat f = key_format(k, N, level);
   switch (f.kind) {

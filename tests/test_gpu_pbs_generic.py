@@ -66,7 +66,8 @@ CASES = [
     ("k2_N1024_l4", 2, 1024, 10, 4, 9, 3),
     ("k6_N256_l4", 6, 256, 10, 4, 8, 1),
     ("k1_N2048_l5", 1, 2048, 6, 5, 8, 3),  # the general path's N = 2048 four-step kernels
-    ("k4_N512_l6", 4, 512, 8, 6, 7, 2),  # the general path's two-launch kernels at N = 512
+    ("k3_N512_l4", 3, 512, 8, 4, 9, 2),  # the general path's two-launch kernels at N = 512
+    ("k4_N512_l6", 4, 512, 8, 6, 7, 2),  # pbs512k4.hip's many-level kernel since round 4
 ]
 
 

@@ -438,3 +438,68 @@ def test_small_levels_full_row(B, oracle, torch_cuda, label):
     dec = B.lwe_decrypt(S.glwe_sk, got, S.p.big_n)
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
     assert np.array_equal(got[:2], run_oracle(oracle, S, cts[:2], acc))
+
+
+# ---- N = 512, k = 4 at l >= 6 (pbs512k4_many_kernel: one level at a time, level-major key) -----------
+K4_MANY_ROWS = {6: (7, 693), 8: (5, 668), 11: (4, 731), 22: (2, 690), 44: (1, 629)}  # l -> (logB, a row's n)
+
+
+def test_k4_many_levels_key_layout(B, oracle, torch_cuda):
+    """[n][q][limb][col][row][slot][lane]: level v = l - 1 - q of key polynomial (row, col)."""
+    level, logB = 6, 7
+    S = Setup(B, oracle, torch_cuda, B.PbsParams(n=2, k=4, N=512, level=level, base_log=logB), 9980)
+    p = S.p
+    assert B.bsk_format(p) == (5, 4, 16)
+    got = B.to_host(S.fbsk).view(np.float64).reshape(p.n, level, 4, 5, 5, 4, 64, 2)
+    bsk = S.bsk.reshape(p.n, level, 5, 5, 512)
+    lane = np.arange(64)
+    K = (lane[None, :] >> 3) + 8 * (lane[None, :] & 7) + 64 * np.arange(4)[:, None]
+    tw = np.exp(1j * np.pi * np.arange(256) / 512)
+    worst = 0.0
+    for i in (0, 1):
+        for q in (0, 2, level - 1):
+            for li in (0, 3):
+                for col in (0, 4):
+                    for row in (1, 4):
+                        lv = signed_limb(bsk[i, level - 1 - q, row, col], li)
+                        ref = np.fft.fft((lv[:256] + 1j * lv[256:]) * tw)[K] / 1024.0
+                        gg = got[i, q, li, col, row]
+                        worst = max(worst, np.max(np.abs(gg[..., 0] + 1j * gg[..., 1] - ref)) / np.max(np.abs(ref)))
+    assert worst < 1e-13, worst
+
+
+@pytest.mark.parametrize("n", [1, 2, 5])
+@pytest.mark.parametrize("level", list(K4_MANY_ROWS))
+def test_k4_many_levels_bit_exact(B, oracle, torch_cuda, level, n):
+    """Bit-exact vs the exact oracle at 6 .. 44 levels (ring prologue and tail, a 5-step rotation), odd
+    batch, residual under the certified bound."""
+    logB = K4_MANY_ROWS[level][0]
+    S = Setup(B, oracle, torch_cuda, B.PbsParams(n=n, k=4, N=512, level=level, base_log=logB), 9990 + level + n)
+    width = 2
+    rng = np.random.RandomState(level + n)
+    msgs = rng.randint(0, 4, size=5)
+    cts = encrypt(B, S, msgs, width, 20 + n, std=2.0 ** -30)
+    acc = lut_acc(B, S, rng.randint(0, 4, size=4), width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    assert np.array_equal(got, run_oracle(oracle, S, cts, acc))
+    assert resid < bound(B, oracle, S) < 0.5
+
+
+@pytest.mark.parametrize("level", [6, 22])
+def test_k4_many_levels_full_row(B, oracle, torch_cuda, level):
+    """Full rows (br 6/7 n = 693, br 22/2 n = 690): 128 samples decrypted, 1 bit-exact, residual
+    under the bound."""
+    logB, n = K4_MANY_ROWS[level]
+    S = Setup(B, oracle, torch_cuda, B.PbsParams(n=n, k=4, N=512, level=level, base_log=logB), 9970 + level)
+    width = 2
+    rng = np.random.RandomState(level)
+    table = rng.randint(0, 4, size=4)
+    msgs = rng.randint(0, 4, size=128)
+    cts = encrypt(B, S, msgs, width, 40 + level)
+    acc = lut_acc(B, S, table, width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    b = bound(B, oracle, S)
+    assert resid < b < 0.5, (resid, b)
+    dec = B.lwe_decrypt(S.glwe_sk, got, S.p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+    assert np.array_equal(got[:1], run_oracle(oracle, S, cts[:1], acc))

@@ -131,7 +131,8 @@ def test_key_formats_and_exact_range():
     # k = 4, N = 512, l = 2 (logB = 16 rows): five 13-bit key limbs
     for k, N, l in [(5, 256, 2), (6, 256, 3), (3, 512, 3), (4, 512, 3), (4, 512, 5)]:
         assert fmt(k, N, l) == (5, 4, 16), (k, N, l)
-    assert fmt(4, 512, 2) == (5, 5, 13) and fmt(5, 256, 4)[0] == 3 and fmt(4, 512, 6)[0] == 3
+    assert fmt(4, 512, 2) == (5, 5, 13) and fmt(5, 256, 4)[0] == 3 and fmt(4, 512, 6) == (5, 4, 16)
+    assert fmt(4, 512, 44) == (5, 4, 16) and L.concrete_hip_pbs_supported(4, 512, 44, 1) == 1  # one level at a time
     assert L.concrete_hip_fourier_bsk_size_bytes(700, 4, 2, 512) == 700 * 2 * 5 * 25 * 256 * 16
     assert L.concrete_hip_pbs_supported(4, 512, 2, 16) == 1
     assert L.concrete_hip_fourier_bsk_size_bytes(700, 4, 3, 512) == 700 * 3 * 4 * 25 * 256 * 16
@@ -140,7 +141,7 @@ def test_key_formats_and_exact_range():
     assert L.concrete_hip_fourier_bsk_size_bytes(722, 3, 1, 512) == 722 * 4 * 16 * 256 * 16
     assert L.concrete_hip_pbs_supported(3, 512, 1, 24) == 1 and L.concrete_hip_pbs_supported(5, 256, 1, 15) == 1
     assert L.concrete_hip_pbs_supported(5, 256, 1, 25) == 1  # past the small-ring gate: the general path
-    for k, N, l, logB in [(6, 256, 4, 8), (4, 512, 8, 5), (2, 1024, 4, 9), (1, 4096, 1, 22),
+    for k, N, l, logB in [(6, 256, 4, 8), (2, 1024, 8, 5), (2, 1024, 4, 9), (1, 4096, 1, 22),
                           (1, 8192, 1, 22), (1, 16384, 2, 15), (1, 2048, 5, 8)]:
         kind, limbs, bits = fmt(k, N, l)
         assert kind == 3 and limbs * bits >= 64, (k, N, l)
@@ -187,9 +188,9 @@ def test_optimizer_table_coverage():
 
 
 def test_optimizer_rows_on_hand_tuned_kernels():
-    """Round 4's dispatch census: 111 of the 235 table rows get a hand-tuned
-    key format (small-ring 74, k = 2 at N = 1024: 18, N = 2048: 19); the rows left to the general
-    path at N <= 2048 are the many-level ones (k = 4: l >= 6, k = 2: l >= 4, N = 2048: l >= 5)."""
+    """Round 4's dispatch census: 126 of the 235 table rows get a hand-tuned
+    key format (small-ring 89, k = 2 at N = 1024: 18, N = 2048: 19); the rows left to the general
+    path at N <= 2048 are the many-level ones (k = 2: l >= 4, N = 2048: l >= 5)."""
     import json
     from collections import Counter
 
@@ -198,9 +199,9 @@ def test_optimizer_rows_on_hand_tuned_kernels():
     fmt = lambda r: L.concrete_hip_bsk_format(r["k"], r["N"], r["br_l"], C.byref(C.c_uint32()),  # noqa: E731
                                               C.byref(C.c_uint32()))
     census = Counter(fmt(r) for r in rows)
-    assert census[5] == 74 and census[4] == 18 and census[2] == 19 and census[3] == 124, census
+    assert census[5] == 89 and census[4] == 18 and census[2] == 19 and census[3] == 109, census
     for r in rows:
         if fmt(r) == 3 and r["N"] <= 2048:
-            assert r["br_l"] >= {512: 6, 1024: 4, 2048: 5}[r["N"]], r
+            assert r["br_l"] >= {1024: 4, 2048: 5}[r["N"]], r
         if fmt(r) != 3:
             assert L.concrete_hip_pbs_supported(r["k"], r["N"], r["br_l"], r["br_b"]) == 1, r

@@ -221,7 +221,7 @@ __global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__
 }
 #endif
 
-// N = 1024, k = 2, l <= 3 (pbs1024k2.hip).  Block = (i, limb, col, q, row), in the order of the
+// N = 1024, k = 2 (pbs1024k2.hip; l >= K2_MANY_MIN: level-major, [n][q][limb][col][row][512]).  Block = (i, limb, col, q, row), in the order of the
 // output layout [n][limb][col][q][row][512]: limb `limb` of key polynomial (row, col) of level
 // v = l - 1 - q (q in digit order), folded, twisted and transformed like the k = 1 key.
 __global__ void __launch_bounds__(256) convert_bsk1024k2_kernel(cplx* __restrict__ dest,
@@ -232,10 +232,19 @@ __global__ void __launch_bounds__(256) convert_bsk1024k2_kernel(cplx* __restrict
   __shared__ ddc buf[M];
   const uint64_t blk = blockIdx.x;
   const uint32_t row = (uint32_t)(blk % 3);
-  const uint32_t q = (uint32_t)((blk / 3) % level);
-  const uint32_t col = (uint32_t)((blk / (3 * level)) % 3);
-  const uint32_t limb = (uint32_t)((blk / (9 * level)) % K2_LIMBS);
-  const uint64_t i = blk / (9 * level * K2_LIMBS);
+  uint32_t q, col, limb;
+  uint64_t i;
+  if (level >= K2_MANY_MIN) {  // level-major: [n][q][limb][col][row]
+    col = (uint32_t)((blk / 3) % 3);
+    limb = (uint32_t)((blk / 9) % K2_LIMBS);
+    q = (uint32_t)((blk / (9 * K2_LIMBS)) % level);
+    i = blk / (9 * K2_LIMBS * level);
+  } else {
+    q = (uint32_t)((blk / 3) % level);
+    col = (uint32_t)((blk / (3 * level)) % 3);
+    limb = (uint32_t)((blk / (9 * level)) % K2_LIMBS);
+    i = blk / (9 * level * K2_LIMBS);
+  }
   const uint32_t v = level - 1 - q;
   const uint64_t* g = src + (((i * level + v) * 3 + row) * 3 + col) * N;  // [n][l][row][col][N]
   for (int j = threadIdx.x; j < M; j += blockDim.x) {
@@ -359,7 +368,7 @@ int convert_bsk_launch(const ConvertArgs& a) {
   const bool n1024 = a.N == 1024 && a.k == 1 && a.limbs == 3 && a.level >= 1 && a.level <= 3;
   const bool n2048 =
       a.N == 2048 && a.k == 1 && a.limbs == (uint32_t)PBS2_LIMBS && a.level >= 1 && a.level <= PBS2_MAX_LEVEL;
-  const bool k2 = a.N == 1024 && a.k == 2 && a.limbs == (uint32_t)K2_LIMBS && a.level >= 1 && a.level <= K2_MAX_LEVEL;
+  const bool k2 = a.N == 1024 && a.k == 2 && a.limbs == (uint32_t)K2_LIMBS && a.level >= 1 && a.level <= 64;
   const bool small = pbs_small_shape(a.k, a.N, a.level) && a.limbs == small_limbs(a.k, a.N, a.level);
   if (!n1024 && !n2048 && !k2 && !small) {
     set_error("unsupported BSK conversion parameters: N=%u k=%u level=%u limbs=%u", a.N, a.k, a.level, a.limbs);

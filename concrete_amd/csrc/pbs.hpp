@@ -69,10 +69,18 @@ constexpr int K2_MAX_LOGB = 24;  // certified bound < 1/2 (oracle/pyoracle.py:gp
 // l 2^(logB-1) <= 2^15 (the l = 1 digit's magnitude; the optimizer's br 2/15, 3/12 rows; l = 4 would
 // hold 36 digit spectra per wave: 66-78 spilled VGPRs)
 constexpr uint32_t K2_MAX_LEVEL = 3;
+// l >= K2_MANY_MIN: one level at a time (pbs1024k2_many_kernel), the key level-major
+// ([n][q][limb][col][row][512]); whole digits with l 2^(logB-1) <= 2^15 and l logB < 64
+constexpr uint32_t K2_MANY_MIN = 4;
 inline bool k2_ok(uint32_t level, uint32_t base_log) {
   if (level == 1) return base_log >= 1 && base_log <= (uint32_t)K2_MAX_LOGB;
-  return level >= 2 && level <= K2_MAX_LEVEL && base_log >= 1 && base_log <= 15 &&
+  if (level >= K2_MANY_MIN && (uint64_t)level * base_log >= 64) return false;
+  return level >= 2 && level <= 64 && base_log >= 1 && base_log <= 15 &&
          ((uint64_t)level << (base_log - 1)) <= (1ull << 15);
+}
+constexpr size_t pbs1024k2_many_lds_bytes() {  // four waves per ciphertext, three scratches
+  return PBS1024_TABLE_BYTES + 3 * K2_CTS * PBS1024_XCH_SLOTS * 16 + (size_t)K2_RING_SLOTS * 3 * 512 * 16 +
+         4 * K2_CTS * 4;
 }
 constexpr size_t pbs1024k2_lds_bytes() {
   return PBS1024_TABLE_BYTES + 3 * K2_CTS * PBS1024_XCH_SLOTS * 16 + (size_t)K2_RING_SLOTS * 3 * 512 * 16 +
@@ -143,7 +151,7 @@ inline bool pbs_small_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_l
 // GENERIC: pbs_generic.hip, L balanced limbs of `bits` bits for any k <= GEN_MAX_K and
 // N = 256 .. 16384.  The format depends on (k, N, l) only: the runtime's key conversion call
 // carries no base_log (context.h:106-109).
-// K2N1024: pbs1024k2.hip (k = 2, N = 1024, l <= 3); SMALL: pbs_small.hip (N = 512, k = 3 and
+// K2N1024: pbs1024k2.hip (k = 2, N = 1024, any l); SMALL: pbs_small.hip (N = 512, k = 3 and
 // N = 256, k = 5 / 6, l <= 3) and pbs512k4.hip (N = 512, k = 4, l = 1, 3 .. 5).  The values are the ABI's format codes
 // (concrete_hip_bsk_format).
 enum class KeyKind { NONE, N1024, N2048, GENERIC, K2N1024, SMALL };
@@ -191,7 +199,7 @@ inline bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_
 //   N1024:   [n][col][limb][row*l + q][512] complex f64
 //   N2048:   [n][limb][col][q][row][+-][512] complex f64 (pbs2048.hip; l <= 4)
 //   GENERIC: [n][col][limb][row][q][N/2] complex f64 (pbs_generic.hip)
-//   K2N1024: [n][limb][col][q][row][512] complex f64 (pbs1024k2.hip; l <= 3)
+//   K2N1024: [n][limb][col][q][row][512] complex f64 (pbs1024k2.hip; l <= 3; l >= 4: [n][q][limb][col][row][512])
 //   SMALL:   [n][limb][cg][q][c2][row][N/2] complex f64, col = cg GC + c2 (pbs_small.hip, pbs512k4.hip;
 //            GC = sm_gc(N, k + 1)); k = 4, N = 512, l >= K4_MANY_MIN: [n][q][limb][col][row][N/2]
 inline uint64_t fourier_bsk_bytes(uint32_t n, uint32_t k, uint32_t level, uint32_t N) {

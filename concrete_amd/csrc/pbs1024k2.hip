@@ -103,6 +103,20 @@ __device__ __forceinline__ void tri_wait(uint32_t* flags, int ctl, int v, uint32
   asm volatile("" ::: "memory");
 }
 
+// the four waves of one ciphertext in the many-level kernel (counters f[ct * 4 + role])
+__device__ __forceinline__ void k2q_signal(uint32_t* f, int ctl, int role, uint32_t& cnt) {
+  asm volatile("" ::: "memory");
+  ++cnt;
+  __hip_atomic_store(&f[ctl * 4 + role], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void k2q_sync(uint32_t* f, int ctl, int role, uint32_t& cnt, const SyncGuard& guard) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  k2q_signal(f, ctl, role, cnt);
+#pragma unroll
+  for (int o = 1; o < 4; ++o) spin_until_ge(&f[ctl * 4 + ((role + o) & 3)], cnt, guard);
+  asm volatile("" ::: "memory");
+}
+
 }  // namespace
 
 // NQ = 1: l = 1, the two sub-digits of one digit (d_hi carried into the next slot); NQ = l = 2, 3:
@@ -489,6 +503,260 @@ static int launch_k2_t(const PbsArgs& a) {
   return 0;
 }
 
+// Many levels (l >= K2_MANY_MIN, runtime), whole digits, one level at a time (as
+// pbs512k4_many_kernel): four waves per ciphertext — the three polynomial owners and a fourth with
+// no accumulator — each keeping two of the eight spectrum slots and Y[limb][column][slot] for them
+// (24 accumulators, whatever l is); the key level-major, [n][q][limb][col][row][512].
+template <bool RESID>
+__global__ void __launch_bounds__(K2_CTS * 256, 1)
+pbs1024k2_many_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx,
+                      const uint64_t* __restrict__ luts, const uint64_t* __restrict__ lut_idx,
+                      const uint64_t* __restrict__ in, const uint64_t* __restrict__ in_idx,
+                      const cplx* __restrict__ fbsk, uint32_t n, uint32_t level, uint32_t base_log,
+                      uint32_t num_samples, unsigned long long* __restrict__ resid_out, SyncGuard guard) {
+  constexpr int N = 1024, LOG2_2N = 11, K1 = 3, LIMBS = K2_LIMBS, MS = 2;
+  constexpr int NW = 4 * K2_CTS;
+  constexpr int GROUP = K1 * 512;           // (level, limb, column): the three row spectra
+  constexpr int WPL = LIMBS * K1;           // key windows per level
+  constexpr int RS = K2_RING_SLOTS, DIST = RS - 1;
+  constexpr int GLDS = 4;
+  constexpr int NISS = GROUP / 64 / GLDS;   // waves 0 .. NISS - 1 issue a group's pieces
+  static_assert(GROUP / 64 == GLDS * NISS && NISS <= NW && WPL % RS == 0 && DIST <= 3, "ring geometry");
+  constexpr int XS = (int)PBS1024_XCH_SLOTS;
+  const uint32_t NGRP = (uint32_t)WPL * level;
+  const uint64_t PER_I = (uint64_t)NGRP * GROUP;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  cplx* tbl = reinterpret_cast<cplx*>(smem);
+  cplx* xch_all = tbl + FFT512_TABLE_ENTRIES;
+  cplx* ring = xch_all + 3 * K2_CTS * XS;   // (the fourth wave has no scratch)
+  uint32_t* tflags = reinterpret_cast<uint32_t*>(ring + RS * GROUP);
+
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int ctl = w >> 2;
+  const int role = ctl == 0 ? (w & 3) : ((w + 1) & 3);  // slots 2 role, 2 role + 1
+  const bool owner = role < 3;
+  const int v = owner ? role : 0;           // owned polynomial
+  const uint32_t s = blockIdx.x * K2_CTS + ctl;
+  const bool active = s < num_samples;
+  cplx* ctx = xch_all + ctl * 3 * XS;
+  cplx* xch = ctx + v * XS;
+  uint64_t* xch64 = reinterpret_cast<uint64_t*>(xch);
+  cplx* myslot = ctx + 2 * role * 64 + lane;  // + jj * 64 + scratch * XS
+
+  const bool issuer = w < NISS;
+  const cplx* key_w = fbsk + (uint64_t)(issuer ? w : 0) * GLDS * 64;
+  cplx* ring_w = ring + (issuer ? w : 0) * GLDS * 64;
+  const uint32_t lane_b = (uint32_t)lane * (uint32_t)sizeof(cplx);
+  auto issue_group = [&](const cplx* key_step, uint32_t g) __attribute__((always_inline)) {
+    if (!issuer) return;
+    const char* src = reinterpret_cast<const char*>(key_step + (uint64_t)g * GROUP);
+    cplx* dst = ring_w + (g % RS) * GROUP;
+#pragma unroll
+    for (int j = 0; j < GLDS; ++j)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const cplx*>(src + j * 1024 + lane_b),
+                                       (lds_ptr_t)(dst + j * 64), 16, 0, 0);
+  };
+  if (n > 0) {
+#pragma unroll
+    for (int g = 0; g < DIST; ++g) issue_group(key_w, (uint32_t)g);
+  }
+
+  build_fft512_tables(tbl, threadIdx.x, NW * 64);
+  if (lane == 0) tflags[w] = 0u;
+  uint32_t tcnt = 0;
+  __syncthreads();
+  const Fft512Tables T = fft512_tables_at(tbl);
+
+  const uint64_t* lwe = in + (active ? (in_idx ? in_idx[s] : s) : 0) * (uint64_t)(n + 1);
+  const uint64_t* lut = luts + (active && lut_idx ? lut_idx[s] : 0ull) * (uint64_t)(K1 * N);
+
+  // acc_v = LUT_v * X^{-ms(b)}: lane t holds coefficients t + 64 m
+  uint64_t A[16];
+  {
+    const uint32_t bt = active ? modswitch(lwe[n], LOG2_2N) : 0u;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const uint32_t src = (uint32_t)(lane + 64 * m + bt) & (2 * N - 1);
+      const uint64_t val = active && owner ? lut[v * N + (src & (N - 1))] : 0ull;
+      A[m] = src < N ? val : 0ull - val;
+    }
+  }
+
+  const int nrep = 64 - (int)level * (int)base_log;
+  const int logB = (int)base_log;
+  double max_resid = 0.0;
+
+  uint64_t a_next = active && owner ? lwe[0] : 0ull;
+  for (uint32_t i = 0; i < n; ++i) {
+    const cplx* key_step = key_w + (uint64_t)i * PER_I;
+    const bool last_step = i + 1 >= n;
+    const uint64_t ai = a_next;
+    if (i + 1 < n) a_next = active && owner ? lwe[i + 1] : 0ull;
+    const uint32_t at = modswitch(ai, LOG2_2N);
+
+    uint64_t st[16];
+    if (owner) {
+#pragma unroll
+      for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = A[m];
+      wave_lds_fence();
+      uint64_t rv[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) rv[m] = xch64[(uint32_t)(lane + 64 * m - (int)at) & (N - 1)];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const uint32_t sp = (uint32_t)(lane + 64 * m - (int)at) & (2 * N - 1);
+        st[m] = decomp_init((sp < N ? rv[m] : 0ull - rv[m]) - A[m], nrep);
+      }
+      wave_lds_fence();
+    }
+
+    cplx Y[LIMBS][K1][MS];
+#pragma unroll
+    for (int li = 0; li < LIMBS; ++li)
+#pragma unroll
+      for (int cc = 0; cc < K1; ++cc)
+#pragma unroll
+        for (int jj = 0; jj < MS; ++jj) Y[li][cc][jj] = {0.0, 0.0};
+#pragma unroll 1
+    for (uint32_t q = 0; q < level; ++q) {
+      // ---- level q: the owners' digit polynomials and forward transforms, published by the
+      //      level's first key-window barrier (every wave read the previous level's spectra right
+      //      after that level's first barrier, 11 windows ago)
+      if (owner) {
+        cplx vv[8];
+        {
+          int32_t d[16];
+#pragma unroll
+          for (int m = 0; m < 16; ++m) d[m] = decomp_next_t(st[m], logB);
+#pragma unroll
+          for (int m = 0; m < 8; ++m) vv[m] = {(double)d[m], (double)d[m + 8]};
+        }
+        cplx tw2[4], tw3[4];
+        fwd_p2_tw(tw2, T, lane >> 3);
+        fwd_p3_tw(tw3, T, lane);
+        fft512_fwd_tw(vv, xch, lane, tw2, tw3, 0, []() __attribute__((always_inline)) {});
+#pragma unroll
+        for (int k2 = 0; k2 < 8; ++k2) xch[k2 * 64 + lane] = vv[k2];
+      }
+      cplx X[K1][MS];
+#pragma unroll
+      for (int wi = 0; wi < WPL; ++wi) {
+        const int li = wi / K1, cc = wi % K1;
+        const uint32_t r = q * (uint32_t)WPL + (uint32_t)wi;
+        if (issuer) {
+          if (r + DIST - 1 < NGRP || !last_step) wait_vmcnt<GLDS * (DIST - 1)>();
+          else if (r + 1 == NGRP) wait_vmcnt<0>();
+          else if (r + 2 == NGRP) wait_vmcnt<GLDS>();
+          else wait_vmcnt<GLDS * 2>();
+        }
+        pair_barrier();
+        if (r + DIST < NGRP || !last_step) issue_group(key_step, r + DIST);
+        if (wi == 0) {
+#pragma unroll
+          for (int row = 0; row < K1; ++row)
+#pragma unroll
+            for (int jj = 0; jj < MS; ++jj) X[row][jj] = myslot[row * XS + jj * 64];
+        }
+        const cplx* G = ring + (wi % RS) * GROUP + 2 * role * 64 + lane;
+#pragma unroll
+        for (int row = 0; row < K1; ++row) {
+#pragma unroll
+          for (int jj = 0; jj < MS; ++jj) {
+            const cplx g = G[row * 512 + jj * 64];
+            cplx& y = Y[li][cc][jj];
+            y.re = __builtin_fma(X[row][jj].re, g.re, __builtin_fma(-X[row][jj].im, g.im, y.re));
+            y.im = __builtin_fma(X[row][jj].re, g.im, __builtin_fma(X[row][jj].im, g.re, y.im));
+          }
+        }
+#pragma unroll
+        for (int jj = 0; jj < MS; ++jj) pin(Y[li][cc][jj]);
+      }
+    }
+
+    // ---- per limb: mail my slots of the three outputs, sync, inverse, barrier ---------------
+#pragma unroll
+    for (int li = 0; li < LIMBS; ++li) {
+#pragma unroll
+      for (int cc = 0; cc < K1; ++cc)
+#pragma unroll
+        for (int jj = 0; jj < MS; ++jj) myslot[cc * XS + jj * 64] = Y[li][cc][jj];
+      if (owner) {
+        k2q_sync(tflags, ctl, role, tcnt, guard);
+        cplx V[8];
+#pragma unroll
+        for (int k2 = 0; k2 < 8; ++k2) V[k2] = xch[k2 * 64 + lane];
+        {
+          cplx gi2[4];
+          inv_p2_stage_tw(gi2, T, lane & 7);
+          fft512_inv_tw(V, xch, T, lane, gi2, 0);
+        }
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          const double tr = V[m].re + RND_MAGIC, ti = V[m].im + RND_MAGIC;
+          if constexpr (RESID) {
+            max_resid = fmax(max_resid, fabs(V[m].re - (tr - RND_MAGIC)));
+            max_resid = fmax(max_resid, fabs(V[m].im - (ti - RND_MAGIC)));
+          }
+          if (li == 0) {
+            A[m] += (uint64_t)__double_as_longlong(tr) - K2_MAGIC_ALL;
+            A[m + 8] += (uint64_t)__double_as_longlong(ti) - K2_MAGIC_ALL;
+          } else {
+            A[m] += (uint64_t)__double_as_longlong(tr) << (16 * li);
+            A[m + 8] += (uint64_t)__double_as_longlong(ti) << (16 * li);
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < 16; ++m) pin(A[m]);
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        k2q_signal(tflags, ctl, role, tcnt);
+      }
+      pair_barrier();  // every owner is done with its scratch
+    }
+  }
+
+  uint64_t* o = out + (active ? (out_idx ? out_idx[s] : s) : 0) * (uint64_t)(2 * N + 1);
+  if (!active || !owner) {
+  } else if (v < 2) {
+#pragma unroll
+    for (int m = 0; m < 16; ++m) xch64[lane + 64 * m] = A[m];
+    wave_lds_fence();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int j = lane + 64 * m;
+      const uint64_t val = xch64[(N - j) & (N - 1)];
+      o[v * N + j] = j == 0 ? val : 0ull - val;
+    }
+  } else if (lane == 0) {
+    o[2 * N] = A[0];
+  }
+
+  if constexpr (RESID) {
+    for (int off = 32; off > 0; off >>= 1) max_resid = fmax(max_resid, __shfl_xor(max_resid, off));
+    if (lane == 0 && active && resid_out) atomicMax(resid_out, (unsigned long long)__double_as_longlong(max_resid));
+  }
+}
+
+template <bool RESID>
+static int launch_k2_many_t(const PbsArgs& a) {
+  const size_t lds = pbs1024k2_many_lds_bytes();
+  auto kern = pbs1024k2_many_kernel<RESID>;
+  CHIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const uint32_t blocks = (a.num_samples + K2_CTS - 1) / K2_CTS;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(K2_CTS * 256), lds, a.stream, a.out, a.out_idx, a.luts, a.lut_idx,
+                     a.in, a.in_idx, reinterpret_cast<const cplx*>(a.fbsk), a.n, a.level, a.base_log,
+                     a.num_samples, a.resid, a.guard);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("pbs launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
 int pbs1024k2_launch(const PbsArgs& a) {
   if (!(a.N == 1024 && a.k == 2 && a.limbs == (uint32_t)K2_LIMBS && k2_ok(a.level, a.base_log))) {
     set_error("unsupported PBS parameters: N=%u k=%u level=%u base_log=%u limbs=%u", a.N, a.k, a.level, a.base_log,
@@ -496,6 +764,7 @@ int pbs1024k2_launch(const PbsArgs& a) {
     return -2;
   }
   if (a.num_samples == 0) return 0;
+  if (a.level >= K2_MANY_MIN) return a.resid ? launch_k2_many_t<true>(a) : launch_k2_many_t<false>(a);
   switch (a.level) {
     case 1: return a.resid ? launch_k2_t<true, 1>(a) : launch_k2_t<false, 1>(a);
     case 2: return a.resid ? launch_k2_t<true, 2>(a) : launch_k2_t<false, 2>(a);

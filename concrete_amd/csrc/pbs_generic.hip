@@ -108,7 +108,7 @@ KeyFormat generic_key_format(uint32_t k, uint32_t N, uint32_t level) {
 KeyFormat key_format(uint32_t k, uint32_t N, uint32_t level) {
   if (k == 1 && N == 1024 && level >= 1 && level <= 3) return {KeyKind::N1024, 3, 22};
   if (k == 1 && N == 2048 && level >= 1 && level <= PBS2_MAX_LEVEL) return {KeyKind::N2048, (uint32_t)PBS2_LIMBS, 16};
-  if (k == 2 && N == 1024 && level >= 1 && level <= K2_MAX_LEVEL) return {KeyKind::K2N1024, (uint32_t)K2_LIMBS, 16};
+  if (k == 2 && N == 1024 && level >= 1 && level <= 64) return {KeyKind::K2N1024, (uint32_t)K2_LIMBS, 16};
   if (pbs_small_shape(k, N, level))
     return {KeyKind::SMALL, small_limbs(k, N, level), small_limbs(k, N, level) == K4_L2_LIMBS ? 13u : 16u};
   return generic_key_format(k, N, level);

@@ -313,3 +313,66 @@ def test_three_levels_full_row(B, oracle, torch_cuda):
     dec = B.lwe_decrypt(S.glwe_sk, got, S.p.big_n)
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
     assert np.array_equal(got[:2], run_oracle(oracle, S, cts[:2], acc))
+
+
+# ---- l >= 4 (pbs1024k2_many_kernel: one level at a time, level-major key; br 4/9 .. 44/1) ---------
+K2_MANY_ROWS = {4: (9, 731), 5: (8, 722), 8: (5, 743), 15: (3, 754), 44: (1, 727)}  # l -> (logB, a row's n)
+
+
+def test_many_levels_key_layout(B, oracle, torch_cuda):
+    """[n][q][limb][col][row][slot][lane]: level v = l - 1 - q of key polynomial (row, col)."""
+    level, logB = 4, 9
+    S = Setup(B, oracle, torch_cuda, B.PbsParams(n=2, k=2, N=1024, level=level, base_log=logB), 8950)
+    p = S.p
+    assert B.bsk_format(p) == (4, 4, 16)
+    got = B.to_host(S.fbsk).view(np.float64).reshape(p.n, level, 4, 3, 3, 8, 64, 2)
+    bsk = S.bsk.reshape(p.n, level, 3, 3, 1024)
+    lane = np.arange(64)
+    K = (lane[None, :] >> 3) + 8 * (lane[None, :] & 7) + 64 * np.arange(8)[:, None]
+    tw = np.exp(1j * np.pi * np.arange(512) / 1024.0)
+    worst = 0.0
+    for i in (0, 1):
+        for q in range(level):
+            for li in (0, 3):
+                for col in (0, 2):
+                    for row in (0, 2):
+                        lv = signed_limb(bsk[i, level - 1 - q, row, col], li)
+                        ref = np.fft.fft((lv[:512] + 1j * lv[512:]) * tw)[K] / 512.0
+                        gg = got[i, q, li, col, row]
+                        worst = max(worst, np.max(np.abs(gg[..., 0] + 1j * gg[..., 1] - ref)) / np.max(np.abs(ref)))
+    assert worst < 1e-13, worst
+
+
+@pytest.mark.parametrize("n", [1, 2, 5])
+@pytest.mark.parametrize("level", list(K2_MANY_ROWS))
+def test_many_levels_bit_exact(B, oracle, torch_cuda, level, n):
+    logB = K2_MANY_ROWS[level][0]
+    S = Setup(B, oracle, torch_cuda, B.PbsParams(n=n, k=2, N=1024, level=level, base_log=logB), 8960 + level + n)
+    width = 3
+    rng = np.random.RandomState(level + n)
+    msgs = rng.randint(0, 8, size=5)
+    cts = encrypt(B, S, msgs, width, 30 + n, std=2.0 ** -30)
+    acc = lut_acc(B, S, rng.randint(0, 8, size=8), width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    assert np.array_equal(got, run_oracle(oracle, S, cts, acc))
+    assert resid < oracle.gpu1024k2_error_bound(B.to_host(S.fbsk).view(np.float64), logB, level) < 0.5
+
+
+@pytest.mark.parametrize("level", [4, 15])
+def test_many_levels_full_row(B, oracle, torch_cuda, level):
+    """The 4-bit rows at br 4/9 (n = 731) and 15/3 (n = 754): 128 samples decrypted, 1 bit-exact,
+    residual under the bound."""
+    logB, n = K2_MANY_ROWS[level]
+    S = Setup(B, oracle, torch_cuda, B.PbsParams(n=n, k=2, N=1024, level=level, base_log=logB), 8970 + level)
+    width = 4
+    rng = np.random.RandomState(level)
+    table = rng.randint(0, 16, size=16)
+    msgs = rng.randint(0, 16, size=128)
+    cts = encrypt(B, S, msgs, width, 50 + level)
+    acc = lut_acc(B, S, table, width)
+    got, resid = run_gpu(B, S, cts, acc, torch_cuda, resid=True)
+    bound = oracle.gpu1024k2_error_bound(B.to_host(S.fbsk).view(np.float64), logB, level)
+    assert resid < bound < 0.5, (resid, bound)
+    dec = B.lwe_decrypt(S.glwe_sk, got, S.p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+    assert np.array_equal(got[:1], run_oracle(oracle, S, cts[:1], acc))

@@ -60,14 +60,15 @@ CASES = [
     ("2bit_k5_N256_l2", 5, 256, 16, 2, 10, 2),
     ("1bit_k6_N256_l2", 6, 256, 12, 2, 12, 1),
     ("3bit_k4_N512", 4, 512, 14, 1, 23, 3),  # pbs512k4.hip since round 4 (test_gpu_pbs_small.py)
-    # shapes that stay on the general path's two-launch kernels: l = 4 at N = 256 (no table row) and
-    # k = 2, N = 1024, l = 4 (br 4/9)
+    # l = 4 at N = 256 (the general path; no table row) and k = 2, N = 1024, l = 4 (br 4/9: the k = 2
+    # kernel's one-level-at-a-time form since round 4)
     ("k5_N256_l4", 5, 256, 12, 4, 7, 2),
     ("k2_N1024_l4", 2, 1024, 10, 4, 9, 3),
     ("k6_N256_l4", 6, 256, 10, 4, 8, 1),
     ("k1_N2048_l5", 1, 2048, 6, 5, 8, 3),  # the general path's N = 2048 four-step kernels
     ("k3_N512_l4", 3, 512, 8, 4, 9, 2),  # the general path's two-launch kernels at N = 512
     ("k4_N512_l6", 4, 512, 8, 6, 7, 2),  # pbs512k4.hip's many-level kernel since round 4
+    ("k3_N1024_l2", 3, 1024, 6, 2, 10, 2),  # the general path's two-launch kernels at N = 1024
 ]
 
 
@@ -153,7 +154,7 @@ def test_generic_8bit_long_chain_decrypts(B, oracle, torch_cuda):
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
 
 
-@pytest.mark.parametrize("ci", [19, 23, 21, 20], ids=[CASES[i][0] for i in (19, 23, 21, 20)])
+@pytest.mark.parametrize("ci", [19, 23, 21, 25, 20], ids=[CASES[i][0] for i in (19, 23, 21, 25, 20)])
 def test_generic_index_arrays(B, oracle, torch_cuda, ci):
     """Mapped LUTs and permuted input/output rows (GPUDFG.cpp:1149-1205) on the general path:
     the one-launch tile kernels (N = 256: 4 ciphertexts per workgroup, the last one partly

@@ -117,7 +117,8 @@ def test_key_formats_and_exact_range():
     # 4 limbs of 16 bits, the digit split on the limb grid as at N = 2048
     assert fmt(2, 1024, 1) == (4, 4, 16) and fmt(2, 1024, 2) == (4, 4, 16)
     assert L.concrete_hip_pbs_supported(2, 1024, 2, 15) == 1  # two levels: whole digits up to 15 bits
-    assert fmt(2, 1024, 3) == (4, 4, 16) and fmt(2, 1024, 4)[0] == 3  # l = 3 (br 3/12); l = 4: general
+    assert fmt(2, 1024, 3) == (4, 4, 16) and fmt(2, 1024, 4) == (4, 4, 16)  # l >= 4: one level at a time
+    assert L.concrete_hip_fourier_bsk_size_bytes(727, 2, 44, 1024) == 727 * 44 * 4 * 9 * 512 * 16
     assert L.concrete_hip_pbs_supported(2, 1024, 3, 12) == 1
     assert L.concrete_hip_fourier_bsk_size_bytes(801, 2, 1, 1024) == 801 * 4 * 9 * 512 * 16
     assert L.concrete_hip_pbs_supported(2, 1024, 1, 24) == 1
@@ -141,7 +142,7 @@ def test_key_formats_and_exact_range():
     assert L.concrete_hip_fourier_bsk_size_bytes(722, 3, 1, 512) == 722 * 4 * 16 * 256 * 16
     assert L.concrete_hip_pbs_supported(3, 512, 1, 24) == 1 and L.concrete_hip_pbs_supported(5, 256, 1, 15) == 1
     assert L.concrete_hip_pbs_supported(5, 256, 1, 25) == 1  # past the small-ring gate: the general path
-    for k, N, l, logB in [(6, 256, 4, 8), (2, 1024, 8, 5), (2, 1024, 4, 9), (1, 4096, 1, 22),
+    for k, N, l, logB in [(6, 256, 4, 8), (1, 2048, 8, 5), (3, 512, 5, 8), (1, 4096, 1, 22),
                           (1, 8192, 1, 22), (1, 16384, 2, 15), (1, 2048, 5, 8)]:
         kind, limbs, bits = fmt(k, N, l)
         assert kind == 3 and limbs * bits >= 64, (k, N, l)
@@ -188,9 +189,9 @@ def test_optimizer_table_coverage():
 
 
 def test_optimizer_rows_on_hand_tuned_kernels():
-    """Round 4's dispatch census: 126 of the 235 table rows get a hand-tuned
-    key format (small-ring 89, k = 2 at N = 1024: 18, N = 2048: 19); the rows left to the general
-    path at N <= 2048 are the many-level ones (k = 2: l >= 4, N = 2048: l >= 5)."""
+    """Round 4's dispatch census: 135 of the 235 table rows get a hand-tuned
+    key format (small-ring 89, k = 2 at N = 1024: 27, N = 2048: 19); the rows left to the general
+    path at N <= 2048 are N = 2048's many-level ones (l >= 5)."""
     import json
     from collections import Counter
 
@@ -199,9 +200,9 @@ def test_optimizer_rows_on_hand_tuned_kernels():
     fmt = lambda r: L.concrete_hip_bsk_format(r["k"], r["N"], r["br_l"], C.byref(C.c_uint32()),  # noqa: E731
                                               C.byref(C.c_uint32()))
     census = Counter(fmt(r) for r in rows)
-    assert census[5] == 89 and census[4] == 18 and census[2] == 19 and census[3] == 109, census
+    assert census[5] == 89 and census[4] == 27 and census[2] == 19 and census[3] == 100, census
     for r in rows:
         if fmt(r) == 3 and r["N"] <= 2048:
-            assert r["br_l"] >= {1024: 4, 2048: 5}[r["N"]], r
+            assert r["N"] == 2048 and r["br_l"] >= 5, r
         if fmt(r) != 3:
             assert L.concrete_hip_pbs_supported(r["k"], r["N"], r["br_l"], r["br_b"]) == 1, r

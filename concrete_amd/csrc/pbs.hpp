@@ -65,13 +65,17 @@ constexpr int K2_LIMBS = 4;
 constexpr int K2_SUBS = 2;
 constexpr int K2_SUB_BITS = 16;
 constexpr int K2_MAX_LOGB = 24;  // certified bound < 1/2 (oracle/pyoracle.py:gpu1024k2_error_bound)
-// l = 1: one digit split into two sub-digits (logB <= 24); l = 2 .. K2_MAX_LEVEL: whole digits with
-// l 2^(logB-1) <= 2^15 (the l = 1 digit's magnitude; the optimizer's br 2/15, 3/12 rows; l = 4 would
-// hold 36 digit spectra per wave: 66-78 spilled VGPRs)
-constexpr uint32_t K2_MAX_LEVEL = 3;
+// l = 1: one digit split into two sub-digits (logB <= 24); l = 2: two whole digits with
+// l 2^(logB-1) <= 2^15 (the l = 1 digit's magnitude; the optimizer's br 2/15 rows), both levels'
+// spectra held in registers (pbs1024k2_kernel)
+constexpr uint32_t K2_MAX_LEVEL = 2;  // pbs1024k2_kernel's levels
 // l >= K2_MANY_MIN: one level at a time (pbs1024k2_many_kernel), the key level-major
-// ([n][q][limb][col][row][512]); whole digits with l 2^(logB-1) <= 2^15 and l logB < 64
-constexpr uint32_t K2_MANY_MIN = 4;
+// ([n][q][limb][col][row][512]); whole digits with l 2^(logB-1) <= 2^15 and l logB < 64.  From l = 3
+// it is faster than holding every level's spectra (3.6 % at l = 3, profiles/r04manyab_rows.log).
+#ifndef K2_MANY_MIN_LEVEL
+#define K2_MANY_MIN_LEVEL 3
+#endif
+constexpr uint32_t K2_MANY_MIN = K2_MANY_MIN_LEVEL;
 inline bool k2_ok(uint32_t level, uint32_t base_log) {
   if (level == 1) return base_log >= 1 && base_log <= (uint32_t)K2_MAX_LOGB;
   if (level >= K2_MANY_MIN && (uint64_t)level * base_log >= 64) return false;
@@ -113,17 +117,21 @@ constexpr size_t pbs_small_lds_bytes(int N, int K1) {
 }
 // N = 512, k = 4 (pbs512k4.hip): the same key format and packing; five polynomials make three packed
 // transforms: four waves per ciphertext (three transform owners, one slot each), K4_CTS ciphertexts per
-// workgroup and a ring of K4_RING_SLOTS 20 KB key groups.  l = 1 (logB <= 24) or l = 3 .. K4_MAX_LEVEL
-// whole digits with l 2^(logB-1) <= 2^15 (the l = 1, logB = 16 magnitude: certified bound 0.35).
-// l = 2: the optimizer's rows have logB = 16, where two whole digits against 16-bit limbs would put the
+// workgroup and a ring of K4_RING_SLOTS 20 KB key groups.  l = 1 (logB <= 24), and whole digits with
+// l 2^(logB-1) <= 2^15 (the l = 1, logB = 16 magnitude: certified bound 0.35) one level at a time from
+// l = 3.  l = 2: the optimizer's rows have logB = 16, where two whole digits against 16-bit limbs would put the
 // bound at 0.69, so that shape's key has five 13-bit limbs (bound 0.09; the format depends on (k, N, l)
 // only, so the whole shape takes it).
 constexpr int K4_CTS = 2;
 constexpr int K4_RING_SLOTS = 4;
-constexpr uint32_t K4_MAX_LEVEL = 5;
+constexpr uint32_t K4_MAX_LEVEL = 2;  // pbs512k4_kernel's levels (l = 2: 13-bit limbs)
 // l >= K4_MANY_MIN: one level at a time (pbs512k4_many_kernel), the key level-major
-// ([n][q][limb][col][row][M]); whole digits with l 2^(logB-1) <= 2^15 and l logB < 64
-constexpr uint32_t K4_MANY_MIN = 6;
+// ([n][q][limb][col][row][M]); whole digits with l 2^(logB-1) <= 2^15 and l logB < 64.  From l = 3
+// it is faster than holding every level's spectra (3-7 % at l = 3 .. 5, profiles/r04manyab_rows.log).
+#ifndef K4_MANY_MIN_LEVEL
+#define K4_MANY_MIN_LEVEL 3
+#endif
+constexpr uint32_t K4_MANY_MIN = K4_MANY_MIN_LEVEL;
 constexpr size_t pbs512k4_lds_bytes() {
   return PBS1024_TABLE_BYTES + 3 * K4_CTS * PBS1024_XCH_SLOTS * 16 + (size_t)K4_RING_SLOTS * 5 * 256 * 16 +
          4 * K4_CTS * 4 * 2 + 4 * 64 * 16;  // + sync counters (padded to 16 B) + the many-level kernel's tz
@@ -142,7 +150,6 @@ inline bool pbs_small_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_l
   if (level == 1) return base_log <= pbs_small_max_logb(N);
   // 13-bit limbs: two whole digits up to 16 bits (certified bound 0.09 on the table rows' keys)
   if (small_limbs(k, N, level) == K4_L2_LIMBS) return base_log <= 16;
-  if (level > K4_MAX_LEVEL && level < K4_MANY_MIN) return false;
   if ((uint64_t)level * base_log >= 64) return false;
   return base_log <= 15 && ((uint64_t)level << (base_log - 1)) <= (1ull << 15);
 }

@@ -119,7 +119,8 @@ __device__ __forceinline__ void k2q_sync(uint32_t* f, int ctl, int role, uint32_
 
 }  // namespace
 
-// NQ = 1: l = 1, the two sub-digits of one digit (d_hi carried into the next slot); NQ = l = 2, 3:
+// NQ = 1: l = 1, the two sub-digits of one digit (d_hi carried into the next slot); NQ = l = 2 (from
+// l = 3 pbs1024k2_many_kernel runs one level at a time):
 // whole digits (l 2^(logB-1) <= 2^15), the levels' products in the same slot (the key
 // holds both levels, [n][limb][col][q][row][512], one ring group per level).
 template <bool RESID, int NQ>
@@ -767,8 +768,7 @@ int pbs1024k2_launch(const PbsArgs& a) {
   if (a.level >= K2_MANY_MIN) return a.resid ? launch_k2_many_t<true>(a) : launch_k2_many_t<false>(a);
   switch (a.level) {
     case 1: return a.resid ? launch_k2_t<true, 1>(a) : launch_k2_t<false, 1>(a);
-    case 2: return a.resid ? launch_k2_t<true, 2>(a) : launch_k2_t<false, 2>(a);
-    default: return a.resid ? launch_k2_t<true, 3>(a) : launch_k2_t<false, 3>(a);
+    default: return a.resid ? launch_k2_t<true, 2>(a) : launch_k2_t<false, 2>(a);
   }
 }
 

@@ -58,8 +58,9 @@ __device__ __forceinline__ void k4_sync(uint32_t* f, int ctl, int role, uint32_t
 }  // namespace
 
 // SUBS = 2, NQ = 1: one digit split into d_lo + 2^16 d_hi (16 < logB <= 24); SUBS = 1: NQ = l whole
-// digits (logB <= 15; l = 1, 3, 4, 5: pbs.hpp K4_MAX_LEVEL), each level's products landing in the same slot (the key holds the levels,
-// [n][limb][col][q][row][M], one ring group per level).
+// digits, each level's products landing in the same slot (the key holds the levels,
+// [n][limb][col][q][row][M], one ring group per level): l = 1 at logB <= 15 and l = 2 on 13-bit limbs;
+// from l = 3 pbs512k4_many_kernel runs one level at a time.
 // LIMBS = 4 balanced 16-bit key limbs, or 5 of 13 bits (l = 2 at logB = 16: two whole 16-bit digits
 // against 16-bit limbs would put the certified bound at 0.69; 13-bit limbs cut the key spectra 8x).
 template <int SUBS, int NQ, int LIMBS, bool RESID>
@@ -728,10 +729,7 @@ int pbs512k4_launch(const PbsArgs& a) {
   switch (a.level) {
     // logB <= 15: |digit| <= 2^14 fits the 16-bit grid whole (one sub-digit)
     case 1: return a.base_log <= 15 ? launch_k4_r<1, 1>(a) : launch_k4_r<2, 1>(a);
-    case 2: return launch_k4_r<1, 2, 5>(a);  // 13-bit key limbs
-    case 3: return launch_k4_r<1, 3>(a);
-    case 4: return launch_k4_r<1, 4>(a);
-    default: return launch_k4_r<1, 5>(a);
+    default: return launch_k4_r<1, 2, 5>(a);  // l = 2: 13-bit key limbs
   }
 }
 

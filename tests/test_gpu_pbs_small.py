@@ -301,15 +301,19 @@ def k4_level_setup(B, oracle, torch, level, n, seed):
 
 @pytest.mark.parametrize("level", [2, 3, 4, 5])
 def test_k4_levels_key_layout(B, oracle, torch_cuda, level):
-    """[n][limb][col][q][row][slot][lane]: level v = l - 1 - q of key polynomial (row, col); at l = 2
-    five 13-bit limbs."""
+    """[n][limb][col][q][row][slot][lane] (l = 2, five 13-bit limbs) or level-major
+    [n][q][limb][col][row][slot][lane] (l >= 3): level v = l - 1 - q of key polynomial (row, col)."""
     S = k4_level_setup(B, oracle, torch_cuda, level, 3, 9600 + level)
     p = S.p
     K1, M, N = 5, 256, 512
     L = 5 if level == 2 else 4
     assert B.bsk_format(p) == ((5, 5, 13) if level == 2 else (5, 4, 16))
     assert B.fourier_bsk_bytes(p) == p.n * level * L * 25 * M * 16
-    got = B.to_host(S.fbsk).view(np.float64).reshape(p.n, L, K1, level, K1, 4, 64, 2)
+    got = B.to_host(S.fbsk).view(np.float64)
+    if level >= 3:  # the one-level-at-a-time kernel's level-major key, [n][q][limb][col][row]
+        got = got.reshape(p.n, level, L, K1, K1, 4, 64, 2).transpose(0, 2, 3, 1, 4, 5, 6, 7)
+    else:
+        got = got.reshape(p.n, L, K1, level, K1, 4, 64, 2)
     bsk = S.bsk.reshape(p.n, level, K1, K1, N)
     lane = np.arange(64)
     K = (lane[None, :] >> 3) + 8 * (lane[None, :] & 7) + 64 * np.arange(4)[:, None]

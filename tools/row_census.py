@@ -1,4 +1,4 @@
-"""PBS/s of every distinct (k, N, l, logB) shape of the optimizer's table at N <= 2048 and l <= 8, on the kernel
+"""PBS/s of every distinct (k, N, l, logB) shape of the optimizer's table at N <= 2048, on the kernel
 the backend picks (its key format) and on the general path (concrete_hip_convert_bsk_generic +
 concrete_hip_pbs_generic), at the largest n among the shape's rows; 2 rows checked bit-exact against
 the oracle per run.  One process, one GPU.
@@ -22,7 +22,7 @@ nb = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 rows = json.load(open(os.path.join(ROOT, "tests", "golden", "v0_last_128_rows.json")))["rows"]
 shapes = {}
 for r in rows:
-    if r["N"] > 2048 or r["br_l"] > 8:  # (the 10-44-level keys are GBs of keygen per row)
+    if r["N"] > 2048:
         continue
     key = (r["k"], r["N"], r["br_l"], r["br_b"])
     s = shapes.setdefault(key, {"rows": 0, "n": 0, "bits": set()})
@@ -79,6 +79,6 @@ for (k, N, l, logB), s in sorted(shapes.items(), key=lambda x: (x[0][1], x[0][0]
     torch.cuda.empty_cache()
     results.append(entry)
     print(json.dumps(entry), flush=True)
-json.dump({"note": "tools/row_census.py: every (k, N, l, logB) shape of v0_last_128 at N <= 2048, l <= 8, the largest n "
+json.dump({"note": "tools/row_census.py: every (k, N, l, logB) shape of v0_last_128 at N <= 2048, the largest n "
                    "of its rows, batch %d; format 3 = the general path" % nb, "shapes": results},
           open(out_path, "w"), indent=1)

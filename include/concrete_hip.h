@@ -122,9 +122,9 @@ int concrete_hip_keyswitch_supported(uint32_t level_count, uint32_t base_log, ui
 /* number of exact key limbs the device format uses for these parameters */
 uint32_t concrete_hip_bsk_limbs(uint32_t polynomial_size, uint32_t level_count, uint32_t base_log);
 /* device key format of (k, N, l): 0 unsupported, 1 / 2 the N = 1024 / 2048 (k = 1) kernels' layouts,
- * 3 the general path (pbs_generic.hip), 4 the k = 2, N = 1024, l <= 3 kernel's layout (pbs1024k2.hip,
+ * 3 the general path (pbs_generic.hip), 4 the k = 2, N = 1024 kernels' layout (pbs1024k2.hip,
  * round 4), 5 the small-ring kernels' (N = 512, k = 3 / N = 256, k = 5, 6, l <= 3: pbs_small.hip; N = 512,
- * k = 4, l <= 5: pbs512k4.hip; round 4); code 2 covers N = 2048, l <= 4; *limbs
+ * k = 4, any l: pbs512k4.hip; round 4); code 2 covers N = 2048, l <= 4; *limbs
  * balanced key limbs of *limb_bits bits each */
 int concrete_hip_bsk_format(uint32_t glwe_dim, uint32_t polynomial_size, uint32_t level_count, uint32_t *limbs,
                             uint32_t *limb_bits);

@@ -26,12 +26,14 @@
 // writer in concrete_amd/keys.py (single-segment, single-far and double-far layouts) and checks
 // malformed messages are refused.  The restated level orders of the standard layouts are checked
 // on read whenever the message carries the client secret keys (a Keyset): check_level_order.
+#include <math.h>
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <exception>
 #include <initializer_list>
 #include <mutex>
@@ -50,8 +52,18 @@ struct concrete_hip_server_keyset {
     concrete_hip_key_info info;
     std::vector<uint64_t> payload;  // concatenated blobs (u64 words)
     // level order found when the key was last expanded against the client secret keys
-    // (CONCRETE_HIP_LEVEL_ORDER_*); mutable: expansion is a const read of the keyset
-    mutable int level_order = 0;
+    // (CONCRETE_HIP_LEVEL_ORDER_*).  Expansion is a const read of the keyset that several threads may
+    // run on one key at once: the field is atomic (every expansion of one key finds the same order).
+    struct Order {
+      std::atomic<int> v{0};
+      Order() = default;
+      Order(const Order& o) : v(o.v.load()) {}
+      Order& operator=(const Order& o) {
+        v.store(o.v.load());
+        return *this;
+      }
+    };
+    mutable Order level_order;
   };
   struct Secret {  // a client LweSecretKey (Keyset.client, concrete-protocol.capnp:139-145, 298-303)
     uint32_t id = 0;
@@ -607,19 +619,32 @@ inline uint64_t tdist(uint64_t a, uint64_t b) {
   const uint64_t d = a - b;
   return (int64_t)d < 0 ? 0 - d : d;
 }
-// Classify per-level decryptions d[v] against the expected scales e[v] and their reversal.
-int classify_levels(const std::vector<uint64_t>& d, const std::vector<uint64_t>& e) {
+// Classify the per-level decryptions d[p][v] (p over checked mask positions) against the expected
+// scales e[v] and their reversal.  The order is decided by the most significant level, whose scale
+// sits far above any key's noise; a deeper level is compared too only when its scale / 4 is at
+// least 64 sigma of the key's noise (sigma from the key's variance field; unknown: top level only).
+// A keyswitch key at secure noise puts its deepest level at the noise floor by design (CFG4's
+// n = 742, l = 5, logB = 3: sigma ~ 2^47.6 against scale / 4 = 2^47), so requiring every level to
+// decrypt would refuse valid keys.  Junk passes one position's top-level check with
+// probability ~2^-(logB + 1) per order; every checked position must agree.
+int classify_levels(const std::vector<std::vector<uint64_t>>& d, const std::vector<uint64_t>& e, double sigma) {
   const size_t l = e.size();
+  size_t vt = 0;
+  for (size_t v = 1; v < l; ++v)
+    if (e[v] > e[vt]) vt = v;
+  const double floor = 256.0 * sigma;  // scale / 4 >= 64 sigma
+  auto resolvable = [&](size_t v) { return v == vt || (sigma > 0.0 && (double)e[v] >= floor); };
   bool as_is = true, reversed = true;
-  for (size_t v = 0; v < l; ++v) {
-    const uint64_t de = tdist(d[v], e[v]), dr = tdist(d[v], e[l - 1 - v]);
-    // a level decrypts to its scale up to noise far below the gap between neighbouring scales
-    if (!(de < e[v] / 4)) as_is = false;
-    if (!(dr < e[l - 1 - v] / 4)) reversed = false;
-  }
-  if (as_is) return CONCRETE_HIP_LEVEL_ORDER_AS_EXPECTED;
-  if (reversed) return CONCRETE_HIP_LEVEL_ORDER_REVERSED;
-  return -1;
+  for (const auto& dp : d)
+    for (size_t v = 0; v < l; ++v) {
+      // stored position v holds expected scale e[v] (as is) or e[l - 1 - v] (reversed)
+      if (resolvable(v) && !(tdist(dp[v], e[v]) < e[v] / 4)) as_is = false;
+      const size_t r = l - 1 - v;
+      if (resolvable(r) && !(tdist(dp[v], e[r]) < e[r] / 4)) reversed = false;
+    }
+  if (as_is && !reversed) return CONCRETE_HIP_LEVEL_ORDER_AS_EXPECTED;
+  if (reversed && !as_is) return CONCRETE_HIP_LEVEL_ORDER_REVERSED;
+  return -1;  // neither, or both (indistinguishable): refuse
 }
 
 // key: standard-domain words; returns CONCRETE_HIP_LEVEL_ORDER_* or -1 (refuse)
@@ -631,37 +656,46 @@ int check_level_order(const concrete_hip_server_keyset* ks, const concrete_hip_k
   const auto* s_in = ks->secret(i.input_id, i.input_lwe_dim);
   const auto* s_out = ks->secret(i.output_id, n_out);
   if (!s_in || !s_out) return CONCRETE_HIP_LEVEL_ORDER_UNCHECKED;
-  uint64_t pos = 0;
-  while (pos < i.input_lwe_dim && s_in->words[pos] != 1) ++pos;
-  if (pos == i.input_lwe_dim) return CONCRETE_HIP_LEVEL_ORDER_UNCHECKED;
-  std::vector<uint64_t> d(l), e(l);
+  // up to 16 mask positions whose secret bit is 1 (each row decryption is one constant coefficient:
+  // O(k N) or O(n_out) work)
+  constexpr size_t MAX_POS = 16;
+  std::vector<uint64_t> pos;
+  for (uint64_t m = 0; m < i.input_lwe_dim && pos.size() < MAX_POS; ++m)
+    if (s_in->words[m] == 1) pos.push_back(m);
+  if (pos.empty()) return CONCRETE_HIP_LEVEL_ORDER_UNCHECKED;
+  std::vector<std::vector<uint64_t>> d(pos.size(), std::vector<uint64_t>(l));
+  std::vector<uint64_t> e(l);
   const uint64_t* so = s_out->words.data();
-  if (is_bsk) {
-    // [n][l][k+1 rows][k+1 polys][N]: row k of level v, constant coefficient of B - sum_r A_r S_r
-    const uint64_t k = i.glwe_dim, N = i.poly_size, glwe = (k + 1) * N;
-    for (uint32_t v = 0; v < l; ++v) {
-      const uint64_t* ct = key + (((uint64_t)pos * l + v) * (k + 1) + k) * glwe;
-      uint64_t acc = ct[k * N];
-      for (uint64_t r = 0; r < k; ++r) {
-        const uint64_t* a = ct + r * N;
-        const uint64_t* sr = so + r * N;
-        acc -= a[0] * sr[0];
-        for (uint64_t j = 1; j < N; ++j) acc += a[j] * sr[N - j];  // negacyclic: X^N = -1
+  for (size_t pi = 0; pi < pos.size(); ++pi) {
+    if (is_bsk) {
+      // [n][l][k+1 rows][k+1 polys][N]: row k of level v, constant coefficient of B - sum_r A_r S_r
+      const uint64_t k = i.glwe_dim, N = i.poly_size, glwe = (k + 1) * N;
+      for (uint32_t v = 0; v < l; ++v) {
+        const uint64_t* ct = key + ((pos[pi] * l + v) * (k + 1) + k) * glwe;
+        uint64_t acc = ct[k * N];
+        for (uint64_t r = 0; r < k; ++r) {
+          const uint64_t* a = ct + r * N;
+          const uint64_t* sr = so + r * N;
+          acc -= a[0] * sr[0];
+          for (uint64_t j = 1; j < N; ++j) acc += a[j] * sr[N - j];  // negacyclic: X^N = -1
+        }
+        d[pi][v] = acc;
+        e[v] = 1ull << (64 - logB * (v + 1));
       }
-      d[v] = acc;
-      e[v] = 1ull << (64 - logB * (v + 1));
-    }
-  } else {
-    // [n_in][l][n_out + 1]: row t decrypts to s_in[pos] 2^(64 - logB (l - t))
-    for (uint32_t t = 0; t < l; ++t) {
-      const uint64_t* ct = key + ((uint64_t)pos * l + t) * (n_out + 1);
-      uint64_t acc = ct[n_out];
-      for (uint64_t j = 0; j < n_out; ++j) acc -= ct[j] * so[j];
-      d[t] = acc;
-      e[t] = 1ull << (64 - logB * (l - t));
+    } else {
+      // [n_in][l][n_out + 1]: row t decrypts to s_in[pos] 2^(64 - logB (l - t))
+      for (uint32_t t = 0; t < l; ++t) {
+        const uint64_t* ct = key + (pos[pi] * l + t) * (n_out + 1);
+        uint64_t acc = ct[n_out];
+        for (uint64_t j = 0; j < n_out; ++j) acc -= ct[j] * so[j];
+        d[pi][t] = acc;
+        e[t] = 1ull << (64 - logB * (l - t));
+      }
     }
   }
-  const int c = classify_levels(d, e);
+  // the key's noise: concrete-protocol's variance is on the unit torus
+  const double sigma = (i.variance > 0.0 && i.variance < 1.0) ? sqrt(i.variance) * 18446744073709551616.0 : 0.0;
+  const int c = classify_levels(d, e, sigma);
   if (c != CONCRETE_HIP_LEVEL_ORDER_REVERSED) return c;
   // re-order: reverse the level blocks of every mask position
   const uint64_t blk = is_bsk ? ((uint64_t)i.glwe_dim + 1) * ((uint64_t)i.glwe_dim + 1) * i.poly_size : n_out + 1;
@@ -689,7 +723,7 @@ int expand(const concrete_hip_server_keyset* ks, const concrete_hip_server_keyse
               "level order", is_bsk ? "bootstrap key" : "keyswitch key", k.info.id);
     return -3;
   }
-  k.level_order = order;
+  k.level_order.v.store(order);
   return 0;
 }
 
@@ -900,7 +934,7 @@ int concrete_hip_server_keyset_level_order(const concrete_hip_server_keyset* sk,
     set_error("server_keyset_level_order: bad argument or index %u", index);
     return -3;
   }
-  return (is_bsk ? sk->bsk[index] : sk->ksk[index]).level_order;
+  return (is_bsk ? sk->bsk[index] : sk->ksk[index]).level_order.v.load();
 }
 
 uint32_t concrete_hip_server_keyset_secret_count(const concrete_hip_server_keyset* sk) {

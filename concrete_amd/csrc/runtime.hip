@@ -210,9 +210,10 @@ uint64_t* slot_buf(SliceSlot& sl, int i, uint64_t bytes) {
   return (uint64_t*)sl.buf[i];
 }
 
-void mark(concrete_hip_keyset* ks, SliceSlot& sl, int i) {
-  // (timing is switched between calls; a racy read only decides whether an event is recorded)
-  if (ks->timing) CHIP_CHECK(hipEventRecord(sl.ev[i], sl.s));
+void mark(concrete_hip_keyset*, SliceSlot& sl, int i) {
+  // sl.timing is the keyset's flag captured when the call started (re-reading it here
+  // raced with set_timing, leaving some events unrecorded before their readback)
+  if (sl.timing) CHIP_CHECK(hipEventRecord(sl.ev[i], sl.s));
 }
 
 // Run body(slot, start, count) for every contiguous slice of the batch, one host thread per slice
@@ -236,10 +237,13 @@ void run_sliced(concrete_hip_keyset* ks, uint64_t num_samples, F&& body) {
     slice_of(num_samples, parts, r, start[r], count[r]);
   }
   bool timing;
+  uint64_t epoch;
   {
     std::lock_guard<std::mutex> g(ks->call_m);
     timing = ks->timing;
+    epoch = ks->timing_epoch;
   }
+  for (uint64_t r = 0; r < parts; ++r) slots[r].timing = timing;
   auto slice = [&](uint64_t r) {
     SliceSlot& sl = slots[r];
     body(sl, start[r], count[r]);
@@ -263,7 +267,10 @@ void run_sliced(concrete_hip_keyset* ks, uint64_t num_samples, F&& body) {
   if (timing) {
     std::vector<double> tl(parts * 6, 0.0);
     std::lock_guard<std::mutex> g(ks->call_m);
-    for (uint64_t r = 0; r < parts && ks->timing; ++r) {
+    // every event of this call was recorded (sl.timing); timing switched off or re-based since the
+    // call started: its events are not on the current time axis, so they are dropped
+    const bool same_epoch = ks->timing && ks->timing_epoch == epoch;
+    for (uint64_t r = 0; r < parts && same_epoch; ++r) {
       SliceSlot& sl = slots[r];
       if (!ks->timing_base[sl.gpu]) continue;  // a device added after timing was enabled
       CHIP_CHECK(hipSetDevice((int)sl.gpu));
@@ -276,7 +283,7 @@ void run_sliced(concrete_hip_keyset* ks, uint64_t num_samples, F&& body) {
       }
       t[5] = (double)count[r];
     }
-    if (ks->timing) ks->timeline.insert(ks->timeline.end(), tl.begin(), tl.end());
+    if (same_epoch) ks->timeline.insert(ks->timeline.end(), tl.begin(), tl.end());
   }
   return_set(ks, set);
 }
@@ -514,6 +521,7 @@ void concrete_hip_keyset_set_timing(concrete_hip_keyset* ks, int enable) {
   std::lock_guard<std::mutex> call(ks->call_m);
   ks->timeline.clear();
   ks->timing = false;
+  ++ks->timing_epoch;
   if (!enable) return;
   // one base event per device, in the past of every later call: slices of different calls (and
   // streams) share the time axis

@@ -140,6 +140,7 @@ struct SliceSlot {
   std::vector<void*> retired;  // outgrown buffers, freed once every slice thread has joined
   HostBuf stage_in, stage_out, stage_lut;  // page-locked staging of the caller's (pageable) memrefs
   uint32_t* status_h = nullptr;  // page-locked landing word of the stream-ordered status read
+  bool timing = false;           // this call records its events (captured once at the call's start)
 };
 
 // The slots of one call.  A keyset keeps a pool of them: concurrent calls on one keyset (several
@@ -166,6 +167,7 @@ struct concrete_hip_keyset {
   std::mutex call_m;
   std::vector<chip::SlotSet*> idle_sets, all_sets;
   bool timing = false;
+  uint64_t timing_epoch = 0;  // bumped by every set_timing: a call's events are read back only in its epoch
   hipEvent_t timing_base[chip::RT_MAX_DEV] = {};  // recorded when timing was enabled, per device
   std::vector<double> timeline;  // 6 per slice of every call since timing was enabled
 };

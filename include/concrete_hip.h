@@ -119,7 +119,9 @@ int concrete_hip_pbs_supported(uint32_t glwe_dim, uint32_t polynomial_size, uint
  * n_out + 1 <= 65536; else 0 (round 4) */
 int concrete_hip_keyswitch_supported(uint32_t level_count, uint32_t base_log, uint32_t input_lwe_dim,
                                      uint32_t output_lwe_dim);
-/* number of exact key limbs the device format uses for these parameters */
+/* DEPRECATED (kept for ABI version 2 callers): number of exact key limbs of the device format for
+ * k = 1 only (it takes no glwe_dim; the k-dependent formats of round 4 differ, e.g. 5 limbs at
+ * k = 4, N = 512, l = 2).  Use concrete_hip_bsk_format, which takes k. */
 uint32_t concrete_hip_bsk_limbs(uint32_t polynomial_size, uint32_t level_count, uint32_t base_log);
 /* device key format of (k, N, l): 0 unsupported, 1 / 2 the N = 1024 / 2048 (k = 1) kernels' layouts,
  * 3 the general path (pbs_generic.hip), 4 the k = 2, N = 1024 kernels' layout (pbs1024k2.hip,

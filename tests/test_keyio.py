@@ -439,8 +439,9 @@ def test_level_order_checked_against_client_keys():
     assert lwe_sk.any() and glwe_sk.any()
     bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 33, std=2.0 ** -45)
     ksk = B.ksk_generate(p, glwe_sk, lwe_sk, 34, std=2.0 ** -45)
-    bi = [K.bsk_info(p, id=i, input_id=0, output_id=1) for i in range(3)]
-    ki = [K.ksk_info(p, id=10 + i, input_id=1, output_id=0) for i in range(3)]
+    var = (2.0 ** -45) ** 2  # every level's scale is far above this noise: all levels are compared
+    bi = [K.bsk_info(p, id=i, input_id=0, output_id=1, variance=var) for i in range(3)]
+    ki = [K.ksk_info(p, id=10 + i, input_id=1, output_id=0, variance=var) for i in range(3)]
     rng = np.random.default_rng(35)
     junk_b = rng.integers(0, 2 ** 64, size=bsk.size, dtype=np.uint64)
     junk_k = rng.integers(0, 2 ** 64, size=ksk.size, dtype=np.uint64)
@@ -461,3 +462,49 @@ def test_level_order_checked_against_client_keys():
     srv = K.ServerKeyset.deserialize(K.serialize_server_keyset(bsks[:2], ksks[:2]))
     assert srv.secret_count == 0
     assert np.array_equal(srv.bsk(1), bsks[1][1]) and srv.level_order("bsk", 1) == "unchecked"
+
+
+@pytest.mark.parametrize("name,n,l,logb", [
+    ("cfg4_ks", 742, 5, 3),    # BASELINE configs[3]'s keyswitch: deepest level at the noise floor
+    ("opt7_ks", 915, 5, 3),    # v0_last_128 7-bit row's keyswitch
+    ("v0_l23", 880, 23, 1),    # 23 levels of 1 bit: most levels below the noise
+])
+def test_level_order_at_secure_noise(name, n, l, logb):
+    """keys generated at the secure noise (secure_std(1, n), the KSK's output
+    dimension) put the deepest keyswitch levels at or below the noise floor.  The order is decided by
+    the most significant level, deeper levels are compared only where their scale clears 64 sigma of
+    the key's variance: such keys read back 'as_expected', and their level-reversed copies
+    'reversed' (re-ordered), whatever the noise draws."""
+    from dataclasses import dataclass
+
+    from concrete_amd import backend as B
+
+    @dataclass
+    class P:
+        n: int
+        k: int
+        N: int
+        ks_level: int
+        ks_base_log: int
+
+        @property
+        def big_n(self):
+            return self.k * self.N
+
+        ksk_len = property(lambda s: s.big_n * s.ks_level * (s.n + 1))
+
+    # only the first 64 input positions carry key rows here (the check reads up to 16 positions
+    # whose secret bit is 1); the rest of the key is irrelevant to the level order
+    p = P(n=n, k=1, N=64, ks_level=l, ks_base_log=logb)
+    std = B.secure_std(1, n)
+    glwe_sk = B.binary_key(p.big_n, 41)
+    lwe_sk = B.binary_key(n, 42)
+    ksk = B.ksk_generate(p, glwe_sk, lwe_sk, 43, std=std)
+    info = [K.KeyInfo(id=i, input_id=1, output_id=0, level_count=l, base_log=logb, input_lwe_dim=p.big_n,
+                      output_lwe_dim=n, variance=std * std) for i in range(2)]
+    rev = _reverse_levels(ksk, p.big_n, l)
+    data = K.serialize_server_keyset([], [(info[0], ksk), (info[1], rev)], root="keyset", layout="mixed",
+                                     secrets=[(0, lwe_sk), (1, glwe_sk)])
+    sk = K.ServerKeyset.deserialize(data, "keyset")
+    assert np.array_equal(sk.ksk(0), ksk) and sk.level_order("ksk", 0) == "as_expected"
+    assert np.array_equal(sk.ksk(1), ksk) and sk.level_order("ksk", 1) == "reversed"

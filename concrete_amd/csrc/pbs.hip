@@ -34,6 +34,7 @@
 #include "fft512.hpp"
 #include "kernel_util.hpp"
 #include "pbs.hpp"
+#include "pbs_hex.hpp"
 
 namespace chip {
 
@@ -580,6 +581,13 @@ static int launch_pair(const PbsArgs& a) {
   // (at 2 per CU, B = 512, it measured 0.9x the pair kernel: DESIGN.md §4.1).  CONCRETE_HIP_PBS_QUAD=0
   // keeps the pair kernel, =1 / =2 forces it with that many ciphertexts per workgroup (read per
   // call: tests, A/B).
+  // six waves per ciphertext (pbs1024_hex.hip): CONCRETE_HIP_PBS_HEX=1 / =2 forces it with that many
+  // ciphertexts per workgroup (read per call: tests, A/B)
+  if (L == 3) {
+    const char* he = getenv("CONCRETE_HIP_PBS_HEX");
+    const int hx = he ? atoi(he) : 0;
+    if (hx == 1 || hx == 2) return pbs1024_hex_launch(a, hx);
+  }
   if (L == 3 && P <= 2 && !getenv("CONCRETE_HIP_PBS_STAMPS")) {
     const char* qe = getenv("CONCRETE_HIP_PBS_QUAD");
     const int q = qe ? atoi(qe) : -1;

@@ -1,0 +1,341 @@
+// pbs1024_hex.hip — the N = 1024, k = 1, l = 3 PBS (cfg2) with six waves per ciphertext.
+//
+// Same semantics, Fourier key, key layout and exact arithmetic as pbs1024_pair_kernel (pbs.hip;
+// reference call site: tfhe-cuda-backend cuda_programmable_bootstrap_lwe_ciphertext_vector_64 as
+// invoked by compiler lib/Runtime/wrappers.cpp:237-240 and lib/Runtime/GPUDFG.cpp:1214-1218,
+// semantics concrete-cpu c_api/bootstrap.rs:347-414, restated in oracle/tfhe_oracle.c:ora_pbs).
+//
+// Why: at <= 2 ciphertexts per CU (the metric's whole-node batch of 4096 is 512 per GPU on 8 GPUs)
+// the pair kernel runs one wave per SIMD, and a lone wave is latency-bound.  A
+// ciphertext's CMUX step holds 6 forward transforms (2 polynomials x 3 levels) and 6 inverse
+// transforms (2 output polynomials x 3 key limbs), so six waves take one of each — a balanced split
+// with the register fft512 unchanged — and two ciphertexts per workgroup put three waves on every
+// SIMD.  Wave u = 3 c + j of a ciphertext:
+//   * rotation and decomposition of polynomial c (its negated accumulator B_c = -acc_c lives in LDS,
+//     shared by the three waves of c), digits of level j, forward transform of that digit
+//     polynomial, spectrum published in the wave's scratch (all 8 frequency slots);
+//   * key product of output polynomial c, key limb j over the six published spectra (LDS) with the
+//     wave's own slice of the Fourier key (straight from L2 into registers, two level batches ahead:
+//     no LDS ring, no workgroup barriers);
+//   * inverse transform of that product, exact rounding, and the limb's contribution added into B_c
+//     with 64-bit LDS atomics (integer adds mod 2^64: exact in any order).
+// Synchronisation per CMUX step, on per-wave LDS counters (one monotonic count, three events):
+//   A: the six spectra of the ciphertext are published (before the key products read them);
+//   B: every wave of the ciphertext has issued its spectrum reads (before a scratch is overwritten
+//      by the inverse transpose);
+//   C: the three waves of polynomial c have added their limbs (before the next rotation reads B_c).
+// The spectra come out of fft512_fwd in its natural (lane, slot) frequency order, which is the
+// order of the key layout (bsk.hip: group (limb, co, ro) holds column co / row ro in slots 0..3 and
+// column 1 - co / row 1 - ro in slots 4..7, so wave (c, j) reads slots 0..3 of groups (j, c, r) and
+// slots 4..7 of groups (j, 1 - c, 1 - r)).
+#include "common.hpp"
+#include "fft512.hpp"
+#include "kernel_util.hpp"
+#include "pbs.hpp"
+#include "pbs_hex.hpp"
+
+namespace chip {
+
+namespace {
+
+constexpr uint64_t HX_MAGIC_ALL = RND_MAGIC_BITS + (RND_MAGIC_BITS << 22) + (RND_MAGIC_BITS << 43);
+constexpr int hx_limb_shift(int li) { return li * 21 + (li > 0 ? 1 : 0); }
+
+__device__ __forceinline__ void hx_signal(uint32_t* ctr, uint32_t& cnt) {
+  asm volatile("" ::: "memory");
+  ++cnt;
+  __hip_atomic_store(ctr, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// wait until counters ctr[0 .. NC) all reach target: the NC reads are issued together per poll
+template <int NC>
+__device__ __forceinline__ void hx_wait(const uint32_t* ctr, uint32_t target, const SyncGuard& guard) {
+  for (uint32_t it = 0;; ++it) {
+    uint32_t lo = 0xffffffffu;
+#pragma unroll
+    for (int o = 0; o < NC; ++o) {
+      const uint32_t x = __hip_atomic_load(ctr + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      lo = x < lo ? x : lo;
+    }
+    if (lo >= target) break;
+    if (it >= guard.spin_limit) {
+      __hip_atomic_fetch_or(guard.status, DEV_STATUS_SYNC_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(0);
+  }
+  asm volatile("" ::: "memory");
+}
+
+}  // namespace
+
+template <int CTS, bool RESID, bool STAMPS = false>
+__global__ void __launch_bounds__(CTS * 384, 1)
+pbs1024_hex_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_idx,
+                   const uint64_t* __restrict__ luts, const uint64_t* __restrict__ lut_idx,
+                   const uint64_t* __restrict__ in, const uint64_t* __restrict__ in_idx,
+                   const cplx* __restrict__ fbsk, uint32_t n, uint32_t base_log, uint32_t num_samples,
+                   unsigned long long* __restrict__ resid_out, SyncGuard guard) {
+  constexpr int K = 1, K1 = 2, N = 1024, LOG2_2N = 11, LIMBS = 3, L = 3;
+  constexpr int GROUP = L * 512;                      // one (limb, co, ro) group: the L level spectra
+  constexpr int PER_I = K1 * K1 * LIMBS * GROUP;      // complex values per Fourier GGSW
+  constexpr int XS = (int)PBS1024_XCH_SLOTS;
+  constexpr int NW = 6 * CTS;
+  static_assert(XCH_SLOTS <= XS, "transpose scratch");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  cplx* tbl = reinterpret_cast<cplx*>(smem);
+  cplx* xch_all = tbl + FFT512_TABLE_ENTRIES;                               // NW scratches
+  uint64_t* acc_all = reinterpret_cast<uint64_t*>(xch_all + NW * XS);       // CTS x 2 x N: B_c
+  uint32_t* hf = reinterpret_cast<uint32_t*>(acc_all + CTS * K1 * N);       // 8 counters per ciphertext
+
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int ctl = w / 6, u = w - 6 * ctl;
+  const int c = u >= 3 ? 1 : 0, j = u - 3 * c;
+  const uint32_t s = blockIdx.x * CTS + ctl;
+  const bool active = s < num_samples;
+  cplx* xch = xch_all + w * XS;
+  const cplx* spec = xch_all + (ctl * 6) * XS;  // spectrum (r, q) at spec + (3 r + q) XS
+  uint64_t* accc = acc_all + (ctl * K1 + c) * N;
+  uint32_t* myctr = hf + ctl * 8 + u;
+  const uint32_t* ctctr = hf + ctl * 8;         // the ciphertext's six counters
+  const uint32_t* polyctr = hf + ctl * 8 + 3 * c;
+
+  const uint64_t* lwe = in + (active ? (in_idx ? in_idx[s] : s) : 0) * (uint64_t)(n + 1);
+  const uint64_t* lut = luts + (active && lut_idx ? lut_idx[s] : 0ull) * (uint64_t)(K1 * N);
+
+  build_fft512_tables(tbl, threadIdx.x, NW * 64);
+  if (lane == 0) *myctr = 0u;
+  // acc_c = LUT_c * X^{-ms(b)} (blind_rotate_assign: polynomial_wrapping_monic_monomial_div), stored
+  // negated (pbs1024_pair_kernel): written by wave j = 0 of each polynomial
+  if (j == 0) {
+    const uint32_t bt = active ? modswitch(lwe[n], LOG2_2N) : 0u;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const uint32_t src = (uint32_t)(lane + 64 * m + bt) & (2 * N - 1);
+      const uint64_t v = active ? lut[c * N + (src & (N - 1))] : 0ull;
+      accc[lane + 64 * m] = src < N ? 0ull - v : v;
+    }
+  }
+  uint32_t cnt = 0;
+  __syncthreads();
+  const Fft512Tables T = fft512_tables_at(tbl);
+
+  const int nrep = 64 - L * (int)base_log;
+  const int logB = (int)base_log;
+  const int32_t neg_base = -(1 << logB);
+  const uint32_t half_m1 = (1u << (logB - 1)) - 1u;
+  const uint32_t khi = 1u << (nrep - 33);  // 2^(nrep-1) in the high word (nrep >= 37 under the gate)
+  double max_resid = 0.0;
+  // diagnostic stamps (STAMPS builds only): cycles per phase, summed over the steps
+  uint64_t acc_t[NSTAMP] = {};
+  uint64_t t_begin = 0, tp = 0;
+  auto lap = [&](int k) __attribute__((always_inline)) {
+    if constexpr (STAMPS) {
+      const uint64_t t = stamp();
+      acc_t[k] += t - tp;
+      tp = t;
+    }
+  };
+  if constexpr (STAMPS) t_begin = tp = stamp();
+
+  // ---- this wave's key slice: output column c, limb j.  Slots 0..3 of row r: group (j, c, r);
+  //      slots 4..7 of row r: group (j, 1 - c, 1 - r) (the pair layout's own/other halves).
+  const cplx* key_lo = fbsk + (uint64_t)(((j * K1 + c) * K1) * GROUP) + lane;            // + r GROUP
+  const cplx* key_hi = fbsk + (uint64_t)(((j * K1 + (1 - c)) * K1 + 1) * GROUP) + lane;  // - r GROUP
+  // batch b = (r, q) = (b / L, b % L): the 8 slots of that row and level
+  auto load_batch = [&](cplx (&g)[8], uint64_t step_off, int b) __attribute__((always_inline)) {
+    const int r = b / L, q = b % L;
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) g[k2] = key_lo[step_off + r * GROUP + q * 512 + k2 * 64];
+#pragma unroll
+    for (int k2 = 4; k2 < 8; ++k2) g[k2] = key_hi[step_off - r * GROUP + q * 512 + k2 * 64];
+  };
+  cplx g0[8], g1[8];
+  if (n > 0) {
+    load_batch(g0, 0, 0);
+    load_batch(g1, 0, 1);
+  }
+
+  uint64_t a_next = active && n > 0 ? lwe[0] : 0ull;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t step_off = (uint64_t)i * PER_I;
+    const uint64_t next_off = i + 1 < n ? step_off + PER_I : step_off;  // past the last step: re-read (unused)
+    const uint64_t ai = a_next;
+    if (i + 1 < n) a_next = active ? lwe[i + 1] : 0ull;
+    const uint32_t at = modswitch(ai, LOG2_2N);
+
+    // ---- ct1 = acc X^at - acc = B - X^at B of polynomial c (pbs1024_pair_kernel's offsets: bit 13
+    //      of o says "src < N", i.e. no wrap, where the rotated term is subtracted), decomposer state
+    uint32_t st[16];
+    {
+      const uint32_t o0 = ((uint32_t)(lane - (int)at) << 3) + 8u * N;
+      const char* accb = reinterpret_cast<const char*>(accc);
+      uint64_t rv[16], bv[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        rv[m] = *reinterpret_cast<const uint64_t*>(accb + ((o0 + 512u * m) & 8191u));
+        bv[m] = accc[lane + 64 * m];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const uint32_t o = o0 + 512u * m;
+        const uint32_t s32 = (uint32_t)((int32_t)(o << 18) >> 31);
+        const uint64_t rvs = rv[m] ^ (((uint64_t)s32 << 32) | s32);
+        const uint64_t x = bv[m] + rvs + (uint64_t)(s32 & 1u);
+        st[m] = ((uint32_t)(x >> 32) + khi) >> (nrep - 32);
+      }
+    }
+
+    lap(0);  // rotation + state
+    // ---- digits of level j (levels below j only carry into it), forward transform, publish
+    {
+      int32_t d[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        int32_t dig = 0;
+#pragma unroll
+        for (int q = 0; q < L; ++q)
+          if (q <= j) dig = decomp_level32(st[m], (uint32_t)(q * logB), logB, half_m1, neg_base, q < j);
+        d[m] = dig;
+      }
+      cplx v[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) v[m] = {(double)d[m], (double)d[m + 8]};
+      fft512_fwd(v, xch, T, lane, 0ull);
+      // my scratch was last read by my own transpose (wave order); B of the previous step released it
+#pragma unroll
+      for (int k2 = 0; k2 < 8; ++k2) xch[k2 * 64 + lane] = v[k2];
+    }
+    lap(1);  // digits + forward + publish
+    hx_signal(myctr, cnt);  // A
+    hx_wait<6>(ctctr, cnt, guard);
+    lap(2);  // wait A
+
+    // ---- key product of output c, limb j over the six spectra; the key two batches ahead
+    cplx Y[8];
+#pragma unroll
+    for (int b = 0; b < K1 * L; ++b) {
+      const int r = b / L, q = b % L;
+      const cplx* X = spec + (r * L + q) * XS + lane;
+      cplx x[8];
+#pragma unroll
+      for (int k2 = 0; k2 < 8; ++k2) x[k2] = X[k2 * 64];
+      cplx (&g)[8] = (b & 1) ? g1 : g0;
+#pragma unroll
+      for (int k2 = 0; k2 < 8; ++k2) {
+        if (b == 0) {  // fma(a, b, 0) == a * b: the same bits as accumulating from zero
+          Y[k2].re = __builtin_fma(x[k2].re, g[k2].re, -x[k2].im * g[k2].im);
+          Y[k2].im = __builtin_fma(x[k2].re, g[k2].im, x[k2].im * g[k2].re);
+        } else {
+          Y[k2].re = __builtin_fma(x[k2].re, g[k2].re, __builtin_fma(-x[k2].im, g[k2].im, Y[k2].re));
+          Y[k2].im = __builtin_fma(x[k2].re, g[k2].im, __builtin_fma(x[k2].im, g[k2].re, Y[k2].im));
+        }
+      }
+      if (b == K1 * L - 1) hx_signal(myctr, cnt);  // B: every spectrum read of this wave is issued
+      // refill: batch b + 2 of this step, or batch b + 2 - 6 of the next
+      if (b + 2 < K1 * L) load_batch(g, step_off, b + 2);
+      else load_batch(g, next_off, b + 2 - K1 * L);
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) pin(Y[k2]);
+    lap(3);  // key products
+
+    // ---- inverse transform of (c, j): my scratch is rewritten only after every wave of the
+    //      ciphertext has read the spectra (B)
+    hx_wait<6>(ctctr, cnt, guard);
+    lap(4);  // wait B
+    fft512_inv(Y, xch, T, lane, 0ull);
+    {
+      // limb j's exact integers, negated (B = -acc), shifted; limb 0 removes the constant of all limbs
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const double tr = RND_MAGIC - Y[m].re, ti = RND_MAGIC - Y[m].im;
+        if constexpr (RESID) {
+          max_resid = fmax(max_resid, fabs(Y[m].re - (RND_MAGIC - tr)));
+          max_resid = fmax(max_resid, fabs(Y[m].im - (RND_MAGIC - ti)));
+        }
+        uint64_t cre, cim;
+        if (j == 0) {
+          cre = (uint64_t)__double_as_longlong(tr) - HX_MAGIC_ALL;
+          cim = (uint64_t)__double_as_longlong(ti) - HX_MAGIC_ALL;
+        } else {
+          const int sh = j == 1 ? hx_limb_shift(1) : hx_limb_shift(2);
+          cre = (uint64_t)__double_as_longlong(tr) << sh;
+          cim = (uint64_t)__double_as_longlong(ti) << sh;
+        }
+        __hip_atomic_fetch_add(&accc[lane + 64 * m], cre, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(&accc[lane + 64 * (m + 8)], cim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    lap(5);  // inverse + rounding + atomic adds
+    hx_signal(myctr, cnt);  // C
+    hx_wait<3>(polyctr, cnt, guard);
+    lap(7);  // wait C
+  }
+  if constexpr (STAMPS) {
+    acc_t[6] = stamp() - t_begin;
+    if (lane == 0 && resid_out) {
+      unsigned long long* dst = resid_out + ((uint64_t)blockIdx.x * NW + w) * NSTAMP;
+      for (int q = 0; q < NSTAMP; ++q) dst[q] = acc_t[q];
+    }
+  }
+
+  // ---- sample extract (nth = 0) of acc = -B: out[j'] = -acc_0[N - j'] (j' > 0), acc_0[0]; body acc_1[0].
+  //      The three waves of polynomial 0 split the mask words (m = j mod 3); wave (1, 0) the body.
+  //      (B_1 is final once polynomial 1's last C sync has passed: the waves of polynomial 1 only.)
+  uint64_t* o = out + (active ? (out_idx ? out_idx[s] : s) : 0) * (uint64_t)(K * N + 1);
+  if (active) {
+    if (c == 0) {
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        if (m % 3 != j) continue;
+        const int jj = lane + 64 * m;
+        const uint64_t val = accc[(N - jj) & (N - 1)];
+        o[jj] = jj == 0 ? 0ull - val : val;
+      }
+    } else if (j == 0 && lane == 0) {
+      o[K * N] = 0ull - accc[0];
+    }
+  }
+
+  if constexpr (RESID && !STAMPS) {
+    for (int off = 32; off > 0; off >>= 1) max_resid = fmax(max_resid, __shfl_xor(max_resid, off));
+    if (lane == 0 && active && resid_out) atomicMax(resid_out, (unsigned long long)__double_as_longlong(max_resid));
+  }
+}
+
+template <int CTS, bool RESID, bool STAMPS = false>
+static int launch_hex_t(const PbsArgs& a) {
+  const size_t lds = pbs1024_hex_lds_bytes(CTS);
+  auto kern = pbs1024_hex_kernel<CTS, RESID, STAMPS>;
+  CHIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const uint32_t blocks = (a.num_samples + CTS - 1) / CTS;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(CTS * 384), lds, a.stream, a.out, a.out_idx, a.luts, a.lut_idx, a.in,
+                     a.in_idx, reinterpret_cast<const cplx*>(a.fbsk), a.n, a.base_log, a.num_samples, a.resid,
+                     a.guard);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("pbs launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+int pbs1024_hex_launch(const PbsArgs& a, int cts) {
+  if (!(a.N == 1024 && a.k == 1 && a.level == 3 && a.limbs == 3 && pbs1024_exact(1, 3, a.base_log))) {
+    set_error("unsupported PBS parameters for the six-wave kernel: N=%u k=%u level=%u base_log=%u", a.N, a.k,
+              a.level, a.base_log);
+    return -2;
+  }
+  if (a.num_samples == 0) return 0;
+  // diagnostic: CONCRETE_HIP_PBS_STAMPS=1 runs the s_memtime-instrumented build (2 ciphertexts per
+  // workgroup); `resid` must then hold 6 * 2 * ceil(num_samples / 2) * NSTAMP u64
+  static const bool stamps = getenv("CONCRETE_HIP_PBS_STAMPS") && atoi(getenv("CONCRETE_HIP_PBS_STAMPS"));
+  if (stamps) return launch_hex_t<2, true, true>(a);
+  if (cts == 1) return a.resid ? launch_hex_t<1, true>(a) : launch_hex_t<1, false>(a);
+  return a.resid ? launch_hex_t<2, true>(a) : launch_hex_t<2, false>(a);
+}
+
+}  // namespace chip

@@ -607,3 +607,58 @@ def test_pbs_quad_tiny_n(B, oracle, torch_cuda, monkeypatch, cts_per_wg, n):
     torch_cuda.cuda.synchronize()
     ref, _ = oracle.pbs_batch(S.op, cts, acc[None, :], fbsk=S.fbsk_cpu)
     assert np.array_equal(B.to_host(out), ref)
+
+
+@pytest.mark.parametrize("cts_per_wg", [1, 2])
+@pytest.mark.parametrize("n,base_log,nb", [(1, 3, 3), (1, 7, 5), (2, 9, 4), (3, 1, 7), (12, 7, 13), (12, 3, 9),
+                                           (12, 9, 6)])
+def test_pbs_hex_kernel(B, oracle, torch_cuda, monkeypatch, cts_per_wg, n, base_log, nb):
+    """The six-wave kernel (pbs1024_hex.hip; CONCRETE_HIP_PBS_HEX forces it with 1 or 2 ciphertexts
+    per workgroup): blind rotations of 0-12 steps (its key prefetch's prologue and the last step's
+    re-read), every logB of the exact range's edges, ragged batches (an odd batch leaves a workgroup's
+    second ciphertext idle), permuted index arrays and per-sample LUTs; bit-exact vs the oracle with
+    the measured rounding residual below the certified bound."""
+    monkeypatch.setenv("CONCRETE_HIP_PBS_HEX", str(cts_per_wg))
+    p = replace(B.CFG2, n=n, level=3, base_log=base_log)
+    S = Setup(B, oracle, torch_cuda, p, 5400 + 10 * n + base_log)
+    width = 2
+    rng = np.random.RandomState(nb * 100 + n)
+    tables = [rng.randint(0, 4, size=4) for _ in range(nb)]
+    msgs = rng.randint(0, 4, size=nb)
+    cts = encrypt(B, S, msgs, width, 61 + n, std=2.0 ** -25)
+    accs = np.stack([lut_acc(B, S, t, width) for t in tables])
+    in_idx = rng.permutation(nb).astype(np.uint64)
+    out_idx = rng.permutation(nb).astype(np.uint64)
+    lut_idx = rng.permutation(nb).astype(np.uint64)
+    dev = "cuda:0"
+    resid = torch_cuda.zeros(1, dtype=torch_cuda.int64, device=dev)
+    out = B.pbs(p, S.fbsk, B.to_device(cts, dev), B.to_device(accs, dev), lut_idx=B.to_device(lut_idx, dev),
+                in_idx=B.to_device(in_idx, dev), out_idx=B.to_device(out_idx, dev), resid=resid)
+    torch_cuda.cuda.synchronize()
+    got = B.to_host(out)
+    ref, _ = oracle.pbs_batch(S.op, cts[in_idx.astype(np.int64)], accs, fbsk=S.fbsk_cpu, lut_idx=lut_idx)
+    exp = np.zeros_like(ref)
+    exp[out_idx.astype(np.int64)] = ref
+    assert np.array_equal(got, exp)
+    if n > 0:
+        r = float(np.array([int(resid.cpu()[0])], dtype=np.int64).view(np.float64)[0])
+        assert r < oracle.fft_error_bound(S.op, S.fbsk_cpu) < 0.5
+
+
+@pytest.mark.parametrize("cts_per_wg", [1, 2])
+def test_pbs_hex_kernel_cfg2_full(B, oracle, cfg2, torch_cuda, monkeypatch, cts_per_wg):
+    """The six-wave kernel on the full cfg2 row (n = 630): 67 ciphertexts bit-exact vs the oracle,
+    every one decrypting to its LUT entry."""
+    monkeypatch.setenv("CONCRETE_HIP_PBS_HEX", str(cts_per_wg))
+    width = 3
+    rng = np.random.RandomState(70 + cts_per_wg)
+    table = rng.randint(0, 8, size=8)
+    msgs = rng.randint(0, 8, size=67)
+    cts = encrypt(B, cfg2, msgs, width, 78 + cts_per_wg)
+    acc = lut_acc(B, cfg2, table, width)
+    got, resid = run_gpu(B, cfg2, cts, acc, torch_cuda, resid=True)
+    ref = run_oracle(oracle, cfg2, cts, acc)
+    assert np.array_equal(got, ref)
+    assert resid < oracle.fft_error_bound(cfg2.op, cfg2.fbsk_cpu) < 0.5
+    dec = B.lwe_decrypt(cfg2.glwe_sk, got, cfg2.p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]

@@ -34,18 +34,29 @@ METRIC = "PBS/sec (whole node) at N=1024 batch=4096; achieved HBM GB/s"
 # the sources a config's PMC record was measured on (a record is used only while they are unchanged)
 KERNEL_HEADERS = ("concrete_amd/csrc/pbs.hpp", "concrete_amd/csrc/fft512.hpp", "concrete_amd/csrc/kernel_util.hpp",
                   "concrete_amd/csrc/common.hpp")
-KERNEL_SOURCES = {"cfg2": ("concrete_amd/csrc/pbs.hip",) + KERNEL_HEADERS,
+KERNEL_SOURCES = {"cfg2": ("concrete_amd/csrc/pbs.hip", "concrete_amd/csrc/pbs1024_hex.hip",
+                           "concrete_amd/csrc/pbs_hex.hpp") + KERNEL_HEADERS,
                   "cfg4": ("concrete_amd/csrc/pbs2048.hip",) + KERNEL_HEADERS,
                   "opt4": ("concrete_amd/csrc/pbs1024k2.hip",) + KERNEL_HEADERS,
                   **{c: ("concrete_amd/csrc/pbs_small.hip",) + KERNEL_HEADERS for c in ("opt1", "opt2", "opt3")}}
 
 
+def _code_only(text: str) -> str:
+    """C/C++ source without comments and whitespace (a comment edit does not change the kernel)."""
+    import re
+    text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
+    text = re.sub(r"//[^\n]*", " ", text)
+    return "".join(text.split())
+
+
 def kernel_source_hash(config: str = "cfg2") -> str:
+    """Hash of the code (comments and whitespace stripped, round 5) of the sources a config's kernel
+    is built from: a committed PMC record is used only while it matches."""
     import hashlib
     h = hashlib.sha1()
     for f in KERNEL_SOURCES.get(config, ("concrete_amd/csrc/pbs_generic.hip",) + KERNEL_HEADERS):
-        with open(os.path.join(ROOT, f), "rb") as fh:
-            h.update(fh.read())
+        with open(os.path.join(ROOT, f), encoding="utf-8") as fh:
+            h.update(_code_only(fh.read()).encode())
     return h.hexdigest()[:16]
 
 

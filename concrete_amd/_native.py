@@ -57,6 +57,8 @@ SIGNATURES = {
     "concrete_hip_device_count": (i32, []),
     "concrete_hip_device_status": (i32, [u32]),
     "concrete_hip_set_spin_limit": (None, [u32]),
+    "concrete_hip_stream_status": (i32, [vp, u32]),
+    "concrete_hip_set_thread_spin_limit": (None, [u32]),
     "concrete_hip_secure_log2_std": (dbl, [u64, u64]),
     "concrete_hip_keygen_binary": (None, [vp, u64, u64]),
     "concrete_hip_lwe_encrypt_batch": (None, [vp, vp, vp, u64, u64, dbl, u64]),

@@ -271,9 +271,22 @@ def device_status(device="cuda:0") -> int:
     return int(_native.lib().concrete_hip_device_status(_gpu_index(device)))
 
 
+def stream_status(device="cuda:0", stream=None) -> int:
+    """Wait for the work issued on `stream` (default: torch's current stream of `device`) and return
+    (and clear) the status of the PBS launches made on it: 0, or -4 when one gave up a wave
+    synchronisation (concrete_hip_stream_status; status words are per stream)."""
+    s = _stream(device) if stream is None else stream.cuda_stream
+    return int(_native.lib().concrete_hip_stream_status(s, _gpu_index(device)))
+
+
 def set_spin_limit(polls: int) -> None:
     """Spin bound of the PBS kernels' wave synchronisation (0 = default); a test hook."""
     _native.lib().concrete_hip_set_spin_limit(int(polls))
+
+
+def set_thread_spin_limit(polls: int) -> None:
+    """The same bound for launches issued by the calling thread only (0 = the process bound)."""
+    _native.lib().concrete_hip_set_thread_spin_limit(int(polls))
 
 
 def keyswitch(p: PbsParams, ksk_dev, lwe_in, out=None, in_idx=None, out_idx=None, num_samples=None):

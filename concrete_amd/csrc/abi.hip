@@ -66,32 +66,66 @@ static std::unordered_map<const void*, KeyEntry> g_keys;
 
 static void set_device(uint32_t gpu) { CHIP_CHECK(hipSetDevice((int)gpu)); }
 
-// Per-device status words (common.hpp SyncGuard): allocated on first use, zeroed, never freed.
+// Status words (common.hpp SyncGuard), one per (device, stream): a launch flags the word of the stream
+// it runs on, so a call reading its own stream's word is told about its own launches only (round 5;
+// the round-4 word was per device, and a spin-bound failure in one call's kernel aborted whichever
+// concurrent call read the word first).  Per device a slab of STATUS_SLOTS words is allocated on first
+// use, zeroed, never freed; slot 0 serves the null stream and any stream past the slab's capacity
+// (shared, as before).  A stream handle keeps its slot for the process's life (a destroyed stream's
+// slot is cleared; a new stream that reuses the handle reuses it).
 constexpr int STATUS_MAX_DEV = 64;
+constexpr uint32_t STATUS_SLOTS = 4096;
+struct DevStatus {
+  uint32_t* slab = nullptr;
+  uint32_t used = 0;
+  std::unordered_map<hipStream_t, uint32_t> slot;
+};
 static std::mutex g_status_mu;
-static uint32_t* g_status[STATUS_MAX_DEV] = {};
+static DevStatus g_status[STATUS_MAX_DEV];
 static std::atomic<uint32_t> g_spin_limit{DEFAULT_SPIN_LIMIT};
+static thread_local uint32_t t_spin_limit = 0;  // per-thread override (test hook), 0 = the global bound
 
-static uint32_t* status_word(int gpu) {
+static void check_gpu_index(int gpu) {
   if (gpu < 0 || gpu >= STATUS_MAX_DEV) {
     fprintf(stderr, "concrete-hip: device index %d out of range\n", gpu);
     abort();
   }
-  std::lock_guard<std::mutex> g(g_status_mu);
-  if (!g_status[gpu]) {
+}
+
+// the status word of (gpu, s), allocating the device's slab on first use (g_status_mu held)
+static uint32_t* status_word_locked(int gpu, hipStream_t s, bool create) {
+  DevStatus& d = g_status[gpu];
+  if (!d.slab) {
+    if (!create) return nullptr;
     int prev = 0;
     CHIP_CHECK(hipGetDevice(&prev));
     CHIP_CHECK(hipSetDevice(gpu));
     void* p = nullptr;
-    CHIP_CHECK(hipMalloc(&p, sizeof(uint32_t)));
-    CHIP_CHECK(hipMemset(p, 0, sizeof(uint32_t)));
+    CHIP_CHECK(hipMalloc(&p, STATUS_SLOTS * sizeof(uint32_t)));
+    CHIP_CHECK(hipMemset(p, 0, STATUS_SLOTS * sizeof(uint32_t)));
     CHIP_CHECK(hipSetDevice(prev));
-    g_status[gpu] = (uint32_t*)p;
+    d.slab = (uint32_t*)p;
+    d.used = 1;  // slot 0: null stream / overflow
   }
-  return g_status[gpu];
+  if (!s) return d.slab;
+  auto it = d.slot.find(s);
+  if (it != d.slot.end()) return d.slab + it->second;
+  if (!create) return nullptr;
+  if (d.used >= STATUS_SLOTS) return d.slab;
+  d.slot.emplace(s, d.used);
+  return d.slab + d.used++;
 }
 
-SyncGuard sync_guard(int gpu) { return SyncGuard{status_word(gpu), g_spin_limit.load(std::memory_order_relaxed)}; }
+SyncGuard sync_guard(int gpu, hipStream_t s) {
+  check_gpu_index(gpu);
+  uint32_t* w;
+  {
+    std::lock_guard<std::mutex> g(g_status_mu);
+    w = status_word_locked(gpu, s, true);
+  }
+  const uint32_t lim = t_spin_limit ? t_spin_limit : g_spin_limit.load(std::memory_order_relaxed);
+  return SyncGuard{w, lim};
+}
 
 void report_hip_state(FILE* f) {
   int n = -1;
@@ -112,42 +146,47 @@ void report_hip_state(FILE* f) {
   abort();
 }
 
+static int status_error(int gpu, uint32_t v, const char* scope) {
+  if (v & DEV_STATUS_SYNC_TIMEOUT) {
+    set_error("device %d: a PBS wave synchronisation exceeded its spin bound on %s; that launch's outputs are wrong",
+              gpu, scope);
+    return -4;
+  }
+  set_error("device %d: status word 0x%x on %s", gpu, v, scope);
+  return -4;
+}
+
+// Device-wide form: synchronises the device and reads (and clears) the words of every stream.
 int take_device_status(int gpu) {
-  uint32_t* w;
+  uint32_t* slab = nullptr;
+  uint32_t used = 0;
   {
     std::lock_guard<std::mutex> g(g_status_mu);
-    w = (gpu >= 0 && gpu < STATUS_MAX_DEV) ? g_status[gpu] : nullptr;
+    if (gpu >= 0 && gpu < STATUS_MAX_DEV) slab = g_status[gpu].slab, used = g_status[gpu].used;
   }
-  if (!w) return 0;  // no PBS kernel has run on this device
+  if (!slab) return 0;  // no PBS kernel has run on this device
   int prev = 0;
   CHIP_CHECK(hipGetDevice(&prev));  // the caller's current device is restored (torch shares it)
   CHIP_CHECK(hipSetDevice(gpu));
   CHIP_CHECK(hipDeviceSynchronize());
-  uint32_t v = 0;
-  CHIP_CHECK(hipMemcpy(&v, w, sizeof v, hipMemcpyDeviceToHost));
-  if (v != 0) CHIP_CHECK(hipMemset(w, 0, sizeof(uint32_t)));
+  std::vector<uint32_t> v(used);
+  CHIP_CHECK(hipMemcpy(v.data(), slab, used * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  uint32_t any = 0;
+  for (uint32_t x : v) any |= x;
+  if (any) CHIP_CHECK(hipMemset(slab, 0, used * sizeof(uint32_t)));
   CHIP_CHECK(hipSetDevice(prev));
-  if (v == 0) return 0;
-  if (v & DEV_STATUS_SYNC_TIMEOUT) {
-    set_error("device %d: a PBS wave synchronisation exceeded its spin bound; that launch's outputs are wrong",
-              gpu);
-    return -4;
-  }
-  set_error("device %d: status word 0x%x", gpu, v);
-  return -4;
+  return any ? status_error(gpu, any, "some stream") : 0;
 }
 
-// Stream-ordered form: the word is read on s after the work issued there (the runtime's slice and
-// shard streams), so concurrent calls on other streams are not waited for.  The word is per device:
-// a flag raised by a launch on another stream is reported by whichever call reads it first (the
-// outputs of that launch are wrong either way; the call that reads it aborts).
+// Stream-ordered form: the word of stream s is read on s after the work issued there (the runtime's
+// slice and shard streams), so concurrent calls on other streams are neither waited for nor blamed.
 int take_stream_status(int gpu, hipStream_t s, uint32_t* h) {
   uint32_t* w;
   {
     std::lock_guard<std::mutex> g(g_status_mu);
-    w = (gpu >= 0 && gpu < STATUS_MAX_DEV) ? g_status[gpu] : nullptr;
+    w = (gpu >= 0 && gpu < STATUS_MAX_DEV) ? status_word_locked(gpu, s, false) : nullptr;
   }
-  if (!w) {  // no PBS kernel has run on this device: only the stream's own work to wait for
+  if (!w) {  // no PBS kernel has run on this stream: only the stream's own work to wait for
     CHIP_CHECK(hipStreamSynchronize(s));
     return 0;
   }
@@ -157,13 +196,17 @@ int take_stream_status(int gpu, hipStream_t s, uint32_t* h) {
   if (v == 0) return 0;
   CHIP_CHECK(hipMemsetAsync(w, 0, sizeof(uint32_t), s));
   CHIP_CHECK(hipStreamSynchronize(s));
-  if (v & DEV_STATUS_SYNC_TIMEOUT) {
-    set_error("device %d: a PBS wave synchronisation exceeded its spin bound; that launch's outputs are wrong",
-              gpu);
-    return -4;
+  return status_error(gpu, v, "this call's stream");
+}
+
+// a destroyed stream's word is cleared (a later stream may reuse the handle)
+static void clear_stream_status(int gpu, hipStream_t s) {
+  uint32_t* w;
+  {
+    std::lock_guard<std::mutex> g(g_status_mu);
+    w = (gpu >= 0 && gpu < STATUS_MAX_DEV && s) ? status_word_locked(gpu, s, false) : nullptr;
   }
-  set_error("device %d: status word 0x%x", gpu, v);
-  return -4;
+  if (w) CHIP_CHECK(hipMemset(w, 0, sizeof(uint32_t)));
 }
 
 // ---- general-format companion keys (pbs_needs_generic_key) ------------------------------
@@ -266,6 +309,8 @@ void* cuda_create_stream(uint32_t gpu_index) {
 
 void cuda_destroy_stream(void* stream, uint32_t gpu_index) {
   set_device(gpu_index);
+  CHIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  clear_stream_status((int)gpu_index, (hipStream_t)stream);
   CHIP_CHECK(hipStreamDestroy((hipStream_t)stream));
 }
 
@@ -344,6 +389,17 @@ void cuda_synchronize_device(uint32_t gpu_index) {
 uint32_t concrete_hip_abi_version(void) { return 3u; }
 const char* concrete_hip_last_error(void) { return last_error(); }
 int concrete_hip_device_status(uint32_t gpu_index) { return take_device_status((int)gpu_index); }
+int concrete_hip_stream_status(void* stream, uint32_t gpu_index) {
+  if (gpu_index >= (uint32_t)STATUS_MAX_DEV) {
+    set_error("stream_status: device index %u out of range", gpu_index);
+    return -3;
+  }
+  set_device(gpu_index);
+  static thread_local uint32_t* landing = nullptr;  // page-locked landing word of this thread
+  if (!landing) CHIP_CHECK(hipHostMalloc((void**)&landing, sizeof(uint32_t), hipHostMallocDefault));
+  return take_stream_status((int)gpu_index, (hipStream_t)stream, landing);
+}
+void concrete_hip_set_thread_spin_limit(uint32_t polls) { t_spin_limit = polls; }
 
 void concrete_hip_set_spin_limit(uint32_t polls) {
   g_spin_limit.store(polls ? polls : DEFAULT_SPIN_LIMIT, std::memory_order_relaxed);
@@ -476,7 +532,7 @@ int concrete_hip_pbs(void* stream, uint32_t gpu_index, uint64_t* lwe_array_out, 
             limbs,
             num_samples,
             (unsigned long long*)resid_bits,
-            sync_guard((int)gpu_index)};
+            sync_guard((int)gpu_index, (hipStream_t)stream)};
   return generic ? pbs_generic_launch(a) : pbs_launch(a);
 }
 
@@ -536,7 +592,7 @@ int concrete_hip_pbs_generic(void* stream, uint32_t gpu_index, uint64_t* lwe_arr
   PbsArgs a{(hipStream_t)stream, lwe_array_out, lwe_output_indexes, lut_vector, lut_vector_indexes, lwe_array_in,
             lwe_input_indexes, generic_bsk, lwe_dimension, glwe_dimension, polynomial_size, base_log, level_count,
             generic_key_format(glwe_dimension, polynomial_size, level_count).limbs, num_samples,
-            (unsigned long long*)resid_bits, sync_guard((int)gpu_index)};
+            (unsigned long long*)resid_bits, sync_guard((int)gpu_index, (hipStream_t)stream)};
   return pbs_generic_launch(a);
 }
 

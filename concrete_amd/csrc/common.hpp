@@ -33,8 +33,8 @@ struct SyncGuard {
   uint32_t* status;     // device word, OR-ed with DEV_STATUS_* bits
   uint32_t spin_limit;  // polls before a sync spin gives up and flags DEV_STATUS_SYNC_TIMEOUT
 };
-SyncGuard sync_guard(int gpu);       // abi.hip: lazily allocated per device
-int take_device_status(int gpu);     // abi.hip: synchronises the device, returns and clears the word
+SyncGuard sync_guard(int gpu, hipStream_t s);  // abi.hip: the word of (gpu, stream), lazily allocated
+int take_device_status(int gpu);     // abi.hip: synchronises the device, returns and clears every word
 
 // Torus helpers -------------------------------------------------------------------------
 __host__ __device__ __forceinline__ uint32_t modswitch(uint64_t x, int log2_2n) {

@@ -159,7 +159,8 @@ inline bool pbs_small_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_l
 // N = 256 .. 16384.  The format depends on (k, N, l) only: the runtime's key conversion call
 // carries no base_log (context.h:106-109).
 // K2N1024: pbs1024k2.hip (k = 2, N = 1024, any l); SMALL: pbs_small.hip (N = 512, k = 3 and
-// N = 256, k = 5 / 6, l <= 3) and pbs512k4.hip (N = 512, k = 4, l = 1, 3 .. 5).  The values are the ABI's format codes
+// N = 256, k = 5 / 6, l <= 3) and pbs512k4.hip (N = 512, k = 4, l = 1 .. 64: l >= K4_MANY_MIN one
+// level at a time).  The values are the ABI's format codes
 // (concrete_hip_bsk_format).
 enum class KeyKind { NONE, N1024, N2048, GENERIC, K2N1024, SMALL };
 struct KeyFormat {
@@ -203,10 +204,13 @@ inline bool pbs_params_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_
 }
 
 // Size in bytes of the device Fourier bootstrapping key.
-//   N1024:   [n][col][limb][row*l + q][512] complex f64
+//   N1024:   [n][limb][co][ro][q][512] complex f64; slots 0..3 of group (limb, co, ro) hold column co /
+//            row ro, slots 4..7 column 1 - co / row 1 - ro (bsk.hip: each wave of a pair reads its
+//            "own" and "other" spectra at fixed positions)
 //   N2048:   [n][limb][col][q][row][+-][512] complex f64 (pbs2048.hip; l <= 4)
 //   GENERIC: [n][col][limb][row][q][N/2] complex f64 (pbs_generic.hip)
-//   K2N1024: [n][limb][col][q][row][512] complex f64 (pbs1024k2.hip; l <= 3; l >= 4: [n][q][limb][col][row][512])
+//   K2N1024: [n][limb][col][q][row][512] complex f64 (pbs1024k2.hip; l < K2_MANY_MIN;
+//            l >= K2_MANY_MIN: [n][q][limb][col][row][512])
 //   SMALL:   [n][limb][cg][q][c2][row][N/2] complex f64, col = cg GC + c2 (pbs_small.hip, pbs512k4.hip;
 //            GC = sm_gc(N, k + 1)); k = 4, N = 512, l >= K4_MANY_MIN: [n][q][limb][col][row][N/2]
 inline uint64_t fourier_bsk_bytes(uint32_t n, uint32_t k, uint32_t level, uint32_t N) {

@@ -28,11 +28,17 @@
 // order of the key layout (bsk.hip: group (limb, co, ro) holds column co / row ro in slots 0..3 and
 // column 1 - co / row 1 - ro in slots 4..7, so wave (c, j) reads slots 0..3 of groups (j, c, r) and
 // slots 4..7 of groups (j, 1 - c, 1 - r)).
+#include <type_traits>
+
 #include "common.hpp"
 #include "fft512.hpp"
 #include "kernel_util.hpp"
 #include "pbs.hpp"
 #include "pbs_hex.hpp"
+
+#ifndef HX_DIAG_NOATOMIC
+#define HX_DIAG_NOATOMIC 0
+#endif
 
 namespace chip {
 
@@ -95,7 +101,6 @@ pbs1024_hex_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_
   const uint32_t s = blockIdx.x * CTS + ctl;
   const bool active = s < num_samples;
   cplx* xch = xch_all + w * XS;
-  const cplx* spec = xch_all + (ctl * 6) * XS;  // spectrum (r, q) at spec + (3 r + q) XS
   uint64_t* accc = acc_all + (ctl * K1 + c) * N;
   uint32_t* myctr = hf + ctl * 8 + u;
   const uint32_t* ctctr = hf + ctl * 8;         // the ciphertext's six counters
@@ -141,20 +146,40 @@ pbs1024_hex_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_
 
   // ---- this wave's key slice: output column c, limb j.  Slots 0..3 of row r: group (j, c, r);
   //      slots 4..7 of row r: group (j, 1 - c, 1 - r) (the pair layout's own/other halves).
-  const cplx* key_lo = fbsk + (uint64_t)(((j * K1 + c) * K1) * GROUP) + lane;            // + r GROUP
-  const cplx* key_hi = fbsk + (uint64_t)(((j * K1 + (1 - c)) * K1 + 1) * GROUP) + lane;  // - r GROUP
-  // batch b = (r, q) = (b / L, b % L): the 8 slots of that row and level
-  auto load_batch = [&](cplx (&g)[8], uint64_t step_off, int b) __attribute__((always_inline)) {
+  // (wave-uniform bases: the loads take the scalar-base + 32-bit lane-offset form)
+  const cplx* key_lo = fbsk + (uint64_t)(((j * K1 + c) * K1) * GROUP);            // + r GROUP
+  const cplx* key_hi = fbsk + (uint64_t)(((j * K1 + (1 - c)) * K1 + 1) * GROUP);  // - r GROUP
+  // Two ciphertexts per workgroup (XM): the key products of output (c, j) are split by frequency
+  // half between the two waves of role u — wave h = ctl computes slots [4h, 4h + 4) for BOTH
+  // ciphertexts — so each key value crosses L2 -> CU once per workgroup; the halves of the other
+  // ciphertext's product are then mailed to its wave (the pair kernel's k2 ^ 4 relabeling lets the
+  // h = 1 wave keep its own half in v[0..3]).  One ciphertext: all eight slots in the wave.
+  constexpr bool XM = CTS == 2;
+  constexpr int KS = XM ? 4 : 8;       // key slots per batch
+  constexpr int PF = XM ? 3 : 2;       // batches in flight
+  constexpr int NB = K1 * L;           // batches (r, q) per step
+  const int h = XM ? ctl : 0;
+  const uint64_t hsign = (uint64_t)h << 63;
+  // batch b = (r, q) = (b / L, b % L): key slots [4h, 4h + KS) of that row and level.  XM: one
+  // wave-uniform base per row (no per-load select): h = 0 reads slots 0..3 of (j, c, r), h = 1 slots
+  // 4..7 of (j, 1 - c, 1 - r)
+  const cplx* krow0 = XM && h ? key_hi + 4 * 64 : key_lo;
+  const cplx* krow1 = XM && h ? key_hi + 4 * 64 - GROUP : key_lo + GROUP;
+  auto load_batch = [&](cplx (&g)[KS], uint64_t step_off, int b) __attribute__((always_inline)) {
     const int r = b / L, q = b % L;
 #pragma unroll
-    for (int k2 = 0; k2 < 4; ++k2) g[k2] = key_lo[step_off + r * GROUP + q * 512 + k2 * 64];
-#pragma unroll
-    for (int k2 = 4; k2 < 8; ++k2) g[k2] = key_hi[step_off - r * GROUP + q * 512 + k2 * 64];
+    for (int k = 0; k < KS; ++k) {
+      const cplx* kb;
+      if (XM) kb = (r ? krow1 : krow0) + (step_off + q * 512 + k * 64);
+      else kb = k < 4 ? key_lo + (step_off + r * GROUP + q * 512 + k * 64)
+                      : key_hi + (step_off - r * GROUP + q * 512 + k * 64);
+      g[k] = kb[lane];
+    }
   };
-  cplx g0[8], g1[8];
+  cplx gb[PF][KS];
   if (n > 0) {
-    load_batch(g0, 0, 0);
-    load_batch(g1, 0, 1);
+#pragma unroll
+    for (int b = 0; b < PF; ++b) load_batch(gb[b], 0, b);
   }
 
   uint64_t a_next = active && n > 0 ? lwe[0] : 0ull;
@@ -191,15 +216,23 @@ pbs1024_hex_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_
     lap(0);  // rotation + state
     // ---- digits of level j (levels below j only carry into it), forward transform, publish
     {
+      // the levels up to mine (the lower ones only carry into it): one uniform branch around whole
+      // loops (a branch per coefficient and level, or every level for every role, cost more)
       int32_t d[16];
+      auto digits = [&](auto JC) __attribute__((always_inline)) {
+        constexpr int JJ = decltype(JC)::value;
 #pragma unroll
-      for (int m = 0; m < 16; ++m) {
-        int32_t dig = 0;
+        for (int m = 0; m < 16; ++m) {
+          int32_t dig = 0;
 #pragma unroll
-        for (int q = 0; q < L; ++q)
-          if (q <= j) dig = decomp_level32(st[m], (uint32_t)(q * logB), logB, half_m1, neg_base, q < j);
-        d[m] = dig;
-      }
+          for (int q = 0; q <= JJ; ++q)
+            dig = decomp_level32(st[m], (uint32_t)(q * logB), logB, half_m1, neg_base, q < JJ);
+          d[m] = dig;
+        }
+      };
+      if (j == 0) digits(std::integral_constant<int, 0>{});
+      else if (j == 1) digits(std::integral_constant<int, 1>{});
+      else digits(std::integral_constant<int, 2>{});
       cplx v[8];
 #pragma unroll
       for (int m = 0; m < 8; ++m) v[m] = {(double)d[m], (double)d[m + 8]};
@@ -209,52 +242,87 @@ pbs1024_hex_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_
       for (int k2 = 0; k2 < 8; ++k2) xch[k2 * 64 + lane] = v[k2];
     }
     lap(1);  // digits + forward + publish
-    hx_signal(myctr, cnt);  // A
-    hx_wait<6>(ctctr, cnt, guard);
+    // A: the spectra of the workgroup are published (XM reads both ciphertexts': a workgroup barrier)
+    if constexpr (XM) {
+      pair_barrier();
+    } else {
+      hx_signal(myctr, cnt);
+      hx_wait<6>(ctctr, cnt, guard);
+    }
     lap(2);  // wait A
 
-    // ---- key product of output c, limb j over the six spectra; the key two batches ahead
-    cplx Y[8];
+    // ---- key product of output c, limb j: XM both ciphertexts at slots [4h, 4h + 4), else mine at
+    //      all eight; the key PF batches ahead
+    constexpr int NT = XM ? 2 : 1;
+    cplx Y[NT][KS];
 #pragma unroll
-    for (int b = 0; b < K1 * L; ++b) {
+    for (int b = 0; b < NB; ++b) {
       const int r = b / L, q = b % L;
-      const cplx* X = spec + (r * L + q) * XS + lane;
-      cplx x[8];
+      cplx x[NT][KS];
 #pragma unroll
-      for (int k2 = 0; k2 < 8; ++k2) x[k2] = X[k2 * 64];
-      cplx (&g)[8] = (b & 1) ? g1 : g0;
+      for (int t = 0; t < NT; ++t) {
+        // t = 0: my ciphertext, t = 1 (XM): the other one
+        const cplx* X = xch_all + ((t == 0 ? ctl : 1 - ctl) * 6 + r * L + q) * XS + (4 * h) * 64 + lane;
 #pragma unroll
-      for (int k2 = 0; k2 < 8; ++k2) {
-        if (b == 0) {  // fma(a, b, 0) == a * b: the same bits as accumulating from zero
-          Y[k2].re = __builtin_fma(x[k2].re, g[k2].re, -x[k2].im * g[k2].im);
-          Y[k2].im = __builtin_fma(x[k2].re, g[k2].im, x[k2].im * g[k2].re);
-        } else {
-          Y[k2].re = __builtin_fma(x[k2].re, g[k2].re, __builtin_fma(-x[k2].im, g[k2].im, Y[k2].re));
-          Y[k2].im = __builtin_fma(x[k2].re, g[k2].im, __builtin_fma(x[k2].im, g[k2].re, Y[k2].im));
-        }
+        for (int k = 0; k < KS; ++k) x[t][k] = X[k * 64];
       }
-      if (b == K1 * L - 1) hx_signal(myctr, cnt);  // B: every spectrum read of this wave is issued
-      // refill: batch b + 2 of this step, or batch b + 2 - 6 of the next
-      if (b + 2 < K1 * L) load_batch(g, step_off, b + 2);
-      else load_batch(g, next_off, b + 2 - K1 * L);
+      cplx (&g)[KS] = gb[b % PF];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+          const cplx xv = x[t][k], gv = g[k];
+          if (b == 0) {  // fma(a, b, 0) == a * b: the same bits as accumulating from zero
+            Y[t][k].re = __builtin_fma(xv.re, gv.re, -xv.im * gv.im);
+            Y[t][k].im = __builtin_fma(xv.re, gv.im, xv.im * gv.re);
+          } else {
+            Y[t][k].re = __builtin_fma(xv.re, gv.re, __builtin_fma(-xv.im, gv.im, Y[t][k].re));
+            Y[t][k].im = __builtin_fma(xv.re, gv.im, __builtin_fma(xv.im, gv.re, Y[t][k].im));
+          }
+        }
+      if (!XM && b == NB - 1) hx_signal(myctr, cnt);  // B: every spectrum read of this wave is issued
+      // refill: batch b + PF of this step, or of the next
+      if (b + PF < NB) load_batch(g, step_off, b + PF);
+      else load_batch(g, next_off, b + PF - NB);
     }
 #pragma unroll
-    for (int k2 = 0; k2 < 8; ++k2) pin(Y[k2]);
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int k = 0; k < KS; ++k) pin(Y[t][k]);
     lap(3);  // key products
 
-    // ---- inverse transform of (c, j): my scratch is rewritten only after every wave of the
-    //      ciphertext has read the spectra (B)
-    hx_wait<6>(ctctr, cnt, guard);
-    lap(4);  // wait B
-    fft512_inv(Y, xch, T, lane, 0ull);
+    // ---- inverse transform of (c, j): my scratch is rewritten only after every reader of the
+    //      spectra is done (B)
+    cplx v[8];
+    if constexpr (XM) {
+      pair_barrier();  // B
+      // the other ciphertext's half straight into its wave's scratch, then signal it
+      // (Y[0] is my ciphertext's, Y[1] the other's: compile-time indexes, registers only)
+      cplx* partner = xch_all + ((1 - ctl) * 6 + u) * XS + lane;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        partner[k * 64] = Y[1][k];
+        v[k] = Y[0][k];  // my half: natural slots 4h + k (k2 ^ 4 order for h = 1)
+      }
+      hx_signal(myctr, cnt);  // M
+      hx_wait<1>(hf + (1 - ctl) * 8 + u, cnt, guard);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[4 + k] = xch[k * 64 + lane];  // the partner's: slots 4 (1 - h) + k
+    } else {
+      hx_wait<6>(ctctr, cnt, guard);  // B
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = Y[0][k];
+    }
+    lap(4);  // wait B (+ mailbox)
+    fft512_inv(v, xch, T, lane, hsign);
     {
       // limb j's exact integers, negated (B = -acc), shifted; limb 0 removes the constant of all limbs
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
-        const double tr = RND_MAGIC - Y[m].re, ti = RND_MAGIC - Y[m].im;
+        const double tr = RND_MAGIC - v[m].re, ti = RND_MAGIC - v[m].im;
         if constexpr (RESID) {
-          max_resid = fmax(max_resid, fabs(Y[m].re - (RND_MAGIC - tr)));
-          max_resid = fmax(max_resid, fabs(Y[m].im - (RND_MAGIC - ti)));
+          max_resid = fmax(max_resid, fabs(v[m].re - (RND_MAGIC - tr)));
+          max_resid = fmax(max_resid, fabs(v[m].im - (RND_MAGIC - ti)));
         }
         uint64_t cre, cim;
         if (j == 0) {
@@ -265,13 +333,23 @@ pbs1024_hex_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_
           cre = (uint64_t)__double_as_longlong(tr) << sh;
           cim = (uint64_t)__double_as_longlong(ti) << sh;
         }
+#if HX_DIAG_NOATOMIC  // timing-only builds: plain stores (wrong results)
+        if (j == 0) accc[lane + 64 * m] = cre, accc[lane + 64 * (m + 8)] = cim;
+#else
         __hip_atomic_fetch_add(&accc[lane + 64 * m], cre, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add(&accc[lane + 64 * (m + 8)], cim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
       }
     }
     lap(5);  // inverse + rounding + atomic adds
-    hx_signal(myctr, cnt);  // C
-    hx_wait<3>(polyctr, cnt, guard);
+    // C: the limbs of polynomial c are in.  XM: a workgroup barrier (every wave runs the same phases
+    // between the A and B barriers anyway; spinning waves would take VALU issue slots)
+    if constexpr (XM) {
+      pair_barrier();
+    } else {
+      hx_signal(myctr, cnt);
+      hx_wait<3>(polyctr, cnt, guard);
+    }
     lap(7);  // wait C
   }
   if constexpr (STAMPS) {

@@ -196,13 +196,21 @@ int concrete_hip_build_accumulators(void *stream, uint32_t gpu_index, uint64_t *
                                     uint64_t num_luts, uint32_t glwe_dim, uint32_t polynomial_size);
 /* number of visible devices */
 int concrete_hip_device_count(void);
-/* Synchronise the device and return (and clear) its sticky status: 0 ok, -4 when a PBS kernel's
- * wave synchronisation gave up after its spin bound since the last check (that launch's outputs
- * are wrong).  cuda_synchronize_device performs the same check and aborts. */
+/* Synchronise the device and return (and clear) the sticky status of every stream on it: 0 ok, -4
+ * when a PBS kernel's wave synchronisation gave up after its spin bound since the last check (that
+ * launch's outputs are wrong).  cuda_synchronize_device performs the same check and aborts. */
 int concrete_hip_device_status(uint32_t gpu_index);
+/* Stream-ordered status of one stream (round 5): waits for the work issued on `stream` (nothing
+ * else), then returns (and clears) the status of the PBS launches made on that stream since its last
+ * check: 0 ok, -4 when one of them gave up a wave synchronisation (its outputs are wrong).  Status
+ * words are per (device, stream), so concurrent calls on other streams are never blamed. */
+int concrete_hip_stream_status(void *stream, uint32_t gpu_index);
 /* Spin bound (LDS-counter polls) of the PBS kernels' wave synchronisation for later launches;
  * 0 restores the default (2^22).  Test hook: a tiny bound forces the timeout path. */
 void concrete_hip_set_spin_limit(uint32_t polls);
+/* The same bound for launches issued by the calling host thread only (0: the process-wide bound).
+ * Test hook: forces the timeout path on one of several concurrent calls. */
+void concrete_hip_set_thread_spin_limit(uint32_t polls);
 
 /* ------------------------------------------------------------------------------------------
  * Part 3: client-side helpers (host code; synthetic workloads and LUT encoding).

@@ -662,3 +662,50 @@ def test_pbs_hex_kernel_cfg2_full(B, oracle, cfg2, torch_cuda, monkeypatch, cts_
     assert resid < oracle.fft_error_bound(cfg2.op, cfg2.fbsk_cpu) < 0.5
     dec = B.lwe_decrypt(cfg2.glwe_sk, got, cfg2.p.big_n)
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+
+
+def test_status_is_per_stream(B, oracle, cfg2, torch_cuda):
+    """the sync-timeout status is attributed to the launch's own stream.  Two
+    threads run the cfg2 PBS concurrently on two streams; one forces the spin bound to one poll for
+    its own launch only (concrete_hip_set_thread_spin_limit).  That thread's stream reports -4, the
+    other's reports 0 and its outputs are bit-exact (sampled rows vs the oracle, every row decrypts);
+    the device-wide check afterwards is clean (both words were cleared by the stream reads)."""
+    import threading
+    torch = torch_cuda
+    width = 3
+    rng = np.random.RandomState(41)
+    table = rng.randint(0, 8, size=8)
+    msgs = rng.randint(0, 8, size=(2, 512))
+    cts = [encrypt(B, cfg2, msgs[i], width, 4141 + i) for i in range(2)]
+    acc = lut_acc(B, cfg2, table, width)
+    dev = "cuda:0"
+    assert B.device_status(dev) == 0
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    d_in = [B.to_device(c, dev) for c in cts]
+    d_acc = B.to_device(acc[None, :], dev)
+    outs = [torch.zeros((512, cfg2.p.lwe_out_size), dtype=torch.int64, device=dev) for _ in range(2)]
+    torch.cuda.synchronize()
+    status = [None, None]
+    gate = threading.Barrier(2)
+
+    def call(i):
+        try:
+            if i == 0:
+                B.set_thread_spin_limit(1)
+            with torch.cuda.stream(streams[i]):
+                gate.wait()
+                B.pbs(cfg2.p, cfg2.fbsk, d_in[i], d_acc, out=outs[i])
+                status[i] = B.stream_status(dev, streams[i])
+        finally:
+            B.set_thread_spin_limit(0)
+
+    th = [threading.Thread(target=call, args=(i,)) for i in range(2)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert status == [-4, 0], status
+    assert B.device_status(dev) == 0
+    got = B.to_host(outs[1])
+    rows = np.array([0, 255, 511])
+    assert np.array_equal(got[rows], run_oracle(oracle, cfg2, cts[1][rows], acc))
+    dec = B.lwe_decrypt(cfg2.glwe_sk, got, cfg2.p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs[1]]

@@ -36,6 +36,9 @@
 #include "pbs.hpp"
 #include "pbs_hex.hpp"
 
+#ifndef HX_SHARED_DIGITS
+#define HX_SHARED_DIGITS 1  // rotation + decomposition shared by the three waves of a polynomial (XM)
+#endif
 #ifndef HX_DIAG_NOATOMIC
 #define HX_DIAG_NOATOMIC 0
 #endif
@@ -192,33 +195,78 @@ pbs1024_hex_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_
 
     // ---- ct1 = acc X^at - acc = B - X^at B of polynomial c (pbs1024_pair_kernel's offsets: bit 13
     //      of o says "src < N", i.e. no wrap, where the rotated term is subtracted), decomposer state
-    uint32_t st[16];
-    {
-      const uint32_t o0 = ((uint32_t)(lane - (int)at) << 3) + 8u * N;
-      const char* accb = reinterpret_cast<const char*>(accc);
-      uint64_t rv[16], bv[16];
+    const uint32_t o0 = ((uint32_t)(lane - (int)at) << 3) + 8u * N;
+    const char* accb = reinterpret_cast<const char*>(accc);
+    auto state_of = [&](uint64_t rv, uint64_t bv, int m) __attribute__((always_inline)) {
+      const uint32_t o = o0 + 512u * m;
+      const uint32_t s32 = (uint32_t)((int32_t)(o << 18) >> 31);
+      const uint64_t rvs = rv ^ (((uint64_t)s32 << 32) | s32);
+      const uint64_t x = bv + rvs + (uint64_t)(s32 & 1u);
+      return ((uint32_t)(x >> 32) + khi) >> (nrep - 32);
+    };
+    auto rot_read = [&](int m) __attribute__((always_inline)) {
+      return *reinterpret_cast<const uint64_t*>(accb + ((o0 + 512u * m) & 8191u));
+    };
+    int32_t d[16];
+    if constexpr (XM && HX_SHARED_DIGITS) {
+      // Shared: wave (c, j) rotates and decomposes (every level) only the coefficient pairs
+      // (m, m + 8) with m in [MB, ME) of its role — 3 / 3 / 2 of the 8 — and stores level q's digits
+      // (two int16 per u32) in the scratch of wave (c, q); after barrier D each wave reads its level's
+      // 16 digits from its own scratch.  (Every scratch is idle between the C and D barriers.)
+      auto produce = [&](auto JC) __attribute__((always_inline)) {
+        constexpr int JJ = decltype(JC)::value;
+        constexpr int MB = JJ == 0 ? 0 : JJ == 1 ? 3 : 6, ME = JJ == 0 ? 3 : JJ == 1 ? 6 : 8, NM = ME - MB;
+        uint64_t rv[2][NM], bv[2][NM];
 #pragma unroll
-      for (int m = 0; m < 16; ++m) {
-        rv[m] = *reinterpret_cast<const uint64_t*>(accb + ((o0 + 512u * m) & 8191u));
-        bv[m] = accc[lane + 64 * m];
-      }
-      __builtin_amdgcn_sched_barrier(0);
+        for (int t = 0; t < NM; ++t)
 #pragma unroll
-      for (int m = 0; m < 16; ++m) {
-        const uint32_t o = o0 + 512u * m;
-        const uint32_t s32 = (uint32_t)((int32_t)(o << 18) >> 31);
-        const uint64_t rvs = rv[m] ^ (((uint64_t)s32 << 32) | s32);
-        const uint64_t x = bv[m] + rvs + (uint64_t)(s32 & 1u);
-        st[m] = ((uint32_t)(x >> 32) + khi) >> (nrep - 32);
+          for (int hh = 0; hh < 2; ++hh) {
+            const int m = MB + t + 8 * hh;
+            rv[hh][t] = rot_read(m);
+            bv[hh][t] = accc[lane + 64 * m];
+          }
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(xch_all + (ctl * 6 + 3 * c) * XS) + lane;
+#pragma unroll
+        for (int t = 0; t < NM; ++t) {
+          const int m = MB + t;
+          uint32_t s0 = state_of(rv[0][t], bv[0][t], m), s1 = state_of(rv[1][t], bv[1][t], m + 8);
+#pragma unroll
+          for (int q = 0; q < L; ++q) {
+            const int32_t d0 = decomp_level32(s0, (uint32_t)(q * logB), logB, half_m1, neg_base, q + 1 < L);
+            const int32_t d1 = decomp_level32(s1, (uint32_t)(q * logB), logB, half_m1, neg_base, q + 1 < L);
+            dst[q * XS * 4 + m * 64] = ((uint32_t)d0 & 0xffffu) | ((uint32_t)d1 << 16);
+          }
+        }
+      };
+      if (j == 0) produce(std::integral_constant<int, 0>{});
+      else if (j == 1) produce(std::integral_constant<int, 1>{});
+      else produce(std::integral_constant<int, 2>{});
+      lap(0);  // rotation + shared digits
+      pair_barrier();  // D
+      const uint32_t* mine = reinterpret_cast<const uint32_t*>(xch) + lane;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const uint32_t pk = mine[m * 64];
+        d[m] = (int32_t)__builtin_amdgcn_sbfe(pk, 0u, 16u);
+        d[m + 8] = (int32_t)pk >> 16;
       }
-    }
-
-    lap(0);  // rotation + state
-    // ---- digits of level j (levels below j only carry into it), forward transform, publish
-    {
+    } else {
+      uint32_t st[16];
+      {
+        uint64_t rv[16], bv[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+          rv[m] = rot_read(m);
+          bv[m] = accc[lane + 64 * m];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) st[m] = state_of(rv[m], bv[m], m);
+      }
+      lap(0);  // rotation + state
       // the levels up to mine (the lower ones only carry into it): one uniform branch around whole
       // loops (a branch per coefficient and level, or every level for every role, cost more)
-      int32_t d[16];
       auto digits = [&](auto JC) __attribute__((always_inline)) {
         constexpr int JJ = decltype(JC)::value;
 #pragma unroll
@@ -233,6 +281,9 @@ pbs1024_hex_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_
       if (j == 0) digits(std::integral_constant<int, 0>{});
       else if (j == 1) digits(std::integral_constant<int, 1>{});
       else digits(std::integral_constant<int, 2>{});
+    }
+    // ---- forward transform of my level's digit polynomial, spectrum published in my scratch
+    {
       cplx v[8];
 #pragma unroll
       for (int m = 0; m < 8; ++m) v[m] = {(double)d[m], (double)d[m + 8]};
@@ -316,6 +367,8 @@ pbs1024_hex_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_
     lap(4);  // wait B (+ mailbox)
     fft512_inv(v, xch, T, lane, hsign);
     {
+      const int lsh = j == 0 ? 0 : j == 1 ? hx_limb_shift(1) : hx_limb_shift(2);
+      const uint64_t lsub = j == 0 ? HX_MAGIC_ALL : 0ull;
       // limb j's exact integers, negated (B = -acc), shifted; limb 0 removes the constant of all limbs
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
@@ -324,15 +377,9 @@ pbs1024_hex_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_
           max_resid = fmax(max_resid, fabs(v[m].re - (RND_MAGIC - tr)));
           max_resid = fmax(max_resid, fabs(v[m].im - (RND_MAGIC - ti)));
         }
-        uint64_t cre, cim;
-        if (j == 0) {
-          cre = (uint64_t)__double_as_longlong(tr) - HX_MAGIC_ALL;
-          cim = (uint64_t)__double_as_longlong(ti) - HX_MAGIC_ALL;
-        } else {
-          const int sh = j == 1 ? hx_limb_shift(1) : hx_limb_shift(2);
-          cre = (uint64_t)__double_as_longlong(tr) << sh;
-          cim = (uint64_t)__double_as_longlong(ti) << sh;
-        }
+        // (branch-free: wave-uniform shift and constant)
+        const uint64_t cre = ((uint64_t)__double_as_longlong(tr) << lsh) - lsub;
+        const uint64_t cim = ((uint64_t)__double_as_longlong(ti) << lsh) - lsub;
 #if HX_DIAG_NOATOMIC  // timing-only builds: plain stores (wrong results)
         if (j == 0) accc[lane + 64 * m] = cre, accc[lane + 64 * (m + 8)] = cim;
 #else

@@ -39,6 +39,12 @@
 #ifndef HX_SHARED_DIGITS
 #define HX_SHARED_DIGITS 1  // rotation + decomposition shared by the three waves of a polynomial (XM)
 #endif
+#ifndef HX_DIAG_NOKEY
+#define HX_DIAG_NOKEY 0  // timing-only builds: no key loads (the key values are the spectra's)
+#endif
+#ifndef HX_DIAG_NOX
+#define HX_DIAG_NOX 0  // timing-only builds: no spectrum reads in the key products
+#endif
 #ifndef HX_DIAG_NOATOMIC
 #define HX_DIAG_NOATOMIC 0
 #endif
@@ -176,7 +182,11 @@ pbs1024_hex_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_
       if (XM) kb = (r ? krow1 : krow0) + (step_off + q * 512 + k * 64);
       else kb = k < 4 ? key_lo + (step_off + r * GROUP + q * 512 + k * 64)
                       : key_hi + (step_off - r * GROUP + q * 512 + k * 64);
+#if HX_DIAG_NOKEY
+      g[k] = {(double)(k + 1), (double)(size_t)kb};
+#else
       g[k] = kb[lane];
+#endif
     }
   };
   cplx gb[PF][KS];
@@ -315,7 +325,13 @@ pbs1024_hex_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_
         // t = 0: my ciphertext, t = 1 (XM): the other one
         const cplx* X = xch_all + ((t == 0 ? ctl : 1 - ctl) * 6 + r * L + q) * XS + (4 * h) * 64 + lane;
 #pragma unroll
-        for (int k = 0; k < KS; ++k) x[t][k] = X[k * 64];
+        for (int k = 0; k < KS; ++k) {
+#if HX_DIAG_NOX
+          x[t][k] = {(double)(b + k), (double)(t + lane)};
+#else
+          x[t][k] = X[k * 64];
+#endif
+        }
       }
       cplx (&g)[KS] = gb[b % PF];
 #pragma unroll
@@ -332,9 +348,10 @@ pbs1024_hex_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_
           }
         }
       if (!XM && b == NB - 1) hx_signal(myctr, cnt);  // B: every spectrum read of this wave is issued
-      // refill: batch b + PF of this step, or of the next
+      // refill: batch b + PF of this step (the next step's first PF batches are issued in the
+      // inverse phase: issued here, all of a step's key loads crowded into this phase, where the
+      // CU's vector-memory path — 288 KB per step — bounded it: +5.8 % without key loads, diagnostic)
       if (b + PF < NB) load_batch(g, step_off, b + PF);
-      else load_batch(g, next_off, b + PF - NB);
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -365,6 +382,10 @@ pbs1024_hex_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_
       for (int k = 0; k < 8; ++k) v[k] = Y[0][k];
     }
     lap(4);  // wait B (+ mailbox)
+    // the next step's first key batches, in flight during the inverse and the next rotation and
+    // forward transform
+#pragma unroll
+    for (int b = 0; b < PF; ++b) load_batch(gb[b], next_off, b);
     fft512_inv(v, xch, T, lane, hsign);
     {
       const int lsh = j == 0 ? 0 : j == 1 ? hx_limb_shift(1) : hx_limb_shift(2);

@@ -511,17 +511,36 @@ void ora_external_product_acc(uint64_t *acc, const uint64_t *ggsw_std, const dou
             for (size_t q = 0; q < l; q++) digits[(row * l + q) * N + j] = tmp[q];
         }
     if (mode == ORA_MODE_SCHOOLBOOK || mode == ORA_MODE_KARATSUBA) {
-        for (size_t row = 0; row < K1; row++)
-            for (size_t q = 0; q < l; q++) {
-                size_t v = l - 1 - q; /* GGSW level matrix index of decomposition level l - q */
-                for (size_t col = 0; col < K1; col++) {
-                    const uint64_t *g = ggsw_std + ((v * K1 + row) * K1 + col) * N;
-                    if (mode == ORA_MODE_SCHOOLBOOK)
-                        ora_polymul_acc_schoolbook(acc + col * N, digits + (row * l + q) * N, g, N);
-                    else
-                        ora_polymul_acc_karatsuba(acc + col * N, digits + (row * l + q) * N, g, N);
-                }
+        /* the K1 l K1 products (row, level, col) are independent: outside a parallel region (one
+         * large-N ciphertext, ora_pbs_batch) they run on the OpenMP threads into private buffers, summed
+         * per column afterwards in a fixed order (integer adds mod 2^64: the same bits either way) */
+        size_t T = K1 * l * K1;
+        int inner = 0;
+#ifdef _OPENMP
+        inner = !omp_in_parallel() && omp_get_max_threads() > 1 && T > 1 && N >= 2048;
+#endif
+        uint64_t *part = inner ? (uint64_t *)calloc(T * N, sizeof(uint64_t)) : NULL;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) if (inner)
+#endif
+        for (long t = 0; t < (long)T; t++) {
+            size_t row = (size_t)t / (l * K1), q = ((size_t)t / K1) % l, col = (size_t)t % K1;
+            size_t v = l - 1 - q; /* GGSW level matrix index of decomposition level l - q */
+            const uint64_t *g = ggsw_std + ((v * K1 + row) * K1 + col) * N;
+            uint64_t *dst = inner ? part + (size_t)t * N : acc + col * N;
+            if (mode == ORA_MODE_SCHOOLBOOK)
+                ora_polymul_acc_schoolbook(dst, digits + (row * l + q) * N, g, N);
+            else
+                ora_polymul_acc_karatsuba(dst, digits + (row * l + q) * N, g, N);
+        }
+        if (inner) {
+            for (size_t t = 0; t < T; t++) {
+                uint64_t *dst = acc + (t % K1) * N;
+                const uint64_t *src = part + t * N;
+                for (size_t j = 0; j < N; j++) dst[j] += src[j];
             }
+            free(part);
+        }
         free(digits);
         return;
     }
@@ -629,9 +648,12 @@ void ora_pbs_batch(uint64_t *out, const uint64_t *out_idx, const uint64_t *luts,
                    size_t n, size_t k, size_t N, size_t l, size_t logB, size_t L, size_t num_samples, int mode,
                    int nthreads, double *max_resid) {
     double resid = 0.0;
+    int outer = 1;
 #ifdef _OPENMP
     if (nthreads <= 0) nthreads = omp_get_max_threads();
-#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) reduction(max : resid)
+    /* few large ciphertexts: one at a time, each external product's products in parallel instead */
+    outer = (long)num_samples * 4 > (long)nthreads || N < 2048;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) reduction(max : resid) if (outer)
 #endif
     for (long s = 0; s < (long)num_samples; s++) {
         size_t oi = out_idx ? (size_t)out_idx[s] : (size_t)s;

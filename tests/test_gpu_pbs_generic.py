@@ -317,7 +317,8 @@ def test_configs4_atomic_pattern_8bit(B, oracle, torch_cuda):
     bits = 8
     lwe_sk = B.binary_key(p.n, 7800)
     glwe_sk = B.binary_key(p.big_n, 7801)
-    fbsk = B.convert_bsk(p, B.bsk_generate(p, lwe_sk, glwe_sk, 7802), "cuda:0")
+    bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 7802)
+    fbsk = B.convert_bsk(p, bsk, "cuda:0")
     ksk = B.ksk_generate(p, glwe_sk, lwe_sk, 7803)
     pts, lut_idx, expect, tables, signs = [], [], [], [], []
     for ci, c in enumerate(cases):
@@ -356,6 +357,40 @@ def test_configs4_atomic_pattern_8bit(B, oracle, torch_cuda):
     assert np.array_equal(B.to_host(d_lut), host_luts)
     dec = B.lwe_decrypt(glwe_sk, B.to_host(out), p.big_n)
     assert [B.decode(d, bits, sg) for d, (_, sg) in zip(dec, expect)] == [e for e, _ in expect]
+    # a full-size row bit-exact in the driver-run suite — the oracle's pure-integer
+    # Karatsuba product over all n = 1006 CMUX steps (its eight products per step on the OpenMP
+    # threads), on the keyswitched input and the device-encoded accumulator of that row
+    row = len(pts) // 2
+    ref, _ = oracle.pbs_batch(op, B.to_host(d_small)[row:row + 1], B.to_host(d_acc)[lut_idx[row]][None, :], bsk=bsk,
+                              mode=oracle.MODE_KARATSUBA)
+    assert np.array_equal(B.to_host(out)[row:row + 1], ref)
+
+
+# the large-N paths at many CMUX steps and many ciphertexts, bit-exact vs the
+# oracle's Karatsuba product (the table rows' k, N, l, logB; n cut to what the oracle finishes in
+# seconds): N = 4096 (the one-launch kernel), N = 8192 (the two-launch path, chunked over streams),
+# N = 2^15 (a polynomial spread over two workgroups).  (label, k, N, n, l, logB, bits, batch)
+LARGE_N_CASES = [
+    ("6bit_k1_N4096_n64", 1, 4096, 64, 1, 22, 6, 67),
+    ("7bit_k1_N8192_n64", 1, 8192, 64, 1, 22, 7, 67),
+    ("8bit_k1_N16384_n24", 1, 16384, 24, 2, 15, 8, 9),
+    ("9bit_k1_N32768_n16", 1, 32768, 16, 2, 15, 9, 6),
+]
+
+
+@pytest.mark.parametrize("case", LARGE_N_CASES, ids=[c[0] for c in LARGE_N_CASES])
+def test_large_n_many_steps_bit_exact(B, oracle, torch_cuda, case):
+    label, k, N, n, l, logB, width, batch = case
+    p, glwe_sk, bsk, fbsk, cts, acc, table, msgs, got, resid = run_case(
+        B, oracle, torch_cuda, (label, k, N, n, l, logB, width), 7900 + n, batch=batch)
+    op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
+    ref, _ = oracle.pbs_batch(op, cts, acc[None, :], bsk=bsk, mode=oracle.MODE_KARATSUBA)
+    assert np.array_equal(got, ref), f"{label}: GPU differs from the exact oracle"
+    kind, limbs, bits = B.bsk_format(p)
+    bound = oracle.generic_error_bound(p.k, p.N, p.level, p.base_log, bits, B.to_host(fbsk).view(np.float64))
+    assert resid < bound < 0.5, (resid, bound)
+    dec = B.lwe_decrypt(glwe_sk, got, p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
 
 
 # v0_last_128 rows at non-zero log norm2 (tests/golden/v0_last_128_rows.json): per width the row

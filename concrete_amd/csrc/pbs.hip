@@ -581,12 +581,23 @@ static int launch_pair(const PbsArgs& a) {
   // (at 2 per CU, B = 512, it measured 0.9x the pair kernel: DESIGN.md §4.1).  CONCRETE_HIP_PBS_QUAD=0
   // keeps the pair kernel, =1 / =2 forces it with that many ciphertexts per workgroup (read per
   // call: tests, A/B).
-  // six waves per ciphertext (pbs1024_hex.hip): CONCRETE_HIP_PBS_HEX=1 / =2 forces it with that many
-  // ciphertexts per workgroup (read per call: tests, A/B)
+  // Six waves per ciphertext (pbs1024_hex.hip, round 5), two ciphertexts per CU: a round of 2 x CUs
+  // ciphertexts takes ~5.41 ms against ~10.2 ms for the pair kernel's round of 4 x CUs (cfg2, one
+  // MI355X, profiles/r05/ab5_sweep.json), so it wins whenever it needs fewer than 1.886x the pair
+  // kernel's rounds — every batch of <= 2 x CUs (the metric's 512 per GPU on 8 GPUs: 92k vs 70k
+  // PBS/s), 1536, 2560 ... — and one ciphertext per workgroup at <= CUs (52.5k vs 40.6k at 256).
+  // CONCRETE_HIP_PBS_HEX=1 / =2 forces it with that many ciphertexts per workgroup, =0 keeps it off;
+  // a forced CONCRETE_HIP_PBS_PAIRS / _QUAD selects those kernels (read per call: tests, A/B).
   if (L == 3) {
     const char* he = getenv("CONCRETE_HIP_PBS_HEX");
-    const int hx = he ? atoi(he) : 0;
+    const int hx = he ? atoi(he) : -1;
     if (hx == 1 || hx == 2) return pbs1024_hex_launch(a, hx);
+    if (hx != 0 && !fe && !getenv("CONCRETE_HIP_PBS_QUAD") && !getenv("CONCRETE_HIP_PBS_STAMPS")) {
+      if (a.num_samples <= cus) return pbs1024_hex_launch(a, 1);
+      const uint64_t r_hex = (a.num_samples + 2ull * cus - 1) / (2ull * cus);
+      const uint64_t r_pair = (a.num_samples + 4ull * cus - 1) / (4ull * cus);
+      if (r_hex * 541 < r_pair * 1020) return pbs1024_hex_launch(a, 2);
+    }
   }
   if (L == 3 && P <= 2 && !getenv("CONCRETE_HIP_PBS_STAMPS")) {
     const char* qe = getenv("CONCRETE_HIP_PBS_QUAD");

@@ -39,6 +39,9 @@
 #ifndef HX_SHARED_DIGITS
 #define HX_SHARED_DIGITS 1  // rotation + decomposition shared by the three waves of a polynomial (XM)
 #endif
+#ifndef HX_PRIO
+#define HX_PRIO 0  // A/B: static wave priorities (1: the youngest third of the waves at 1; 2: w / 4)
+#endif
 #ifndef HX_DIAG_NOKEY
 #define HX_DIAG_NOKEY 0  // timing-only builds: no key loads (the key values are the spectra's)
 #endif
@@ -195,6 +198,12 @@ pbs1024_hex_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_
     for (int b = 0; b < PF; ++b) load_batch(gb[b], 0, b);
   }
 
+  if constexpr (HX_PRIO == 1) {
+    if (w >= 8) __builtin_amdgcn_s_setprio(1);
+  } else if constexpr (HX_PRIO == 2) {
+    if (w >= 8) __builtin_amdgcn_s_setprio(2);
+    else if (w >= 4) __builtin_amdgcn_s_setprio(1);
+  }
   uint64_t a_next = active && n > 0 ? lwe[0] : 0ull;
   for (uint32_t i = 0; i < n; ++i) {
     const uint64_t step_off = (uint64_t)i * PER_I;

@@ -386,7 +386,7 @@ void cuda_synchronize_device(uint32_t gpu_index) {
 // ----------------------------------------------------------------------------------------
 // extensions
 // ----------------------------------------------------------------------------------------
-uint32_t concrete_hip_abi_version(void) { return 3u; }
+uint32_t concrete_hip_abi_version(void) { return 4u; }
 const char* concrete_hip_last_error(void) { return last_error(); }
 int concrete_hip_device_status(uint32_t gpu_index) { return take_device_status((int)gpu_index); }
 int concrete_hip_stream_status(void* stream, uint32_t gpu_index) {

@@ -108,7 +108,9 @@ void cuda_negate_lwe_ciphertext_vector_64(void *stream, uint32_t gpu_index, void
  * ------------------------------------------------------------------------------------------ */
 
 /* ABI version of this header (2: round 3 — context-resolved memref_*_cuda_u64, stream emulator;
- * 3: round 4 — keyswitch support query, key level-order check against client keys). */
+ * 3: round 4 — keyswitch support query, key level-order check against client keys;
+ * 4: round 5 — status words per (device, stream): concrete_hip_stream_status,
+ *    concrete_hip_set_thread_spin_limit). */
 uint32_t concrete_hip_abi_version(void);
 /* thread-local message of the last failed concrete_hip_* call */
 const char *concrete_hip_last_error(void);

@@ -195,7 +195,9 @@ def main():
         p = B.CFG2 if args.config == "cfg2" else B.CFG4
         width = 3 if args.config == "cfg2" else 5
     if not args.cpu_sample:
-        args.cpu_sample = {"cfg2": 4096, "cfg4": 1024}.get(args.config, 32 if p.N <= 1024 else 16 if p.N <= 4096 else 2)
+        # about 10-30 s of CPU work on 16 host cores (fft64 restatement, OpenMP over ciphertexts)
+        args.cpu_sample = {"cfg2": 4096, "cfg4": 1024}.get(
+            args.config, 512 if p.N <= 1024 else 128 if p.N <= 4096 else 32 if p.N <= 16384 else 4)
     # ---- keys: deterministic synthetic keyset (product keygen); device key on rank 0 -> RCCL bcast
     lwe_sk = B.binary_key(p.n, 1)
     glwe_sk = B.binary_key(p.big_n, 2)
@@ -523,14 +525,13 @@ def main():
                 bitexact = bool(np.array_equal(ref, out[: args.verify]))
             if cpu_leg:
                 sample = cts[: args.cpu_sample]
-                if not opt:
-                    # the reference's own arithmetic (concrete-cpu's fft64: one f64 spectrum of the
-                    # u64 key, f64 products rounded mod 2^64, output noise in the low bits), not the
-                    # exact limb split the GPU and the checker use
-                    op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, limbs=1)
-                    kw = {"fbsk": O.bsk_to_fourier(op, bsk), "mode": O.MODE_FFT64}
-                    desc = ("fft64 arithmetic restated: one f64 key spectrum, f64 products rounded mod 2^64 "
-                            "(radix-2 FFT, not concrete-fft's SIMD kernels)")
+                # the reference's own arithmetic for every config (concrete-cpu's fft64: one f64
+                # spectrum of the u64 key, f64 products rounded mod 2^64, output noise in the low
+                # bits), not the exact limb split the GPU and the checker use
+                op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, limbs=1)
+                kw = {"fbsk": O.bsk_to_fourier(op, bsk), "mode": O.MODE_FFT64}
+                desc = ("fft64 arithmetic restated: one f64 key spectrum, f64 products rounded mod 2^64 "
+                        "(radix-2 FFT, not concrete-fft's SIMD kernels)")
                 t1 = time.perf_counter()
                 O.pbs_batch(op, sample, acc[None, :], nthreads=cpu_threads, **kw)
                 dt = time.perf_counter() - t1

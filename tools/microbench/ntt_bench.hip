@@ -167,7 +167,7 @@ __global__ void __launch_bounds__(NWAVES * 64) ntt_kern(const Tw* __restrict__ g
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t* s = scr + w * SCR;
   uint32_t v[16];
-  for (int m = 0; m < 16; ++m) v[m] = (uint32_t)((jA(lane, m) * 2654435761u) % P);
+  for (int m = 0; m < 16; ++m) v[m] = (uint32_t)(((uint64_t)jA(lane, m) * 2654435761ull) % P);
   const long long c0 = clock64();
   for (int r = 0; r < (CHECK ? 1 : R); ++r) {
     ntt_fwd(v, tw, s, lane);

@@ -13,7 +13,7 @@ export TMPDIR=/tmp
 run() {  # name counters...
   local name=$1; shift
   timeout -k 10 ${PMC_TIMEOUT:-240} rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o run -- \
-    python $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline --verify 0 --no-e2e $EXTRA > $OUT/$name.log 2>&1
+    python $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline --verify 0 --no-e2e --no-share $EXTRA > $OUT/$name.log 2>&1
 }
 [[ $PASSES == *a* ]] && run a SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS
 [[ $PASSES == *b* ]] && run b SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 SQ_INSTS_LDS SQ_INSTS_SALU

@@ -8,7 +8,7 @@ roofline.valu, roofline.dram).
             (the SQ_INSTS_* counters count wave-instructions, summed over the device).
 The record carries the hash of the kernel sources it was measured on; bench.py uses it only while
 the sources are unchanged.
-Usage: python tools/pmc_record.py gpurun_out/<tag> profiles/<round>_<config>_pmc.json CONFIG BATCH
+Usage: python tools/pmc_record.py gpurun_out/<tag> profiles/<round>_<config>_pmc.json CONFIG BATCH [KERNEL]
        (<tag> holds the pass directories of tools/pmc.sh: d/e for traffic, b for the f64 mix)
 """
 import csv
@@ -21,8 +21,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from bench import kernel_source_hash  # noqa: E402
 
-KERNEL = {"cfg2": "pbs1024_pair", "cfg4": "pbs2048", "opt4": "pbs1024k2", "opt1": "pbs_small", "opt2": "pbs_small",
-          "opt3": "pbs_small"}
+KERNEL = {"cfg2": "pbs1024_pair", "cfg4": "pbs2048", "opt5": "pbs2048", "opt4": "pbs1024k2", "opt1": "pbs_small",
+          "opt2": "pbs_small", "opt3": "pbs_small"}
 # the general path (optB configs) runs several launches per PBS call (pbs_generic.hip): the record
 # sums every gen_* dispatch of the process's single call (tools/pmc.sh: --steps 1 --warmup 0 --no-e2e),
 # except the once-per-key conversion
@@ -49,7 +49,8 @@ def collect(src, kname):
 
 def main():
     src, dst, config, batch = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
-    kname = KERNEL.get(config, config)
+    # optional 5th argument: the kernel-name substring (e.g. pbs1024_hex for cfg2 at B = 512)
+    kname = sys.argv[5] if len(sys.argv) > 5 else KERNEL.get(config, config)
     v = collect(src, kname)
     rec = {"kernel": kname if not kname.startswith("opt") else "gen_* (sum over one PBS call)", "config": config, "batch": batch, "source_hash": kernel_source_hash(config), "pmc_dir": src,
            "counters": v}

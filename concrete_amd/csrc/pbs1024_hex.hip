@@ -10,24 +10,25 @@
 // ciphertext's CMUX step holds 6 forward transforms (2 polynomials x 3 levels) and 6 inverse
 // transforms (2 output polynomials x 3 key limbs), so six waves take one of each — a balanced split
 // with the register fft512 unchanged — and two ciphertexts per workgroup put three waves on every
-// SIMD.  Wave u = 3 c + j of a ciphertext:
-//   * rotation and decomposition of polynomial c (its negated accumulator B_c = -acc_c lives in LDS,
-//     shared by the three waves of c), digits of level j, forward transform of that digit
-//     polynomial, spectrum published in the wave's scratch (all 8 frequency slots);
-//   * key product of output polynomial c, key limb j over the six published spectra (LDS) with the
-//     wave's own slice of the Fourier key (straight from L2 into registers, two level batches ahead:
-//     no LDS ring, no workgroup barriers);
-//   * inverse transform of that product, exact rounding, and the limb's contribution added into B_c
-//     with 64-bit LDS atomics (integer adds mod 2^64: exact in any order).
-// Synchronisation per CMUX step, on per-wave LDS counters (one monotonic count, three events):
-//   A: the six spectra of the ciphertext are published (before the key products read them);
-//   B: every wave of the ciphertext has issued its spectrum reads (before a scratch is overwritten
-//      by the inverse transpose);
-//   C: the three waves of polynomial c have added their limbs (before the next rotation reads B_c).
-// The spectra come out of fft512_fwd in its natural (lane, slot) frequency order, which is the
-// order of the key layout (bsk.hip: group (limb, co, ro) holds column co / row ro in slots 0..3 and
-// column 1 - co / row 1 - ro in slots 4..7, so wave (c, j) reads slots 0..3 of groups (j, c, r) and
-// slots 4..7 of groups (j, 1 - c, 1 - r)).
+// SIMD.  Wave u = 3 c + j of a ciphertext, per CMUX step:
+//   * produce (two ciphertexts per workgroup): rotation X^a B - B of polynomial c and its balanced
+//     decomposition at every level for the coefficient pairs (m, m + 8), m in the wave's third of
+//     the register slots; level q's digits (packed int16 pairs) go to the scratch of wave (c, q).
+//     The negated accumulators B_c live in LDS, shared by the three waves of c.  [barrier D]
+//   * forward transform of the level-j digit polynomial, spectrum published in the wave's scratch
+//     (all 8 frequency slots, fft512's natural order).  [barrier A]
+//   * key products of output c, limb j: the two waves of role u (one per ciphertext) split the
+//     slots — wave h computes [4h, 4h + 4) for BOTH ciphertexts over their six spectra (LDS) — so
+//     each key value is read once per CU, straight from L2 into registers, six batches of four
+//     16-byte values per step, the next step's first three issued in the inverse phase.  [barrier B]
+//   * the other ciphertext's half mailed into its wave's scratch (pair counter), inverse transform
+//     with the k2 ^ 4 relabeling for h = 1, exact rounding, and the limb's contribution added into
+//     B_c with 64-bit LDS atomics (integer adds mod 2^64: exact in any order).  [barrier C]
+// The key layout is the pair kernel's (bsk.hip: group (limb, co, ro) holds column co / row ro in
+// slots 0..3 and column 1 - co / row 1 - ro in slots 4..7, so wave (c, j) reads slots 0..3 of groups
+// (j, c, r) and slots 4..7 of groups (j, 1 - c, 1 - r)).  One ciphertext per workgroup (batches of
+// <= CUs): every wave rotates and decomposes its own digits and computes all eight slots of its own
+// ciphertext's product; the syncs are per-ciphertext LDS counters.
 #include <type_traits>
 
 #include "common.hpp"
@@ -39,14 +40,8 @@
 #ifndef HX_SHARED_DIGITS
 #define HX_SHARED_DIGITS 1  // rotation + decomposition shared by the three waves of a polynomial (XM)
 #endif
-#ifndef HX_PRIO
-#define HX_PRIO 0  // A/B: static wave priorities (1: the youngest third of the waves at 1; 2: w / 4)
-#endif
 #ifndef HX_DIAG_NOKEY
 #define HX_DIAG_NOKEY 0  // timing-only builds: no key loads (the key values are the spectra's)
-#endif
-#ifndef HX_DIAG_NOX
-#define HX_DIAG_NOX 0  // timing-only builds: no spectrum reads in the key products
 #endif
 #ifndef HX_DIAG_NOATOMIC
 #define HX_DIAG_NOATOMIC 0
@@ -198,12 +193,6 @@ pbs1024_hex_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_
     for (int b = 0; b < PF; ++b) load_batch(gb[b], 0, b);
   }
 
-  if constexpr (HX_PRIO == 1) {
-    if (w >= 8) __builtin_amdgcn_s_setprio(1);
-  } else if constexpr (HX_PRIO == 2) {
-    if (w >= 8) __builtin_amdgcn_s_setprio(2);
-    else if (w >= 4) __builtin_amdgcn_s_setprio(1);
-  }
   uint64_t a_next = active && n > 0 ? lwe[0] : 0ull;
   for (uint32_t i = 0; i < n; ++i) {
     const uint64_t step_off = (uint64_t)i * PER_I;
@@ -334,13 +323,7 @@ pbs1024_hex_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out_
         // t = 0: my ciphertext, t = 1 (XM): the other one
         const cplx* X = xch_all + ((t == 0 ? ctl : 1 - ctl) * 6 + r * L + q) * XS + (4 * h) * 64 + lane;
 #pragma unroll
-        for (int k = 0; k < KS; ++k) {
-#if HX_DIAG_NOX
-          x[t][k] = {(double)(b + k), (double)(t + lane)};
-#else
-          x[t][k] = X[k * 64];
-#endif
-        }
+        for (int k = 0; k < KS; ++k) x[t][k] = X[k * 64];
       }
       cplx (&g)[KS] = gb[b % PF];
 #pragma unroll

@@ -1,0 +1,23 @@
+"""Collect the bench lines of tools/r05_final.sh (parts a and d) into one record:
+python tools/collect_bench.py gpurun_out/<tag> profiles/<round>_bench_all_configs.json"""
+import glob
+import json
+import os
+import sys
+
+src, dst = sys.argv[1], sys.argv[2]
+out = {"note": "bench.py lines of every config on the final sources, one MI355X box (tools/r05_final.sh); "
+               "cfg2 = BASELINE configs[1] (the metric), cfg4 = configs[3], opt8 = configs[4]'s optimizer row; "
+               "opt1..opt6 at batch 4096, opt7..opt9 at 1024, opt10 at 512",
+       "lines": {}}
+for f in sorted(glob.glob(os.path.join(src, "bench_*.log"))):
+    name = os.path.basename(f)[len("bench_"):-len(".log")]
+    lines = [l for l in open(f).read().splitlines() if l.startswith("{")]
+    if lines:
+        out["lines"]["cfg2" if name == "default" else name] = json.loads(lines[-1])
+json.dump(out, open(dst, "w"), indent=1)
+for k, v in out["lines"].items():
+    r = v.get("roofline", {})
+    print(f"{k:6s} {v['value']:>10} PBS/s  frac {r.get('frac')}  traffic {r.get('traffic')}  "
+          f"valu {(r.get('valu') or {}).get('frac')}  cpu {(v.get('cpu_baseline') or {}).get('value')}  "
+          f"bitexact {v.get('checks', {}).get('bitexact')}  decrypt {v.get('checks', {}).get('decrypt_ok')}")

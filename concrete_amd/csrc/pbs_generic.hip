@@ -1667,6 +1667,321 @@ __global__ void __launch_bounds__(512) gen_fused_kernel(FusedArgs a) {
 }
 
 
+// ------------------------------------------------------------------------------------------
+// gen_coop_kernel: k = 1, N = 8192 (M = 4096, R = 8 rows) with one ciphertext on TWO workgroups
+// (round 5; the optimizer's 7-bit rows, v0_last_128:194).  gen_fused_kernel's one-CU form does
+// not fit at N = 8192 (both polynomials' rows, X and the accumulator exceed one CU), and the
+// two-launch path moves X, Y and the accumulator through HBM every step (9x the algorithmic bytes).
+// Here workgroup c of a pair owns GLWE polynomial c: its accumulator (in registers, rows as in
+// gen_fused_kernel), the rotation, decomposition and forward transforms of its digits, and the
+// inverse transforms of output c.  Per CMUX step the two workgroups exchange, through L2/MALL:
+//   X  each keeps the column DFT outputs k1 in [4c, 4c + 4) of its digit spectra and hands the
+//      other half to its partner, so each holds BOTH polynomials' spectra at its four k1;
+//   Y  per slot m, the products of both outputs at its k1 (key values straight from L2), the
+//      other output's half handed over, its own output's eight k1 then go through the inverse
+//      column DFT and the row transforms.
+// Hand-offs: MI355X_MICROARCH.md / cdna_hip_programming.md §6 Guideline 16, R1: 16-B payload
+// stores with sc1 (write-through), every storing wave drained (vmcnt(0)), a workgroup barrier,
+// one lane's agent-scope flag store; the consumer's wave 0 polls the flag (relaxed, agent), a
+// barrier, then every payload load a 16-B buffer load with sc1.  Events are counted per call
+// (flags zeroed by the launcher), placement-independent.  Pairs form by ticket (the order in which
+// workgroups start): a workgroup that waits has a running or next-to-start partner, so the launch
+// cannot deadlock while two CUs are free for it; every wait is bounded (guard.spin_limit polls,
+// then DEV_STATUS_SYNC_TIMEOUT).
+// Arithmetic: gen_fused_kernel's / gen_big_step_kernel's (same transforms, tau, key, rounding), so
+// the certified bound (generic_pbs_ok) holds unchanged; the tests compare bit for bit.
+// ------------------------------------------------------------------------------------------
+struct CoopArgs {
+  uint64_t* out;
+  const uint64_t* out_idx;
+  const uint64_t* in;
+  const uint64_t* in_idx;
+  const uint64_t* luts;
+  const uint64_t* lut_idx;
+  const cplx* G;    // Fourier key [n][c][lim][r][q][M], four-step frequency order
+  const cplx* Tau;  // column twiddles [R][512]
+  unsigned long long* resid;
+  cplx* xb;         // X halves [pair][sender][l T][4][512]
+  cplx* yb;         // Y halves [pair][sender][2 (slot parity)][4][512]
+  uint32_t* flags;  // [pair][sender] published events, then the ticket counter
+  uint32_t* status;
+  uint32_t spin_limit, base, count, n, base_log, bits, xb_bytes, yb_bytes;
+};
+constexpr int COOP_R = 8;
+// timing-only builds (wrong results): COOP_DIAG_NOSYNC (no hand-off waits or flags),
+// COOP_DIAG_NOKEY (no key loads)
+#ifndef COOP_DIAG_NOSYNC
+#define COOP_DIAG_NOSYNC 0
+#endif
+#ifndef COOP_DIAG_NOKEY
+#define COOP_DIAG_NOKEY 0
+#endif
+
+using v4u = __attribute__((ext_vector_type(4))) unsigned int;
+__device__ __forceinline__ v4u cplx_bits(cplx v) {
+  const uint64_t r = (uint64_t)__double_as_longlong(v.re), i = (uint64_t)__double_as_longlong(v.im);
+  v4u o;
+  o.x = (uint32_t)r, o.y = (uint32_t)(r >> 32), o.z = (uint32_t)i, o.w = (uint32_t)(i >> 32);
+  return o;
+}
+__device__ __forceinline__ cplx bits_cplx(v4u o) {
+  return {__longlong_as_double((long long)(((uint64_t)o.y << 32) | o.x)),
+          __longlong_as_double((long long)(((uint64_t)o.w << 32) | o.z))};
+}
+
+template <int LV, int T, int L, bool W32>
+__global__ void __launch_bounds__(512) gen_coop_kernel(CoopArgs a) {
+  constexpr int R = COOP_R, M = R * 512, N = 2 * M, RS = 576, LOGR = 3, LOG2_2N = Geo<M>::LOG + 2;
+  constexpr int NXH = LV * T;  // digit spectra of one polynomial per step
+  constexpr uint32_t SC1 = 16;  // cache-policy aux bit: sc1 (write-through stores, L1-bypassing loads)
+  using St = typename std::conditional<W32, uint32_t, uint64_t>::type;
+  using Dg = typename std::conditional<W32, int32_t, int64_t>::type;
+  __shared__ cplx lds[R * RS + FFT512_TABLE_ENTRIES + R * 512];
+  __shared__ uint32_t sh_ticket;
+  cplx* E = lds;
+  cplx* tab = lds + R * RS;
+  cplx* tau = tab + FFT512_TABLE_ENTRIES;
+  build_fft512_tables(tab, threadIdx.x, 512);
+  for (int x = threadIdx.x; x < R * 512; x += 512) tau[x] = a.Tau[x];
+  if (threadIdx.x == 0)
+    sh_ticket = __hip_atomic_fetch_add(a.flags + 2 * a.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const Fft512Tables TB = fft512_tables_at(tab);
+  const uint32_t tk = __builtin_amdgcn_readfirstlane(sh_ticket);
+  const uint32_t p = tk >> 1;
+  const int c = (int)(tk & 1u);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int j1 = w, pos = threadIdx.x;
+  cplx* row = E + w * RS;
+  const uint64_t ct = a.base + p;
+  const uint64_t in_row = a.in_idx ? a.in_idx[ct] : ct;
+  const uint64_t* lwe = a.in + in_row * (uint64_t)(a.n + 1);
+  auto jcol = [&](int e) { return lane + 64 * (e & 7) + 512 * (e >> 3); };
+  uint64_t A[16];
+  {
+    const uint64_t* lut = a.luts + (a.lut_idx ? a.lut_idx[ct] : 0ull) * (uint64_t)(2 * N) + (uint64_t)c * N;
+    const uint32_t bt = modswitch(lwe[a.n], LOG2_2N);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t src = ((uint32_t)(j1 + R * jcol(e)) + bt) & (2 * N - 1);
+      const uint64_t v = lut[src & (N - 1)];
+      A[e] = src < (uint32_t)N ? v : 0ull - v;
+    }
+  }
+  const int logB = (int)a.base_log, sb = (int)a.bits;
+  const int nrep = 64 - LV * logB;
+  const bool split = T > 1;
+  const St half = split ? (St)1 << (sb - 1) : (St)0, bmask = split ? ((St)1 << sb) - (St)1 : ~(St)0;
+  double max_resid = 0.0;
+
+  // ---- hand-off endpoints (byte offsets: per-lane voffset of the sc1 buffer accesses)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(a.xb, 0, (int)a.xb_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(a.yb, 0, (int)a.yb_bytes, 0x00020000);
+  const uint32_t x_out = (p * 2 + c) * (uint32_t)(NXH * 4 * 512 * 16) + pos * 16;
+  const uint32_t x_in = (p * 2 + (1 - c)) * (uint32_t)(NXH * 4 * 512 * 16) + pos * 16;
+  const uint32_t y_out = (p * 2 + c) * (uint32_t)(2 * 4 * 512 * 16) + pos * 16;
+  const uint32_t y_in = (p * 2 + (1 - c)) * (uint32_t)(2 * 4 * 512 * 16) + pos * 16;
+  uint32_t* myflag = a.flags + 2 * p + c;
+  const uint32_t* pflag = a.flags + 2 * p + (1 - c);
+  auto publish = [&](uint32_t ev) __attribute__((always_inline)) {
+    if (COOP_DIAG_NOSYNC) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(myflag, ev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto consume = [&](uint32_t ev) __attribute__((always_inline)) {
+    if (COOP_DIAG_NOSYNC) return;
+    if (w == 0) {
+      for (uint32_t it = 0;; ++it) {
+        if (__hip_atomic_load(pflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ev) break;
+        if (it >= a.spin_limit) {
+          if (lane == 0) __hip_atomic_fetch_or(a.status, DEV_STATUS_SYNC_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // payload loads stay below the poll
+  };
+  pair_barrier();  // tables, tau
+
+#pragma unroll 1
+  for (uint32_t i = 0; i < a.n; ++i) {
+    const uint32_t ev0 = i * (uint32_t)(L + 1);
+    // ---- forward: X^{a_i} acc - acc through the LDS copy of polynomial c (row order)
+    const uint32_t at = modswitch(lwe[i], LOG2_2N);
+    uint64_t* accl = reinterpret_cast<uint64_t*>(E);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) accl[j1 * (N / R) + jcol(e)] = A[e];
+    pair_barrier();
+    St S[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t src = ((uint32_t)(j1 + R * jcol(e)) - at) & (2 * N - 1);
+      const uint32_t idx = src & (N - 1);
+      const uint64_t rv = accl[(idx & (R - 1)) * (N / R) + (idx >> LOGR)];
+      const uint64_t x = (src < (uint32_t)N ? rv : 0ull - rv) - A[e];
+      S[e] = (St)(nrep > 0 ? decomp_init(x, nrep) : x);
+    }
+    pair_barrier();  // the rows are free again
+    // X[r][s][kh]: r = 0 my polynomial, r = 1 the partner's; s = q T + t; frequencies (4 c + kh) 512 + pos
+    cplx X[2][NXH][4];
+#pragma unroll
+    for (int q = 0; q < LV; ++q) {
+      Dg D[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        if constexpr (W32) D[e] = decomp_next_t<uint32_t>(S[e], logB);
+        else D[e] = decomp_next64(S[e], logB);
+      }
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        cplx v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const Dg s0 = (Dg)(((St)D[e] + half) & bmask) - (Dg)half;
+          const Dg s1 = (Dg)(((St)D[e + 8] + half) & bmask) - (Dg)half;
+          D[e] = (D[e] - s0) >> sb;
+          D[e + 8] = (D[e + 8] - s1) >> sb;
+          v[e] = {(double)s0, (double)s1};
+        }
+        fft512_fwd(v, row, TB, lane);
+        if (j1 != 0)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = cmul(v[e], tau[j1 * 512 + e * 64 + lane]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) row[e * 64 + lane] = v[e];
+        pair_barrier();
+        cplx u[R];
+#pragma unroll
+        for (int jj = 0; jj < R; ++jj) u[jj] = E[jj * RS + pos];
+        dft_col<R, false>(u);
+        const int s = q * T + t;
+        // (uniform branches: a select on c would become an indexed, scratch-backed array)
+        auto keep_send = [&](auto CC) __attribute__((always_inline)) {
+          constexpr int C0 = decltype(CC)::value;
+#pragma unroll
+          for (int kh = 0; kh < 4; ++kh) {
+            X[0][s][kh] = u[4 * C0 + kh];
+            __builtin_amdgcn_raw_buffer_store_b128(cplx_bits(u[4 * (1 - C0) + kh]), xr,
+                                                   x_out + (uint32_t)((s * 4 + kh) * 512 * 16), 0, SC1);
+          }
+        };
+        if (c) keep_send(std::integral_constant<int, 1>{});
+        else keep_send(std::integral_constant<int, 0>{});
+        pair_barrier();
+      }
+    }
+    publish(ev0 + 1);
+    consume(ev0 + 1);
+#pragma unroll
+    for (int s = 0; s < NXH; ++s)
+#pragma unroll
+      for (int kh = 0; kh < 4; ++kh)
+        X[1][s][kh] = bits_cplx(__builtin_amdgcn_raw_buffer_load_b128(xr, x_in + (uint32_t)((s * 4 + kh) * 512 * 16), 0, SC1));
+
+    // ---- products and inverse transforms, slot by slot (the key values straight from L2; loading
+    //      the next slot's ahead, across the hand-off and inverse, spills at two waves per SIMD and
+    //      measured slower: 1.94k vs 2.27k PBS/s, profiles/r05/coop_ab.json)
+    const cplx* Gi = a.G + (uint64_t)i * (2 * L * 2 * LV) * M + (uint64_t)(4 * c * 512) + pos;
+#pragma unroll 1
+    for (int m = 0; m < L; ++m) {
+      cplx y[2][4];
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+        for (int kh = 0; kh < 4; ++kh) y[cc][kh] = {0.0, 0.0};
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const int lim = m - t;
+        if (lim < 0) continue;
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            const int rr = r == 0 ? c : 1 - c;  // the key row of X[r]
+#pragma unroll
+            for (int q = 0; q < LV; ++q) {
+              const cplx* g = Gi + (uint64_t)(((cc * L + lim) * 2 + rr) * LV + q) * M;
+#pragma unroll
+              for (int kh = 0; kh < 4; ++kh) {
+                const cplx xv = X[r][q * T + t][kh];
+                const cplx gv = COOP_DIAG_NOKEY ? cplx{xv.im, (double)lim} : g[kh * 512];
+                y[cc][kh].re = __builtin_fma(xv.re, gv.re, __builtin_fma(-xv.im, gv.im, y[cc][kh].re));
+                y[cc][kh].im = __builtin_fma(xv.re, gv.im, __builtin_fma(xv.im, gv.re, y[cc][kh].im));
+              }
+            }
+          }
+      }
+      // the partner's output at my k1 to the partner; its half of mine back
+      const uint32_t par = (uint32_t)(m & 1) * (4 * 512 * 16);
+      auto send = [&](auto CC) __attribute__((always_inline)) {
+        constexpr int C0 = decltype(CC)::value;
+#pragma unroll
+        for (int kh = 0; kh < 4; ++kh)
+          __builtin_amdgcn_raw_buffer_store_b128(cplx_bits(y[1 - C0][kh]), yr, y_out + par + (uint32_t)(kh * 512 * 16),
+                                                 0, SC1);
+      };
+      if (c) send(std::integral_constant<int, 1>{});
+      else send(std::integral_constant<int, 0>{});
+      publish(ev0 + 2 + (uint32_t)m);
+      consume(ev0 + 2 + (uint32_t)m);
+      cplx u[R];
+      auto gather = [&](auto CC) __attribute__((always_inline)) {
+        constexpr int C0 = decltype(CC)::value;
+#pragma unroll
+        for (int kh = 0; kh < 4; ++kh) {
+          u[4 * C0 + kh] = y[C0][kh];
+          u[4 * (1 - C0) + kh] =
+              bits_cplx(__builtin_amdgcn_raw_buffer_load_b128(yr, y_in + par + (uint32_t)(kh * 512 * 16), 0, SC1));
+        }
+      };
+      if (c) gather(std::integral_constant<int, 1>{});
+      else gather(std::integral_constant<int, 0>{});
+      dft_col<R, true>(u);
+#pragma unroll
+      for (int jj = 0; jj < R; ++jj) E[jj * RS + pos] = u[jj];
+      pair_barrier();
+      cplx v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = row[e * 64 + lane];
+      wave_lds_fence();  // the row is read whole before the transform writes its scratch over it
+      if (j1 != 0)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = cmulc(v[e], tau[j1 * 512 + e * 64 + lane]);
+      cplx gi2[4];
+      inv_p2_stage_tw(gi2, TB, lane & 7);
+      fft512_inv_tw(v, row, TB, lane, gi2, 0);
+      const uint32_t sh = ((uint32_t)m * a.bits) & 63u;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const double tr = v[e].re + RND_MAGIC, ti = v[e].im + RND_MAGIC;
+        max_resid = fmax(max_resid, fmax(fabs(v[e].re - (tr - RND_MAGIC)), fabs(v[e].im - (ti - RND_MAGIC))));
+        A[e] += ((uint64_t)__double_as_longlong(tr) - RND_MAGIC_BITS) << sh;
+        A[e + 8] += ((uint64_t)__double_as_longlong(ti) - RND_MAGIC_BITS) << sh;
+      }
+      pair_barrier();  // the rows are written by the next slot's column DFTs
+    }
+  }
+
+  // sample extract (nth = 0): out[j] = -A_0[N - j] (j > 0), out[0] = A_0[0], out[N] = A_1[0]
+  const uint64_t orow = a.out_idx ? a.out_idx[ct] : ct;
+  uint64_t* o = a.out + orow * (uint64_t)(N + 1);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const uint32_t j = (uint32_t)(j1 + R * jcol(e));
+    if (c == 0)
+      o[(N - j) & (N - 1)] = j == 0 ? A[e] : 0ull - A[e];
+    else if (j == 0)
+      o[N] = A[e];
+  }
+  if (a.resid) {
+    for (int off = 32; off > 0; off >>= 1) max_resid = fmax(max_resid, __shfl_xor(max_resid, off));
+    if (lane == 0) atomicMax(a.resid, (unsigned long long)__double_as_longlong(max_resid));
+  }
+}
+
 // Y[ct][c][m][f] = sum over (r, q, t) with 0 <= m - t < L of X[ct][r][q][t][f] * G_i[c][m-t][r][q][f]
 struct MacArgs {
   const cplx* X;
@@ -2434,6 +2749,49 @@ static bool fused_dispatch(const FusedArgs& f, uint32_t k, uint32_t N, uint32_t 
   return false;
 }
 
+// k = 1, N = 8192 with an instance for (l, T, L): gen_coop_kernel, one ciphertext on two workgroups.
+// false: no instance (or CONCRETE_HIP_GEN_COOP=0, A/B runs and tests): the two-launch path runs.
+// Hand-off scratch per ciphertext: X halves 2 x l T x 32 KB, Y halves 2 x 2 x 32 KB; the flags are
+// zeroed before every chunk (events are counted from 1 within a launch).
+static bool coop_dispatch(const PbsArgs& a, const Tables& tb, uint32_t T, uint32_t L, uint32_t b, int* rc) {
+  const char* ce = getenv("CONCRETE_HIP_GEN_COOP");  // read per call (tests cover both paths)
+  if ((ce && atoi(ce) == 0) || a.k != 1 || a.N != 8192 || !four_step(a.N)) return false;
+  const bool w32 = (uint64_t)a.level * a.base_log <= 31;
+  void (*kern)(CoopArgs) = nullptr;
+#define GEN_COOP(LVv, Tv, Lv)                                                                    \
+  if (a.level == LVv && T == Tv && L == Lv) kern = w32 ? gen_coop_kernel<LVv, Tv, Lv, true> : gen_coop_kernel<LVv, Tv, Lv, false>;
+  GEN_COOP(1, 2, 6)
+#undef GEN_COOP
+  if (!kern) return false;
+  const uint64_t xb_ct = 2ull * a.level * T * 4 * 512 * sizeof(cplx), yb_ct = 2ull * 2 * 4 * 512 * sizeof(cplx);
+  const char* ke = getenv("CONCRETE_HIP_GEN_CHUNK");
+  const uint32_t chunk = (uint32_t)std::min<uint64_t>(a.num_samples, ke && atoi(ke) > 0 ? (uint64_t)atoi(ke) : 4096);
+  const uint64_t flag_bytes = ((2ull * chunk + 1) * 4 + 15) / 16 * 16;
+  char* scratch = nullptr;
+  keep_pool_memory();
+  CHIP_CHECK(hipMallocAsync((void**)&scratch, flag_bytes + (xb_ct + yb_ct) * chunk, a.stream));
+  uint32_t* flags = reinterpret_cast<uint32_t*>(scratch);
+  cplx* xb = reinterpret_cast<cplx*>(scratch + flag_bytes);
+  cplx* yb = reinterpret_cast<cplx*>(scratch + flag_bytes + xb_ct * chunk);
+  *rc = 0;
+  for (uint32_t base = 0; base < a.num_samples; base += chunk) {
+    const uint32_t cnt = std::min(chunk, a.num_samples - base);
+    CHIP_CHECK(hipMemsetAsync(flags, 0, flag_bytes, a.stream));
+    const CoopArgs ca{a.out, a.out_idx, a.in, a.in_idx, a.luts, a.lut_idx, reinterpret_cast<const cplx*>(a.fbsk),
+                      tb.Tau, a.resid, xb, yb, flags, a.guard.status, a.guard.spin_limit, base, cnt, a.n, a.base_log,
+                      b, (uint32_t)(xb_ct * cnt), (uint32_t)(yb_ct * cnt)};
+    hipLaunchKernelGGL(kern, dim3(2 * cnt), dim3(512), 0, a.stream, ca);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      set_error("generic pbs (coop) launch failed: %s", hipGetErrorString(e));
+      *rc = -1;
+      break;
+    }
+  }
+  CHIP_CHECK(hipFreeAsync(scratch, a.stream));
+  return true;
+}
+
 // N >= 32768: the split path (S = N / 16384 workgroups per polynomial), one stream, chunks of
 // <= 2 GB of scratch run one after another: init, then per CMUX step the product, the back half
 // and the next step's front half.
@@ -2573,6 +2931,10 @@ int pbs_generic_launch(const PbsArgs& a) {
   const uint32_t T = (a.base_log + b - 1) / b;
   const Tables tb = tables_for(a.N);
   if (a.N == 32768) return pbs_split_launch<2>(a, fmt, tb, T);
+  {
+    int rc = 0;
+    if (coop_dispatch(a, tb, T, L, b, &rc)) return rc;
+  }
   if (a.N == 65536) return pbs_split_launch<4>(a, fmt, tb, T);
   {
     const FusedArgs f{a.out, a.out_idx, a.in, a.in_idx, a.luts, a.lut_idx, reinterpret_cast<const cplx*>(a.fbsk),

@@ -233,6 +233,48 @@ def test_generic_chunked_two_streams(B, oracle, torch_cuda, ci, streams, monkeyp
     assert np.array_equal(B.to_host(out), ref)
 
 
+@pytest.mark.parametrize("chunk", [None, "3"])
+@pytest.mark.parametrize("batch", [1, 2, 7])
+def test_generic_coop_kernel(B, oracle, torch_cuda, batch, chunk, monkeypatch):
+    """N = 8192 on gen_coop_kernel (one ciphertext on two workgroups that hand spectra halves to each
+    other through L2 every CMUX step, round 5): odd and single-ciphertext batches, several chunks
+    (CONCRETE_HIP_GEN_CHUNK=3: the flags re-zeroed per launch), permuted rows and mapped LUTs; bit-exact
+    vs the exact oracle and equal to the two-launch path (CONCRETE_HIP_GEN_COOP=0) on the same inputs."""
+    label, k, N, n, l, logB, width = CASES[6]
+    assert N == 8192
+    p, lwe_sk, glwe_sk, bsk, fbsk = setup(B, torch_cuda, k, N, n, l, logB, 7750 + batch)
+    rng = np.random.RandomState(13 + batch)
+    tables = [rng.randint(0, 1 << width, size=1 << width).astype(np.uint64) for _ in range(2)]
+    luts = np.stack([B.trivial_glwe(p, B.expand_lut(t, p.N, width)) for t in tables])
+    msgs = rng.randint(0, 1 << width, size=batch)
+    cts = B.lwe_encrypt(lwe_sk, [B.encode(m, width) for m in msgs], p.n, 2.0 ** -30, 7753 + batch)
+    in_idx = rng.permutation(batch).astype(np.uint64)
+    out_idx = rng.permutation(batch).astype(np.uint64)
+    lut_idx = rng.randint(0, 2, size=batch).astype(np.uint64)
+    dev = "cuda:0"
+    d = {name: B.to_device(a, dev) for name, a in (("in_idx", in_idx), ("out_idx", out_idx), ("lut_idx", lut_idx))}
+    if chunk:
+        monkeypatch.setenv("CONCRETE_HIP_GEN_CHUNK", chunk)
+    outs = []
+    for coop in ("1", "0"):
+        monkeypatch.setenv("CONCRETE_HIP_GEN_COOP", coop)
+        out = torch_cuda.zeros((batch, p.lwe_out_size), dtype=torch_cuda.int64, device=dev)
+        r = torch_cuda.zeros(1, dtype=torch_cuda.int64, device=dev)
+        B.pbs(p, fbsk, B.to_device(cts, dev), B.to_device(luts, dev), out=out, resid=r, **d)
+        torch_cuda.cuda.synchronize()
+        outs.append(B.to_host(out))
+        resid = float(np.array([r.item()], dtype=np.int64).view(np.float64)[0])
+        kind, limbs, bits = B.bsk_format(p)
+        bound = oracle.generic_error_bound(p.k, p.N, p.level, p.base_log, bits, B.to_host(fbsk).view(np.float64))
+        assert resid < bound < 0.5, (coop, resid, bound)
+    assert B.device_status() == 0
+    op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
+    ref, _ = oracle.pbs_batch(op, cts, luts, bsk=bsk, mode=oracle.MODE_KARATSUBA, lut_idx=lut_idx, in_idx=in_idx,
+                              out_idx=out_idx)
+    assert np.array_equal(outs[0], ref), "coop kernel differs from the exact oracle"
+    assert np.array_equal(outs[1], ref), "two-launch path differs from the exact oracle"
+
+
 def test_generic_outside_exact_range_refused(B):
     """Sets whose certified bound would exceed the gate are refused, not rounded wrongly."""
     assert not B.pbs_supported(B.PbsParams(n=8, k=1, N=131072, level=2, base_log=15))
@@ -368,7 +410,7 @@ def test_configs4_atomic_pattern_8bit(B, oracle, torch_cuda):
 
 # the large-N paths at many CMUX steps and many ciphertexts, bit-exact vs the
 # oracle's Karatsuba product (the table rows' k, N, l, logB; n cut to what the oracle finishes in
-# seconds): N = 4096 (the one-launch kernel), N = 8192 (the two-launch path, chunked over streams),
+# seconds): N = 4096 (the one-launch kernel), N = 8192 (one ciphertext on two workgroups, round 5),
 # N = 2^15 (a polynomial spread over two workgroups).  (label, k, N, n, l, logB, bits, batch)
 LARGE_N_CASES = [
     ("6bit_k1_N4096_n64", 1, 4096, 64, 1, 22, 6, 67),

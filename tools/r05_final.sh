@@ -3,7 +3,7 @@
 #   a: GPU suite, smoke(), the default bench line, kernel-trace stats + PMC records of cfg2 (4096,
 #      pair kernel) and cfg2 at 512 (six-wave kernel), cfg4
 #   b: kernel-trace stats + PMC records of opt1..opt6 (batch 4096)
-#   c: PMC records of opt7 / opt8 (batch 1024, one stream under --pmc)
+#   c: the N = 8192 tests, PMC records of opt6 (4096), opt7 / opt8 (batch 1024, one stream under --pmc)
 #   d: bench lines of every config (CPU baseline, bit-exact rows)
 TAG=${1:-r05f}
 PART=${2:-a}
@@ -46,6 +46,8 @@ b)
   for C in opt1 opt2 opt3 opt4 opt5 opt6; do prof $C bde ""; done
   ;;
 c)
+  step pytest_coop 400 python -u -m pytest tests/test_gpu_pbs_generic.py -v --timeout 200 --timeout-method thread -k "coop or N8192"
+  prof opt6 bde ""
   export CONCRETE_HIP_GEN_STREAMS=1
   prof opt7 bde "--batch 1024" 400
   prof opt8 bde "--batch 1024" 500
@@ -57,6 +59,7 @@ d)
   for C in opt7 opt8 opt9; do
     step bench_$C 500 python -u bench.py --config $C --batch 1024 --verify 1 --no-e2e --no-sdfg
   done
+  CONCRETE_HIP_GEN_COOP=0 step bench_opt7_twolaunch 500 python -u bench.py --config opt7 --batch 1024 --verify 1 --no-e2e --no-sdfg
   step bench_opt10 700 python -u bench.py --config opt10 --batch 512 --verify 1 --no-e2e --no-sdfg
   ;;
 esac

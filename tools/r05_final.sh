@@ -4,7 +4,8 @@
 #      pair kernel) and cfg2 at 512 (six-wave kernel), cfg4
 #   b: kernel-trace stats + PMC records of opt1..opt6 (batch 4096)
 #   c: the N = 8192 tests, PMC records of opt6 (4096), opt7 / opt8 (batch 1024, one stream under --pmc)
-#   d: bench lines of every config (CPU baseline, bit-exact rows)
+#   d: bench lines of cfg4, opt1..opt6 (CPU baseline, bit-exact rows)
+#   e: bench lines of opt7..opt10 (opt7 also on the two-launch path)
 TAG=${1:-r05f}
 PART=${2:-a}
 R=$GRAFT_REPO_ROOT
@@ -56,6 +57,8 @@ d)
   for C in cfg4 opt1 opt2 opt3 opt4 opt5 opt6; do
     step bench_$C 400 python -u bench.py --config $C --verify 2 --no-e2e --no-sdfg
   done
+  ;;
+e)
   for C in opt7 opt8 opt9; do
     step bench_$C 500 python -u bench.py --config $C --batch 1024 --verify 1 --no-e2e --no-sdfg
   done

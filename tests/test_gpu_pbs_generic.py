@@ -275,6 +275,50 @@ def test_generic_coop_kernel(B, oracle, torch_cuda, batch, chunk, monkeypatch):
     assert np.array_equal(outs[1], ref), "two-launch path differs from the exact oracle"
 
 
+def test_generic_coop_kernel_under_load_and_bounded_waits(B, oracle, torch_cuda):
+    """gen_coop_kernel's hand-offs (cdna_hip_programming.md §6 G16: test under uneven load) while a
+    second stream streams 1 GB copies across the chip: bit-exact vs the oracle and no timeout; then
+    with the spin bound forced to one poll for this thread's launches, the call's stream reports the
+    timeout (-4) instead of hanging, and the device is clean afterwards."""
+    torch = torch_cuda
+    label, k, N, n, l, logB, width = CASES[6]
+    p, lwe_sk, glwe_sk, bsk, fbsk = setup(B, torch, k, N, n, l, logB, 7780)
+    rng = np.random.RandomState(17)
+    table = rng.randint(0, 1 << width, size=1 << width).astype(np.uint64)
+    msgs = rng.randint(0, 1 << width, size=96)
+    cts = B.lwe_encrypt(lwe_sk, [B.encode(m, width) for m in msgs], p.n, 2.0 ** -30, 7783)
+    acc = B.trivial_glwe(p, B.expand_lut(table, p.N, width))
+    dev = "cuda:0"
+    d_in, d_acc = B.to_device(cts, dev), B.to_device(acc[None, :], dev)
+    src = torch.empty(1 << 27, dtype=torch.float64, device=dev)
+    dst = torch.empty_like(src)
+    side, main = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    assert B.device_status(dev) == 0
+    with torch.cuda.stream(side):
+        for _ in range(24):
+            dst.copy_(src)
+    with torch.cuda.stream(main):
+        out = B.pbs(p, fbsk, d_in, d_acc)
+        assert B.stream_status(dev, main) == 0
+    torch.cuda.synchronize()
+    rows = np.array([0, 47, 95])
+    op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
+    ref, _ = oracle.pbs_batch(op, cts[rows], acc[None, :], bsk=bsk, mode=oracle.MODE_KARATSUBA)
+    got = B.to_host(out)
+    assert np.array_equal(got[rows], ref)
+    dec = B.lwe_decrypt(glwe_sk, got, p.big_n)
+    assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs]
+    try:
+        B.set_thread_spin_limit(1)
+        with torch.cuda.stream(main):
+            B.pbs(p, fbsk, d_in, d_acc)
+            st = B.stream_status(dev, main)
+    finally:
+        B.set_thread_spin_limit(0)
+    assert st == -4, st
+    assert B.device_status(dev) == 0
+
+
 def test_generic_outside_exact_range_refused(B):
     """Sets whose certified bound would exceed the gate are refused, not rounded wrongly."""
     assert not B.pbs_supported(B.PbsParams(n=8, k=1, N=131072, level=2, base_log=15))

@@ -6,6 +6,7 @@
 #   c: the N = 8192 tests, PMC records of opt6 (4096), opt7 / opt8 (batch 1024, one stream under --pmc)
 #   d: bench lines of cfg4, opt1..opt6 (CPU baseline, bit-exact rows)
 #   e: bench lines of opt7..opt10 (opt7 also on the two-launch path)
+#   f: the GPU suite, smoke() and the default bench line again (after the PMC records are in)
 TAG=${1:-r05f}
 PART=${2:-a}
 R=$GRAFT_REPO_ROOT
@@ -59,11 +60,17 @@ d)
   done
   ;;
 e)
+  step pytest_coop_e 400 python -u -m pytest tests/test_gpu_pbs_generic.py -v --timeout 200 --timeout-method thread -k "coop"
   for C in opt7 opt8 opt9; do
     step bench_$C 500 python -u bench.py --config $C --batch 1024 --verify 1 --no-e2e --no-sdfg
   done
   CONCRETE_HIP_GEN_COOP=0 step bench_opt7_twolaunch 500 python -u bench.py --config opt7 --batch 1024 --verify 1 --no-e2e --no-sdfg
   step bench_opt10 700 python -u bench.py --config opt10 --batch 512 --verify 1 --no-e2e --no-sdfg
+  ;;
+f)
+  step pytest_gpu_f 1000 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread
+  step smoke_f 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+  step bench_default 400 python -u bench.py
   ;;
 esac
 echo "part $PART done"

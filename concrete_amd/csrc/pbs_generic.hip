@@ -1716,6 +1716,9 @@ constexpr int COOP_R = 8;
 #ifndef COOP_DIAG_NOKEY
 #define COOP_DIAG_NOKEY 0
 #endif
+#ifndef COOP_LIMB
+#define COOP_LIMB 1  // limb-major products: each key value read once per step (2.53k vs 2.30k PBS/s)
+#endif
 
 using v4u = __attribute__((ext_vector_type(4))) unsigned int;
 __device__ __forceinline__ v4u cplx_bits(cplx v) {
@@ -1885,15 +1888,46 @@ __global__ void __launch_bounds__(512) gen_coop_kernel(CoopArgs a) {
     //      the next slot's ahead, across the hand-off and inverse, spills at two waves per SIMD and
     //      measured slower: 1.94k vs 2.27k PBS/s, profiles/r05/coop_ab.json)
     const cplx* Gi = a.G + (uint64_t)i * (2 * L * 2 * LV) * M + (uint64_t)(4 * c * 512) + pos;
+    cplx Yn[2][4];  // COOP_LIMB: slot m's t = 1 terms (limb m - 1), carried from the previous slot
 #pragma unroll 1
     for (int m = 0; m < L; ++m) {
       cplx y[2][4];
 #pragma unroll
       for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
-        for (int kh = 0; kh < 4; ++kh) y[cc][kh] = {0.0, 0.0};
+        for (int kh = 0; kh < 4; ++kh) y[cc][kh] = COOP_LIMB && T == 2 && m > 0 ? Yn[cc][kh] : cplx{0.0, 0.0};
+      if constexpr (COOP_LIMB && T == 2) {
+        // limb m's key values once: its t = 0 terms into slot m, its t = 1 terms into slot m + 1
+        // (half the key bytes of the slot-major form); one output's values in flight at a time.
+        // (The last limb's t = 1 terms land in slot L, zero mod 2^64; skipping them in a second
+        // copy of the loop spilled 13 VGPRs.)
 #pragma unroll
-      for (int t = 0; t < T; ++t) {
+        for (int cc = 0; cc < 2; ++cc) {
+#pragma unroll
+          for (int kh = 0; kh < 4; ++kh) Yn[cc][kh] = {0.0, 0.0};
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            const int rr = r == 0 ? c : 1 - c;
+#pragma unroll
+            for (int q = 0; q < LV; ++q) {
+              const cplx* g = Gi + (uint64_t)(((cc * L + m) * 2 + rr) * LV + q) * M;
+#pragma unroll
+              for (int kh = 0; kh < 4; ++kh) {
+                const cplx x0 = X[r][q * T][kh], x1 = X[r][q * T + 1][kh];
+                const cplx gv = COOP_DIAG_NOKEY ? cplx{x0.im, (double)m} : g[kh * 512];
+                y[cc][kh].re = __builtin_fma(x0.re, gv.re, __builtin_fma(-x0.im, gv.im, y[cc][kh].re));
+                y[cc][kh].im = __builtin_fma(x0.re, gv.im, __builtin_fma(x0.im, gv.re, y[cc][kh].im));
+                Yn[cc][kh].re = __builtin_fma(x1.re, gv.re, __builtin_fma(-x1.im, gv.im, Yn[cc][kh].re));
+                Yn[cc][kh].im = __builtin_fma(x1.re, gv.im, __builtin_fma(x1.im, gv.re, Yn[cc][kh].im));
+              }
+            }
+          }
+          // one output's key values in flight at a time (without this barrier: 2.34k vs 2.51k)
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < (COOP_LIMB && T == 2 ? 0 : T); ++t) {
         const int lim = m - t;
         if (lim < 0) continue;
 #pragma unroll

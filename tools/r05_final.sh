@@ -7,6 +7,7 @@
 #   d: bench lines of cfg4, opt1..opt6 (CPU baseline, bit-exact rows)
 #   e: bench lines of opt7..opt10 (opt7 also on the two-launch path)
 #   f: the GPU suite, smoke() and the default bench line again (after the PMC records are in)
+#   g: after a general-path edit: the N = 8192 tests, PMC records and bench lines of opt6..opt8
 TAG=${1:-r05f}
 PART=${2:-a}
 R=$GRAFT_REPO_ROOT
@@ -66,6 +67,17 @@ e)
   done
   CONCRETE_HIP_GEN_COOP=0 step bench_opt7_twolaunch 500 python -u bench.py --config opt7 --batch 1024 --verify 1 --no-e2e --no-sdfg
   step bench_opt10 700 python -u bench.py --config opt10 --batch 512 --verify 1 --no-e2e --no-sdfg
+  ;;
+g)
+  step pytest_coop_g 400 python -u -m pytest tests/test_gpu_pbs_generic.py -v --timeout 200 --timeout-method thread -k "coop or N8192"
+  prof opt6 bde ""
+  CONCRETE_HIP_GEN_STREAMS=1 prof opt7 bde "--batch 1024" 400
+  CONCRETE_HIP_GEN_STREAMS=1 prof opt8 bde "--batch 1024" 500
+  step bench_opt6 400 python -u bench.py --config opt6 --verify 2 --no-e2e --no-sdfg
+  for C in opt7 opt8; do
+    step bench_$C 500 python -u bench.py --config $C --batch 1024 --verify 1 --no-e2e --no-sdfg
+  done
+  CONCRETE_HIP_GEN_COOP=0 step bench_opt7_twolaunch 500 python -u bench.py --config opt7 --batch 1024 --verify 1 --no-e2e --no-sdfg
   ;;
 f)
   step pytest_gpu_f 1000 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread

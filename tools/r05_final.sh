@@ -8,6 +8,7 @@
 #   e: bench lines of opt7..opt10 (opt7 also on the two-launch path)
 #   f: the GPU suite, smoke() and the default bench line again (after the PMC records are in)
 #   g: after a general-path edit: the N = 8192 tests, PMC records and bench lines of opt6..opt8
+#   h: the opt6..opt8 bench lines again, once g's records are committed (bench.py attaches them)
 TAG=${1:-r05f}
 PART=${2:-a}
 R=$GRAFT_REPO_ROOT
@@ -78,6 +79,12 @@ g)
     step bench_$C 500 python -u bench.py --config $C --batch 1024 --verify 1 --no-e2e --no-sdfg
   done
   CONCRETE_HIP_GEN_COOP=0 step bench_opt7_twolaunch 500 python -u bench.py --config opt7 --batch 1024 --verify 1 --no-e2e --no-sdfg
+  ;;
+h)
+  step bench_opt6 400 python -u bench.py --config opt6 --verify 2 --no-e2e --no-sdfg
+  for C in opt7 opt8; do
+    step bench_$C 500 python -u bench.py --config $C --batch 1024 --verify 1 --no-e2e --no-sdfg
+  done
   ;;
 f)
   step pytest_gpu_f 1000 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread

@@ -2799,7 +2799,9 @@ static bool coop_dispatch(const PbsArgs& a, const Tables& tb, uint32_t T, uint32
   if (!kern) return false;
   const uint64_t xb_ct = 2ull * a.level * T * 4 * 512 * sizeof(cplx), yb_ct = 2ull * 2 * 4 * 512 * sizeof(cplx);
   const char* ke = getenv("CONCRETE_HIP_GEN_CHUNK");
-  const uint32_t chunk = (uint32_t)std::min<uint64_t>(a.num_samples, ke && atoi(ke) > 0 ? (uint64_t)atoi(ke) : 4096);
+  // (<= 8192 ciphertexts per launch: the kernel's hand-off buffer descriptors count bytes in 31 bits)
+  const uint32_t chunk = (uint32_t)std::min<uint64_t>(
+      a.num_samples, std::min<uint64_t>(ke && atoi(ke) > 0 ? (uint64_t)atoi(ke) : 4096, 8192));
   const uint64_t flag_bytes = ((2ull * chunk + 1) * 4 + 15) / 16 * 16;
   char* scratch = nullptr;
   keep_pool_memory();

@@ -319,6 +319,35 @@ def test_generic_coop_kernel_under_load_and_bounded_waits(B, oracle, torch_cuda)
     assert B.device_status(dev) == 0
 
 
+@pytest.mark.parametrize("ci", [5, 6, 7], ids=[CASES[i][0] for i in (5, 6, 7)])
+def test_generic_edge_inputs(B, oracle, torch_cuda, ci):
+    """test_gpu_pbs.py::test_pbs_edge_inputs on the large-N paths (N = 4096 one launch, N = 8192 two
+    workgroups per ciphertext, N = 16384 two launches): zero mask elements (tfhe's skip rule), mask
+    elements whose modulus switch is 0 but which are not 0, values just below a modulus-switch rounding
+    boundary, a body that rounds up to 2N, ms = N (negation), all-zero and all-ones ciphertexts;
+    bit-exact vs the oracle's Karatsuba product."""
+    label, k, N, n, l, logB, width = CASES[ci]
+    p, lwe_sk, glwe_sk, bsk, fbsk = setup(B, torch_cuda, k, N, n, l, logB, 7800 + ci)
+    rng = np.random.RandomState(23)
+    table = rng.randint(0, 1 << width, size=1 << width).astype(np.uint64)
+    msgs = rng.randint(0, 1 << width, size=8)
+    cts = B.lwe_encrypt(lwe_sk, [B.encode(m, width) for m in msgs], p.n, 2.0 ** -30, 7803 + ci)
+    log2_2n = (2 * N).bit_length() - 1
+    cts[0, : p.n // 2] = 0
+    cts[1, :] = 0
+    cts[2, :] = np.uint64(0xFFFFFFFFFFFFFFFF)
+    cts[3, : p.n] = np.uint64(1)                                      # ms(1) == 0 but a_i != 0
+    cts[4, : p.n] = np.uint64((1 << (63 - log2_2n)) - 1)              # just below a rounding boundary
+    cts[5, p.n] = np.uint64(0xFFFFFFFFFFFFFFFF - 5)                   # body rounds up to 2N
+    cts[6, : p.n] = np.uint64(1 << 63)                                # ms = N (negation)
+    acc = B.trivial_glwe(p, B.expand_lut(table, p.N, width))
+    out = B.pbs(p, fbsk, B.to_device(cts, "cuda:0"), B.to_device(acc[None, :], "cuda:0"))
+    torch_cuda.cuda.synchronize()
+    op = oracle.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log)
+    ref, _ = oracle.pbs_batch(op, cts, acc[None, :], bsk=bsk, mode=oracle.MODE_KARATSUBA)
+    assert np.array_equal(B.to_host(out), ref)
+
+
 def test_generic_outside_exact_range_refused(B):
     """Sets whose certified bound would exceed the gate are refused, not rounded wrongly."""
     assert not B.pbs_supported(B.PbsParams(n=8, k=1, N=131072, level=2, base_log=15))

@@ -1753,7 +1753,7 @@ __global__ void __launch_bounds__(512) gen_coop_kernel(CoopArgs a) {
   const uint32_t tk = __builtin_amdgcn_readfirstlane(sh_ticket);
   const uint32_t p = tk >> 1;
   const int c = (int)(tk & 1u);
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int j1 = w, pos = threadIdx.x;
   cplx* row = E + w * RS;
   const uint64_t ct = a.base + p;

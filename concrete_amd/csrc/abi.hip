@@ -9,6 +9,7 @@
 #include <atomic>
 #include <mutex>
 #include <unordered_map>
+#include <vector>
 
 #include "../../include/concrete_hip.h"
 #include "common.hpp"
@@ -69,19 +70,26 @@ static void set_device(uint32_t gpu) { CHIP_CHECK(hipSetDevice((int)gpu)); }
 // Status words (common.hpp SyncGuard), one per (device, stream): a launch flags the word of the stream
 // it runs on, so a call reading its own stream's word is told about its own launches only (round 5;
 // the round-4 word was per device, and a spin-bound failure in one call's kernel aborted whichever
-// concurrent call read the word first).  Per device a slab of STATUS_SLOTS words is allocated on first
-// use, zeroed, never freed; slot 0 serves the null stream and any stream past the slab's capacity
-// (shared, as before).  A stream handle keeps its slot for the process's life (a destroyed stream's
-// slot is cleared; a new stream that reuses the handle reuses it).
+// concurrent call read the word first).  Per device a slab of STATUS_SLOTS words (+ one reduction
+// word) is allocated on first use, zeroed, never freed; slot 0 serves the null stream and every
+// stream that arrives while all other slots are taken (shared, mapped explicitly so that reads find
+// the word launches write).  A stream's slot returns to the device's free list when the stream is
+// destroyed (release_stream_status: cuda_destroy_stream, the runtime's and the SDFG's slot release),
+// so a server that creates and destroys a stream per call (wrappers.cpp:129/160, 185/255, 283/362)
+// never runs out (round 6).
 constexpr int STATUS_MAX_DEV = 64;
 constexpr uint32_t STATUS_SLOTS = 4096;
 struct DevStatus {
-  uint32_t* slab = nullptr;
-  uint32_t used = 0;
+  uint32_t* slab = nullptr;  // STATUS_SLOTS words + the take_device_status reduction word
+  uint32_t used = 0;         // high-water mark of handed-out slots (slot 0 included)
+  uint32_t live = 0;         // slots other than 0 held by live streams
+  std::vector<uint32_t> free_slots;
   std::unordered_map<hipStream_t, uint32_t> slot;
 };
 static std::mutex g_status_mu;
 static DevStatus g_status[STATUS_MAX_DEV];
+static std::mutex g_take_mu[STATUS_MAX_DEV];  // one take_device_status per device at a time (reduction word)
+static uint32_t g_status_cap = STATUS_SLOTS;  // test hook (concrete_hip_set_status_slot_cap), g_status_mu
 static std::atomic<uint32_t> g_spin_limit{DEFAULT_SPIN_LIMIT};
 static thread_local uint32_t t_spin_limit = 0;  // per-thread override (test hook), 0 = the global bound
 
@@ -92,7 +100,8 @@ static void check_gpu_index(int gpu) {
   }
 }
 
-// the status word of (gpu, s), allocating the device's slab on first use (g_status_mu held)
+// the status word of (gpu, s), allocating the device's slab on first use (g_status_mu held);
+// nullptr when !create and s has no word yet (no PBS kernel has run on it)
 static uint32_t* status_word_locked(int gpu, hipStream_t s, bool create) {
   DevStatus& d = g_status[gpu];
   if (!d.slab) {
@@ -101,8 +110,8 @@ static uint32_t* status_word_locked(int gpu, hipStream_t s, bool create) {
     CHIP_CHECK(hipGetDevice(&prev));
     CHIP_CHECK(hipSetDevice(gpu));
     void* p = nullptr;
-    CHIP_CHECK(hipMalloc(&p, STATUS_SLOTS * sizeof(uint32_t)));
-    CHIP_CHECK(hipMemset(p, 0, STATUS_SLOTS * sizeof(uint32_t)));
+    CHIP_CHECK(hipMalloc(&p, (STATUS_SLOTS + 1) * sizeof(uint32_t)));
+    CHIP_CHECK(hipMemset(p, 0, (STATUS_SLOTS + 1) * sizeof(uint32_t)));
     CHIP_CHECK(hipSetDevice(prev));
     d.slab = (uint32_t*)p;
     d.used = 1;  // slot 0: null stream / overflow
@@ -111,9 +120,18 @@ static uint32_t* status_word_locked(int gpu, hipStream_t s, bool create) {
   auto it = d.slot.find(s);
   if (it != d.slot.end()) return d.slab + it->second;
   if (!create) return nullptr;
-  if (d.used >= STATUS_SLOTS) return d.slab;
-  d.slot.emplace(s, d.used);
-  return d.slab + d.used++;
+  uint32_t k = 0;  // overflow: the shared word, recorded so that the stream's reads find it
+  if (d.live + 1 < g_status_cap) {
+    if (!d.free_slots.empty()) {
+      k = d.free_slots.back();
+      d.free_slots.pop_back();
+    } else {
+      k = d.used++;  // used = live + 1 + free slots <= cap <= STATUS_SLOTS
+    }
+    ++d.live;
+  }
+  d.slot.emplace(s, k);
+  return d.slab + k;
 }
 
 SyncGuard sync_guard(int gpu, hipStream_t s) {
@@ -156,30 +174,43 @@ static int status_error(int gpu, uint32_t v, const char* scope) {
   return -4;
 }
 
-// Device-wide form: synchronises the device and reads (and clears) the words of every stream.
+// Every word is taken with an atomic exchange and OR-ed into the reduction word (slab[STATUS_SLOTS]):
+// a flag that a kernel still running on another stream sets while the slab is being read is either
+// taken here or left for its own stream's read, never wiped unseen (the round-5 form copied
+// the slab and then zeroed all of it).
+__global__ void status_take_kernel(uint32_t* slab, uint32_t used) {
+  uint32_t acc = 0;
+  for (uint32_t i = threadIdx.x; i < used; i += blockDim.x) acc |= atomicExch(slab + i, 0u);
+  if (acc) atomicOr(slab + STATUS_SLOTS, acc);
+}
+
+// Device-wide form: synchronises the device and takes (reads and clears) the words of every stream.
 int take_device_status(int gpu) {
+  if (gpu < 0 || gpu >= STATUS_MAX_DEV) return 0;
+  std::lock_guard<std::mutex> tg(g_take_mu[gpu]);
   uint32_t* slab = nullptr;
   uint32_t used = 0;
   {
     std::lock_guard<std::mutex> g(g_status_mu);
-    if (gpu >= 0 && gpu < STATUS_MAX_DEV) slab = g_status[gpu].slab, used = g_status[gpu].used;
+    slab = g_status[gpu].slab, used = g_status[gpu].used;
   }
   if (!slab) return 0;  // no PBS kernel has run on this device
   int prev = 0;
   CHIP_CHECK(hipGetDevice(&prev));  // the caller's current device is restored (torch shares it)
   CHIP_CHECK(hipSetDevice(gpu));
   CHIP_CHECK(hipDeviceSynchronize());
-  std::vector<uint32_t> v(used);
-  CHIP_CHECK(hipMemcpy(v.data(), slab, used * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  status_take_kernel<<<1, 256, 0, nullptr>>>(slab, used);
+  CHIP_CHECK(hipGetLastError());
   uint32_t any = 0;
-  for (uint32_t x : v) any |= x;
-  if (any) CHIP_CHECK(hipMemset(slab, 0, used * sizeof(uint32_t)));
+  CHIP_CHECK(hipMemcpy(&any, slab + STATUS_SLOTS, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (any) CHIP_CHECK(hipMemset(slab + STATUS_SLOTS, 0, sizeof(uint32_t)));
   CHIP_CHECK(hipSetDevice(prev));
   return any ? status_error(gpu, any, "some stream") : 0;
 }
 
 // Stream-ordered form: the word of stream s is read on s after the work issued there (the runtime's
 // slice and shard streams), so concurrent calls on other streams are neither waited for nor blamed.
+// (An overflowed stream shares slot 0 and may be told of another overflowed stream's failure.)
 int take_stream_status(int gpu, hipStream_t s, uint32_t* h) {
   uint32_t* w;
   {
@@ -199,14 +230,35 @@ int take_stream_status(int gpu, hipStream_t s, uint32_t* h) {
   return status_error(gpu, v, "this call's stream");
 }
 
-// a destroyed stream's word is cleared (a later stream may reuse the handle)
-static void clear_stream_status(int gpu, hipStream_t s) {
-  uint32_t* w;
+// A stream about to be destroyed (its work synchronised by the caller): its word is cleared and its
+// slot goes back to the device's free list.  Slot 0 (shared) is never cleared here.
+void release_stream_status(int gpu, hipStream_t s) {
+  if (gpu < 0 || gpu >= STATUS_MAX_DEV || !s) return;
+  uint32_t* w = nullptr;
   {
     std::lock_guard<std::mutex> g(g_status_mu);
-    w = (gpu >= 0 && gpu < STATUS_MAX_DEV && s) ? status_word_locked(gpu, s, false) : nullptr;
+    DevStatus& d = g_status[gpu];
+    auto it = d.slot.find(s);
+    if (it == d.slot.end()) return;
+    const uint32_t k = it->second;
+    d.slot.erase(it);
+    if (k == 0) return;
+    --d.live;
+    w = d.slab + k;
+    // cleared before the slot can be handed out again (the lock is held across the clear)
+    int prev = 0;
+    CHIP_CHECK(hipGetDevice(&prev));
+    CHIP_CHECK(hipSetDevice(gpu));
+    CHIP_CHECK(hipMemset(w, 0, sizeof(uint32_t)));
+    CHIP_CHECK(hipSetDevice(prev));
+    d.free_slots.push_back(k);
   }
-  if (w) CHIP_CHECK(hipMemset(w, 0, sizeof(uint32_t)));
+}
+
+uint32_t status_slots_in_use(int gpu) {
+  if (gpu < 0 || gpu >= STATUS_MAX_DEV) return 0;
+  std::lock_guard<std::mutex> g(g_status_mu);
+  return g_status[gpu].live;
 }
 
 // ---- general-format companion keys (pbs_needs_generic_key) ------------------------------
@@ -248,6 +300,7 @@ void release_std_source(const void* primary) {
     g_src.erase(it);
   }
   if (c) {
+    key_spectrum_forget(c);
     int prev = 0;
     CHIP_CHECK(hipGetDevice(&prev));
     CHIP_CHECK(hipSetDevice(gpu));
@@ -280,10 +333,12 @@ const void* generic_companion_key(const void* primary, uint32_t n, uint32_t k, u
     src_dev = (const uint64_t*)tmp;
   }
   ConvertArgs a{s, d, src_dev, n, k, level, N, generic_key_format(k, N, level).limbs};
-  const int rc = convert_bsk_generic_launch(a);
+  int rc = convert_bsk_generic_launch(a);
+  if (rc == 0) rc = key_spectrum_record(s, d, generic_key_format(k, N, level), n, k, N, level);
   CHIP_CHECK(hipStreamSynchronize(s));
   if (tmp) CHIP_CHECK(hipFree(tmp));
   if (rc != 0) {
+    key_spectrum_forget(d);
     CHIP_CHECK(hipFree(d));
     return nullptr;
   }
@@ -310,7 +365,7 @@ void* cuda_create_stream(uint32_t gpu_index) {
 void cuda_destroy_stream(void* stream, uint32_t gpu_index) {
   set_device(gpu_index);
   CHIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
-  clear_stream_status((int)gpu_index, (hipStream_t)stream);
+  release_stream_status((int)gpu_index, (hipStream_t)stream);
   CHIP_CHECK(hipStreamDestroy((hipStream_t)stream));
 }
 
@@ -349,6 +404,7 @@ static void release_registered(void* ptr) {
   }
   if (f) {
     release_std_source(f);
+    key_spectrum_forget(f);
     CHIP_CHECK(hipFree(f));
   }
 }
@@ -358,6 +414,7 @@ void cuda_drop(void* ptr, uint32_t gpu_index) {
   set_device(gpu_index);
   release_registered(ptr);
   release_key_bytes(ptr, nullptr, true);
+  key_spectrum_forget(ptr);
   CHIP_CHECK(hipFree(ptr));
 }
 
@@ -366,12 +423,14 @@ void cuda_drop_async(void* ptr, void* stream, uint32_t gpu_index) {
   set_device(gpu_index);
   release_registered(ptr);
   release_key_bytes(ptr, (hipStream_t)stream, true);
+  key_spectrum_forget(ptr);
   CHIP_CHECK(hipFreeAsync(ptr, (hipStream_t)stream));
 }
 
 int concrete_hip_release_device_buffer(const void* ptr) {
   if (!ptr) return 0;
   release_registered((void*)ptr);
+  key_spectrum_forget(ptr);
   return release_key_bytes(ptr, nullptr, false);
 }
 
@@ -386,7 +445,7 @@ void cuda_synchronize_device(uint32_t gpu_index) {
 // ----------------------------------------------------------------------------------------
 // extensions
 // ----------------------------------------------------------------------------------------
-uint32_t concrete_hip_abi_version(void) { return 4u; }
+uint32_t concrete_hip_abi_version(void) { return 5u; }
 const char* concrete_hip_last_error(void) { return last_error(); }
 int concrete_hip_device_status(uint32_t gpu_index) { return take_device_status((int)gpu_index); }
 int concrete_hip_stream_status(void* stream, uint32_t gpu_index) {
@@ -400,6 +459,13 @@ int concrete_hip_stream_status(void* stream, uint32_t gpu_index) {
   return take_stream_status((int)gpu_index, (hipStream_t)stream, landing);
 }
 void concrete_hip_set_thread_spin_limit(uint32_t polls) { t_spin_limit = polls; }
+
+uint32_t concrete_hip_status_slots_in_use(uint32_t gpu_index) { return status_slots_in_use((int)gpu_index); }
+
+void concrete_hip_set_status_slot_cap(uint32_t slots) {
+  std::lock_guard<std::mutex> g(g_status_mu);
+  g_status_cap = (slots == 0 || slots > STATUS_SLOTS) ? STATUS_SLOTS : slots;
+}
 
 void concrete_hip_set_spin_limit(uint32_t polls) {
   g_spin_limit.store(polls ? polls : DEFAULT_SPIN_LIMIT, std::memory_order_relaxed);
@@ -475,6 +541,11 @@ int concrete_hip_convert_bsk(void* stream, uint32_t gpu_index, void* dest_fourie
   ConvertArgs a{s, dest_fourier, src_dev, input_lwe_dim, glwe_dim, level_count, polynomial_size,
                 default_limbs(glwe_dim, polynomial_size, level_count)};
   int rc = convert_bsk_launch(a);
+  // the key's measured spectrum against the certified bound (keycheck.hip; synchronises s, as the
+  // reference does after its conversion, context.h:110-113)
+  if (rc == 0) rc = key_spectrum_record(s, dest_fourier, key_format(glwe_dim, polynomial_size, level_count),
+                                        input_lwe_dim, glwe_dim, polynomial_size, level_count);
+  else key_spectrum_forget(dest_fourier);
   if (tmp) CHIP_CHECK(hipFreeAsync(tmp, s));
   return rc;
 }
@@ -493,7 +564,7 @@ int concrete_hip_pbs(void* stream, uint32_t gpu_index, uint64_t* lwe_array_out, 
     set_error("pbs: lwe_dimension must be > 0");
     return -3;
   }
-  const bool generic = !pbs_params_ok(glwe_dimension, polynomial_size, level_count, base_log);
+  bool generic = !pbs_params_ok(glwe_dimension, polynomial_size, level_count, base_log);
   if (generic && !pbs_needs_generic_key(glwe_dimension, polynomial_size, level_count, base_log)) {
     set_error("pbs: unsupported parameters k=%u N=%u level=%u base_log=%u", glwe_dimension, polynomial_size,
               level_count, base_log);
@@ -502,6 +573,17 @@ int concrete_hip_pbs(void* stream, uint32_t gpu_index, uint64_t* lwe_array_out, 
   set_device(gpu_index);
   const void* key = fourier_bsk;
   uint32_t limbs = default_limbs(glwe_dimension, polynomial_size, level_count);
+  const KeyKind kind = key_format(glwe_dimension, polynomial_size, level_count).kind;
+  if (!generic && key_bound_check(fourier_bsk, kind, glwe_dimension, polynomial_size, level_count, base_log) != 0) {
+    // this key's spectrum is too large for the hand-tuned kernel at this base_log: the general path's
+    // narrower limbs may still be exact (its companion's own bound is checked below)
+    if (kind == KeyKind::GENERIC ||
+        !generic_pbs_ok(glwe_dimension, polynomial_size, level_count, base_log) ||
+        !generic_companion_key(fourier_bsk, lwe_dimension, glwe_dimension, level_count, polynomial_size,
+                               (hipStream_t)stream))
+      return -2;  // message set by key_bound_check
+    generic = true;
+  }
   if (generic) {
     // digits wider than the hand-tuned kernel takes: the general path, on this key's companion
     key = generic_companion_key(fourier_bsk, lwe_dimension, glwe_dimension, level_count, polynomial_size,
@@ -515,6 +597,8 @@ int concrete_hip_pbs(void* stream, uint32_t gpu_index, uint64_t* lwe_array_out, 
       return -2;
     }
     limbs = generic_key_format(glwe_dimension, polynomial_size, level_count).limbs;
+    if (key_bound_check(key, KeyKind::GENERIC, glwe_dimension, polynomial_size, level_count, base_log) != 0)
+      return -2;
   }
   PbsArgs a{(hipStream_t)stream,
             lwe_array_out,
@@ -567,7 +651,9 @@ int concrete_hip_convert_bsk_generic(void* stream, uint32_t gpu_index, void* des
     src_dev = (const uint64_t*)tmp;
   }
   ConvertArgs a{s, dest, src_dev, input_lwe_dim, glwe_dim, level_count, polynomial_size, f.limbs};
-  const int rc = convert_bsk_generic_launch(a);
+  int rc = convert_bsk_generic_launch(a);
+  if (rc == 0) rc = key_spectrum_record(s, dest, f, input_lwe_dim, glwe_dim, polynomial_size, level_count);
+  else key_spectrum_forget(dest);
   if (tmp) CHIP_CHECK(hipFreeAsync(tmp, s));
   return rc;
 }
@@ -588,6 +674,8 @@ int concrete_hip_pbs_generic(void* stream, uint32_t gpu_index, uint64_t* lwe_arr
               polynomial_size, level_count, base_log);
     return -2;
   }
+  if (key_bound_check(generic_bsk, KeyKind::GENERIC, glwe_dimension, polynomial_size, level_count, base_log) != 0)
+    return -2;
   set_device(gpu_index);
   PbsArgs a{(hipStream_t)stream, lwe_array_out, lwe_output_indexes, lut_vector, lut_vector_indexes, lwe_array_in,
             lwe_input_indexes, generic_bsk, lwe_dimension, glwe_dimension, polynomial_size, base_log, level_count,

@@ -98,6 +98,7 @@ void* keyset_bsk_on(concrete_hip_keyset* ks, uint32_t idx, uint32_t gpu, hipStre
   if (src >= 0) {
     // one conversion per keyset; the other devices get the converted bytes (xGMI peer copy)
     CHIP_CHECK(hipMemcpyPeerAsync(d, (int)gpu, e->dev[src], src, bytes, s));
+    key_spectrum_copy(d, e->dev[src]);  // the copy carries the source's measured spectrum (keycheck.hip)
   } else if (concrete_hip_convert_bsk(s, gpu, d, e->host.data(), 0, e->n, e->k, e->level, e->N) != 0) {
     rt_die("%s", concrete_hip_last_error());
   }
@@ -165,6 +166,7 @@ void slot_release(SliceSlot& sl) {
   for (int i = 0; i < 4; ++i)
     if (sl.ev[i]) CHIP_CHECK(hipEventDestroy(sl.ev[i]));
   if (sl.status_h) CHIP_CHECK(hipHostFree(sl.status_h));
+  release_stream_status((int)sl.gpu, sl.s);
   CHIP_CHECK(hipStreamDestroy(sl.s));
   sl = SliceSlot{};
 }

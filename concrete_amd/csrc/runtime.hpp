@@ -155,6 +155,8 @@ struct SlotSet {
 // into h (page-locked) and s is synchronised — no device-wide synchronisation, so other streams'
 // calls keep running.  Returns 0, or -4 with the message set when a PBS wave synchronisation gave up.
 int take_stream_status(int gpu, hipStream_t s, uint32_t* h);
+// abi.hip: a stream about to be destroyed (its work synchronised): clear its word, free its slot
+void release_stream_status(int gpu, hipStream_t s);
 
 }  // namespace chip
 

@@ -99,6 +99,7 @@ void slot_free(Slot& sl) {
     if (p) CHIP_CHECK(hipFree(p));
   for (void* p : sl.retired) CHIP_CHECK(hipFree(p));
   if (sl.status_h) CHIP_CHECK(hipHostFree(sl.status_h));
+  release_stream_status((int)sl.gpu, sl.s);
   CHIP_CHECK(hipStreamDestroy(sl.s));
   sl = Slot{};
 }

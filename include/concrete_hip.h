@@ -110,7 +110,10 @@ void cuda_negate_lwe_ciphertext_vector_64(void *stream, uint32_t gpu_index, void
 /* ABI version of this header (2: round 3 — context-resolved memref_*_cuda_u64, stream emulator;
  * 3: round 4 — keyswitch support query, key level-order check against client keys;
  * 4: round 5 — status words per (device, stream): concrete_hip_stream_status,
- *    concrete_hip_set_thread_spin_limit). */
+ *    concrete_hip_set_thread_spin_limit;
+ * 5: round 6 — status slots recycled on stream destroy (concrete_hip_status_slots_in_use,
+ *    concrete_hip_set_status_slot_cap), converted keys checked against the certified bound
+ *    (concrete_hip_key_spectrum_max)). */
 uint32_t concrete_hip_abi_version(void);
 /* thread-local message of the last failed concrete_hip_* call */
 const char *concrete_hip_last_error(void);
@@ -137,6 +140,18 @@ int concrete_hip_bsk_format(uint32_t glwe_dim, uint32_t polynomial_size, uint32_
  * -1 when (k, N, l) is not on the general path */
 double concrete_hip_generic_error_bound(uint32_t glwe_dim, uint32_t polynomial_size, uint32_t level_count,
                                         uint32_t base_log, double max_key_spectrum);
+/* The exactness gate against the converted key (round 6).  Every conversion (concrete_hip_convert_bsk,
+ * concrete_hip_convert_bsk_generic, cuda_convert_lwe_programmable_bootstrap_key_64, keyset keys and
+ * general-format companions) reduces the largest limb-spectrum magnitude max|G| of the key it wrote,
+ * records it with the key's device address, and returns -2 when no base_log could use the key exactly;
+ * it synchronises its stream (the reference does too, context.h:110-113).  A PBS on a recorded key
+ * evaluates its kernel's certified rounding bound with that max|G| at its base_log and
+ * returns -2 when the bound reaches 1/2 (a hand-tuned kernel's key first falls back to the general
+ * path's companion when the backend holds its standard key and the companion's bound holds).
+ * concrete_hip_key_spectrum_max: the recorded max|G| of a converted key, -1 when none;
+ * concrete_hip_key_error_bound: the certified bound of a PBS on that key at base_log, -1 when none. */
+double concrete_hip_key_spectrum_max(const void *fourier_key);
+double concrete_hip_key_error_bound(const void *fourier_key, uint32_t base_log);
 /* bytes of the device (Fourier, exact-limb) bootstrapping key */
 uint64_t concrete_hip_fourier_bsk_size_bytes(uint32_t input_lwe_dim, uint32_t glwe_dim, uint32_t level_count,
                                              uint32_t polynomial_size);
@@ -213,6 +228,13 @@ void concrete_hip_set_spin_limit(uint32_t polls);
 /* The same bound for launches issued by the calling host thread only (0: the process-wide bound).
  * Test hook: forces the timeout path on one of several concurrent calls. */
 void concrete_hip_set_thread_spin_limit(uint32_t polls);
+/* Status slots held by live streams of the device (round 6): a stream gets a slot on its first PBS
+ * launch and returns it when it is destroyed (cuda_destroy_stream, the runtime's own streams), so a
+ * caller that creates and destroys a stream per call (wrappers.cpp:129/160) never exhausts them. */
+uint32_t concrete_hip_status_slots_in_use(uint32_t gpu_index);
+/* Test hook: at most `slots` status slots per device (0 restores 4096); a stream arriving while all
+ * are taken shares slot 0, whose reads still report that stream's launches. */
+void concrete_hip_set_status_slot_cap(uint32_t slots);
 
 /* ------------------------------------------------------------------------------------------
  * Part 3: client-side helpers (host code; synthetic workloads and LUT encoding).

@@ -16,7 +16,7 @@
   } while (0)
 
 int main(void) {
-  CHECK(concrete_hip_abi_version() == 4);
+  CHECK(concrete_hip_abi_version() == 5);
   /* cfg2 and cfg4 (BASELINE.json) are supported, N = 2^17 is not (up to 2^16 since round 4) */
   CHECK(concrete_hip_pbs_supported(1, 1024, 3, 7) == 1);
   CHECK(concrete_hip_pbs_supported(1, 2048, 1, 23) == 1);

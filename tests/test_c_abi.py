@@ -25,7 +25,7 @@ def test_c_client_compiles_links_and_runs(tmp_path):
 @pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not installed")
 def test_header_is_valid_cpp(tmp_path):
     src = tmp_path / "h.cpp"
-    src.write_text('#include "concrete_hip.h"\nint main() { return concrete_hip_abi_version() == 4 ? 0 : 1; }\n')
+    src.write_text('#include "concrete_hip.h"\nint main() { return concrete_hip_abi_version() == 5 ? 0 : 1; }\n')
     subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-fsyntax-only", "-I", os.path.join(ROOT, "include"),
                     str(src)], check=True)
 

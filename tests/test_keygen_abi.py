@@ -23,7 +23,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_queries():
     L = _native.lib()
-    assert L.concrete_hip_abi_version() == 4
+    assert L.concrete_hip_abi_version() == 5
     assert L.concrete_hip_pbs_supported(1, 1024, 3, 7) == 1
     assert L.concrete_hip_pbs_supported(1, 1024, 3, 30) == 0  # l * logB >= 64
     # the pair kernel's exactness gate is (k+1) l 2^logB <= 4096 (3-limb rounding bound < 1/4);

@@ -85,16 +85,39 @@ def pmc_traffic(batch: int, config: str):
     return None, None
 
 
-def pmc_f64_flop(batch: int, config: str):
-    """f64 FLOP per launch from a committed PMC record (SQ f64 instruction mix); the work is per
-    ciphertext, so a record at another batch is scaled by the batch ratio (and says so)."""
+def dispatched_kernel(batch: int, config: str, cus: int = 256):
+    """The kernel (PMC record `kernel` field) that runs a whole call of `batch` ciphertexts, or None
+    when the call is split over several kernels (cfg2: concrete_amd/csrc/pbs1024_plan.hpp)."""
+    if config == "cfg2":
+        import ctypes as C
+        from concrete_amd import _native
+        parts = (C.c_uint32 * 3)()
+        _native.lib().concrete_hip_pbs1024_plan(batch, cus, parts)
+        used = [k for k, x in zip(("pbs1024_pair", "pbs1024_hex", "pbs1024_hex"), parts) if x]
+        return used[0] if len(set(used)) == 1 else None
+    # the general path's records sum every gen_* launch of one call (the same launches at any batch)
+    return PMC_KERNEL.get(config, "gen_* (sum over one PBS call)" if config.startswith("opt") else None)
+
+
+# kernel-name substrings of the PMC records (tools/pmc_record.py KERNEL)
+PMC_KERNEL = {"cfg4": "pbs2048", "opt5": "pbs2048", "opt4": "pbs1024k2", "opt1": "pbs_small", "opt2": "pbs_small",
+              "opt3": "pbs_small"}
+
+
+def pmc_f64_flop(batch: int, config: str, cus: int = 256):
+    """f64 FLOP per launch from a committed PMC record (SQ f64 instruction mix).  A record at this
+    batch is used as is; the work is per ciphertext, so a record at another batch is scaled by the
+    batch ratio, but only when it was taken on the kernel this batch's call runs (cfg2
+    runs the six-wave kernel at <= 2 x CUs, the pair kernel above, and a split between)."""
     recs = [r for r in pmc_records(config) if "f64_flop" in r]
-    # a record at this batch first (cfg2 runs another kernel at <= 2 x CUs ciphertexts)
-    recs.sort(key=lambda r: r.get("batch") != batch)
     for rec in recs:
-        if "f64_flop" in rec:
+        if rec.get("batch") == batch:
+            return rec["f64_flop"], rec["src"]
+    kern = dispatched_kernel(batch, config, cus)
+    for rec in recs:
+        if kern is not None and rec.get("kernel") == kern:
             scale = batch / rec["batch"]
-            return rec["f64_flop"] * scale, rec["src"] + ("" if scale == 1 else f" (scaled from batch {rec['batch']})")
+            return rec["f64_flop"] * scale, rec["src"] + f" (scaled from batch {rec['batch']}, same kernel)"
     return None, None
 
 
@@ -496,7 +519,8 @@ def main():
         bitexact = None
         cpu = None
         traffic, traffic_src = pmc_traffic(args.batch, args.config)
-        flop, flop_src = pmc_f64_flop(args.batch, args.config)
+        flop, flop_src = pmc_f64_flop(args.batch, args.config,
+                                      torch.cuda.get_device_properties(dev).multi_processor_count)
         kern_s = kern_ms * 1e-3
         valu = None if flop is None else {
             "achieved": round(flop / kern_s / 1e12, 2), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",

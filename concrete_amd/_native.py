@@ -62,6 +62,7 @@ SIGNATURES = {
     "concrete_hip_status_slots_in_use": (u32, [u32]),
     "concrete_hip_set_status_slot_cap": (None, [u32]),
     "concrete_hip_key_spectrum_max": (C.c_double, [vp]),
+    "concrete_hip_pbs1024_plan": (u64, [u64, u32, C.POINTER(u32)]),
     "concrete_hip_key_error_bound": (C.c_double, [vp, u32]),
     "concrete_hip_secure_log2_std": (dbl, [u64, u64]),
     "concrete_hip_keygen_binary": (None, [vp, u64, u64]),

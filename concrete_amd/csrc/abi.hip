@@ -15,6 +15,7 @@
 #include "common.hpp"
 #include "pbs.hpp"
 #include "companion.hpp"
+#include "pbs1024_plan.hpp"
 
 namespace chip {
 
@@ -459,6 +460,12 @@ int concrete_hip_stream_status(void* stream, uint32_t gpu_index) {
   return take_stream_status((int)gpu_index, (hipStream_t)stream, landing);
 }
 void concrete_hip_set_thread_spin_limit(uint32_t polls) { t_spin_limit = polls; }
+
+uint64_t concrete_hip_pbs1024_plan(uint64_t num_samples, uint32_t cus, uint32_t* parts) {
+  const Pbs1024Plan p = plan_pbs1024(num_samples, cus);
+  if (parts) parts[0] = p.pair, parts[1] = p.hex2, parts[2] = p.hex1;
+  return p.cost;
+}
 
 uint32_t concrete_hip_status_slots_in_use(uint32_t gpu_index) { return status_slots_in_use((int)gpu_index); }
 

@@ -34,6 +34,7 @@
 #include "fft512.hpp"
 #include "kernel_util.hpp"
 #include "pbs.hpp"
+#include "pbs1024_plan.hpp"
 #include "pbs_hex.hpp"
 
 namespace chip {
@@ -565,6 +566,19 @@ static int launch_pair_p(const PbsArgs& a) {
   return a.resid ? launch_pair_t<P, L, true, false>(a) : launch_pair_t<P, L, false, false>(a);
 }
 
+// the contiguous part [start, start + count) of a batched call: the index arrays (the runtime's u64
+// in / out / LUT indexes, wrappers.cpp:215-232) advance with it, or without them the LWE rows do
+static PbsArgs pbs_args_range(const PbsArgs& a, uint32_t start, uint32_t count) {
+  PbsArgs r = a;
+  r.num_samples = count;
+  if (a.in_idx) r.in_idx = a.in_idx + start;
+  else r.in = a.in + (uint64_t)start * (a.n + 1);
+  if (a.out_idx) r.out_idx = a.out_idx + start;
+  else r.out = a.out + (uint64_t)start * (a.k * a.N + 1);
+  if (a.lut_idx) r.lut_idx = a.lut_idx + start;
+  return r;
+}
+
 template <int L>
 static int launch_pair(const PbsArgs& a) {
   if (a.num_samples == 0) return 0;
@@ -588,15 +602,27 @@ static int launch_pair(const PbsArgs& a) {
   // PBS/s), 1536, 2560 ... — and one ciphertext per workgroup at <= CUs (52.5k vs 40.6k at 256).
   // CONCRETE_HIP_PBS_HEX=1 / =2 forces it with that many ciphertexts per workgroup, =0 keeps it off;
   // a forced CONCRETE_HIP_PBS_PAIRS / _QUAD selects those kernels (read per call: tests, A/B).
+  // Round 6: the call is split over the kernels by pbs1024_plan.hpp (whole pair rounds, six-wave
+  // rounds, at most one round of one ciphertext per workgroup), each part a contiguous range of the
+  // batch launched on the caller's stream.
   if (L == 3) {
     const char* he = getenv("CONCRETE_HIP_PBS_HEX");
     const int hx = he ? atoi(he) : -1;
     if (hx == 1 || hx == 2) return pbs1024_hex_launch(a, hx);
     if (hx != 0 && !fe && !getenv("CONCRETE_HIP_PBS_QUAD") && !getenv("CONCRETE_HIP_PBS_STAMPS")) {
-      if (a.num_samples <= cus) return pbs1024_hex_launch(a, 1);
-      const uint64_t r_hex = (a.num_samples + 2ull * cus - 1) / (2ull * cus);
-      const uint64_t r_pair = (a.num_samples + 4ull * cus - 1) / (4ull * cus);
-      if (r_hex * 541 < r_pair * 1020) return pbs1024_hex_launch(a, 2);
+      const Pbs1024Plan plan = plan_pbs1024(a.num_samples, cus);
+      uint32_t start = 0;
+      int rc = 0;
+      if (plan.pair) {
+        rc = launch_pair_p<4, L>(pbs_args_range(a, start, plan.pair));
+        start += plan.pair;
+      }
+      if (rc == 0 && plan.hex2) {
+        rc = pbs1024_hex_launch(pbs_args_range(a, start, plan.hex2), 2);
+        start += plan.hex2;
+      }
+      if (rc == 0 && plan.hex1) rc = pbs1024_hex_launch(pbs_args_range(a, start, plan.hex1), 1);
+      return rc;
     }
   }
   if (L == 3 && P <= 2 && !getenv("CONCRETE_HIP_PBS_STAMPS")) {

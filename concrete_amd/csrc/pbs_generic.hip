@@ -1688,6 +1688,19 @@ __global__ void __launch_bounds__(512) gen_fused_kernel(FusedArgs a) {
 // workgroups start): a workgroup that waits has a running or next-to-start partner, so the launch
 // cannot deadlock while two CUs are free for it; every wait is bounded (guard.spin_limit polls,
 // then DEV_STATUS_SYNC_TIMEOUT).
+// Why no agent-scope release / acquire fences: the LLVM gfx950 model's release
+// (buffer_wbl2 sc1, a write-back of the XCD's whole L2, ~1.7-6.5 us) and acquire (buffer_inv sc1,
+// ~1.7 us) would cost more than a hand-off's payload at seven hand-offs per CMUX step.  The hand-off
+// instead takes the form MI355X_MICROARCH.md §"Workgroup dispatch, XCD placement & inter-workgroup
+// visibility" lists as valid without them (its "Valid forms" table, first row, and the Consumer
+// bullet's conditions 1-4): EVERY payload byte is stored sc1 (write-through past the producer's L2,
+// so the partner's XCD, wherever it is, reads it from memory) and loaded by a buffer sc1 load to
+// registers (L1-bypassing; no stale line of this CU's L1 can be hit); every storing wave drains its
+// stores (vmcnt(0)) before the workgroup barrier that precedes the one-lane flag store (sc1: an
+// agent-scope relaxed store); the consumer's polling wave sees the flag with an sc1 load, the other
+// waves load only after the barrier that wave joins; hipMalloc'd buffers, one workgroup per CU.  It
+// is the measured form, not an architectural guarantee; the tests compare every hand-off's result
+// bit for bit (test_generic_coop_kernel*, the N = 8192 rows in full).
 // Arithmetic: gen_fused_kernel's / gen_big_step_kernel's (same transforms, tau, key, rounding), so
 // the certified bound (generic_pbs_ok) holds unchanged; the tests compare bit for bit.
 // ------------------------------------------------------------------------------------------

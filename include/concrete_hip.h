@@ -228,6 +228,11 @@ void concrete_hip_set_spin_limit(uint32_t polls);
 /* The same bound for launches issued by the calling host thread only (0: the process-wide bound).
  * Test hook: forces the timeout path on one of several concurrent calls. */
 void concrete_hip_set_thread_spin_limit(uint32_t polls);
+/* How a cfg2-shaped call (k = 1, N = 1024, l = 3) of num_samples ciphertexts is split on a device of
+ * `cus` compute units (round 6): parts[0..2] = ciphertexts run on the pair kernel (4 per CU), the
+ * six-wave kernel at 2 per CU and at 1 per CU, in that launch order; returns the estimated time in
+ * 1/100 ms per round at n = 630 (concrete_amd/csrc/pbs1024_plan.hpp). */
+uint64_t concrete_hip_pbs1024_plan(uint64_t num_samples, uint32_t cus, uint32_t *parts);
 /* Status slots held by live streams of the device (round 6): a stream gets a slot on its first PBS
  * launch and returns it when it is destroyed (cuda_destroy_stream, the runtime's own streams), so a
  * caller that creates and destroys a stream per call (wrappers.cpp:129/160) never exhausts them. */

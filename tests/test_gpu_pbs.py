@@ -709,3 +709,56 @@ def test_status_is_per_stream(B, oracle, cfg2, torch_cuda):
     assert np.array_equal(got[rows], run_oracle(oracle, cfg2, cts[1][rows], acc))
     dec = B.lwe_decrypt(cfg2.glwe_sk, got, cfg2.p.big_n)
     assert [B.decode(d, width) for d in dec] == [int(table[m]) for m in msgs[1]]
+
+
+@pytest.mark.parametrize("shape", ["pair+hex1", "pair+hex2", "hex2", "hex1", "pair"])
+@pytest.mark.parametrize("indexed", [False, True])
+def test_pbs_split_over_kernels(B, oracle, torch_cuda, monkeypatch, shape, indexed):
+    """a cfg2-shaped call between round sizes is cut into contiguous parts run by
+    the pair kernel, the six-wave kernel at 2 and at 1 ciphertext per workgroup
+    (concrete_amd/csrc/pbs1024_plan.hpp), back to back on the caller's stream.  Ragged batches chosen
+    so the plan holds each combination of parts (batch sizes relative to the device's CU count);
+    with and without permuted index arrays and per-sample LUTs, every row equals the single-kernel
+    run (the pair kernel forced) and sampled rows equal the oracle."""
+    from concrete_amd import _native
+    L = _native.lib()
+    cus = torch_cuda.cuda.get_device_properties(0).multi_processor_count
+    nb = {"pair+hex1": 4 * cus + cus // 2 + 3, "pair+hex2": 4 * cus + cus + 7, "hex2": cus + 3, "hex1": 5,
+          "pair": 4 * cus - 9}[shape]
+    parts = (C.c_uint32 * 3)()
+    L.concrete_hip_pbs1024_plan(nb, cus, parts)
+    got_parts = [x > 0 for x in parts]
+    assert got_parts == [s in shape.split("+") for s in ("pair", "hex2", "hex1")], (shape, list(parts))
+    p = replace(B.CFG2, n=12)
+    S = Setup(B, oracle, torch_cuda, p, 6100 + nb)
+    width = 2
+    rng = np.random.RandomState(nb)
+    msgs = rng.randint(0, 4, size=nb)
+    cts = encrypt(B, S, msgs, width, 6200 + nb, std=2.0 ** -25)
+    ntab = 5 if indexed else 1
+    tables = [rng.randint(0, 4, size=4) for _ in range(ntab)]
+    accs = np.stack([lut_acc(B, S, t, width) for t in tables])
+    dev = "cuda:0"
+    kw = {}
+    if indexed:
+        in_idx = rng.permutation(nb).astype(np.uint64)
+        out_idx = rng.permutation(nb).astype(np.uint64)
+        lut_idx = rng.randint(0, ntab, size=nb).astype(np.uint64)
+        kw = dict(in_idx=B.to_device(in_idx, dev), out_idx=B.to_device(out_idx, dev),
+                  lut_idx=B.to_device(lut_idx, dev))
+    d_in, d_acc = B.to_device(cts, dev), B.to_device(accs, dev)
+    split = B.to_host(B.pbs(p, S.fbsk, d_in, d_acc, **kw))
+    monkeypatch.setenv("CONCRETE_HIP_PBS_PAIRS", "4")
+    single = B.to_host(B.pbs(p, S.fbsk, d_in, d_acc, **kw))
+    torch_cuda.cuda.synchronize()
+    assert np.array_equal(split, single)
+    rows = np.unique(np.array([0, 1, nb // 3, nb // 2, nb - 2, nb - 1]))
+    if indexed:
+        src = np.zeros(nb, dtype=np.int64)
+        src[out_idx.astype(np.int64)] = in_idx.astype(np.int64)  # output row -> input row
+        lut_of = np.zeros(nb, dtype=np.uint64)
+        lut_of[out_idx.astype(np.int64)] = lut_idx
+        ref, _ = oracle.pbs_batch(S.op, cts[src[rows]], accs, fbsk=S.fbsk_cpu, lut_idx=lut_of[rows])
+    else:
+        ref, _ = oracle.pbs_batch(S.op, cts[rows], accs, fbsk=S.fbsk_cpu)
+    assert np.array_equal(split[rows], ref)

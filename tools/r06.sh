@@ -1,0 +1,54 @@
+#!/bin/bash
+# Round-6 GPU evidence.  Usage: tools/r06.sh TAG PART
+#   sweep: the split tests, then the cfg2 batch sweep (tools/batch_sweep.py)
+#   suite: the whole GPU suite, smoke() and the default bench line
+#   prof:  kernel-trace stats + PMC records (cfg2 at 4096 and 512, cfg4)
+#   ks:    the keyswitch secondary: trace + PMC passes (int8 MFMA ops, L2 bytes)
+#   opt:   bench lines + PMC records of opt9 / opt10
+TAG=${1:-r06}
+PART=${2:-sweep}
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+( while sleep 30; do date +%T >> $O/heartbeat_$PART.log; done ) &
+HB=$!
+trap "kill $HB" EXIT
+step() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name $(date +%T)"
+  timeout -k 10 $to "$@" > $O/$name.log 2>&1
+  local rc=$?
+  echo "   rc=$rc"
+  tail -3 $O/$name.log | cut -c1-400
+  case $rc in 124|134|137|139) echo "stopping after $name (rc $rc)"; exit $rc;; esac
+  return 0
+}
+export TMPDIR=/tmp
+prof() {  # config passes batch-args [pmc timeout] [suffix]
+  local C=$1 P=$2 BA=$3 T=${4:-240}
+  cd /tmp
+  step trace_$C$5 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$C$5 -o run -- \
+    python3 $R/bench.py --config $C --steps 3 --warmup 1 --no-cpu-baseline --verify 0 --no-ks --no-e2e --no-sdfg --no-share $BA
+  cd $R
+  PMC_TIMEOUT=$T step pmc_$C$5 $((T * 4 + 60)) bash tools/pmc.sh $TAG/$C$5 $P --config $C --no-ks --no-sdfg $BA
+}
+case $PART in
+sweep)
+  step pytest_split 400 python -u -m pytest tests/test_gpu_pbs.py -v --timeout 200 --timeout-method thread -k "split or hex or pair or status"
+  step batch_sweep 600 python -u tools/batch_sweep.py --out $O/batch_sweep.json
+  ;;
+suite)
+  step pytest_gpu 1000 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread
+  step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+  step bench_default 400 python -u bench.py
+  ;;
+prof)
+  prof cfg2 bde ""
+  prof cfg2 bde "--global-batch 512" 240 _b512
+  prof cfg4 bde ""
+  ;;
+*)
+  echo "unknown part $PART"; exit 2
+  ;;
+esac

@@ -28,6 +28,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # The issue rate measured on gfx950 (~5 cycles per f64 wave-instruction per SIMD)
 # puts the reachable ceiling near 256 CU x 4 SIMD x 64 lanes x 2 flop / 5 cycles x 2.4 GHz = 63 TFLOP/s.
 FP64_PEAK_TFS = 78.6
+# int8 matrix cores: v_mfma_i32_32x32x32_i8 runs the cycles of the BF16 form of the same M x N at twice
+# the K, i.e. 2x the dense BF16 rate (MI355X_MICROARCH.md, Matrix cores: ~2.5 PF dense BF16)
+I8_PEAK_TOPS = 5000.0
 METRIC = "PBS/sec (whole node) at N=1024 batch=4096; achieved HBM GB/s"
 
 
@@ -119,6 +122,21 @@ def pmc_f64_flop(batch: int, config: str, cus: int = 256):
             scale = batch / rec["batch"]
             return rec["f64_flop"] * scale, rec["src"] + f" (scaled from batch {rec['batch']}, same kernel)"
     return None, None
+
+
+def pmc_ks_record(batch: int, config: str):
+    """The keyswitch's PMC record at this batch (tools/pmc_record.py on the ks_mfma kernel): L2 (TCC)
+    requests and HBM bytes per launch of the matrix-core kernel; None without one."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_ks_pmc.json")), reverse=True):
+        with open(f) as fh:
+            rec = json.load(fh)
+        if rec.get("batch") == batch and rec.get("config") == config + "_ks":
+            out = {k: rec[k] for k in ("kernel", "traffic_bytes", "l2_bytes", "l2_read_requests", "l2_hit", "i8_ops",
+                                       "mfma_busy") if k in rec}
+            out["src"] = os.path.relpath(f, ROOT)
+            return out
+    return None
 
 
 def host_cpus():
@@ -374,13 +392,24 @@ def main():
         ks_launch_bytes = 8 * (p.ksk_len + args.batch * (p.lwe_out_size + p.lwe_in_size))
         ks_rate = args.batch / (ks_ms * 1e-3)
         ks_gbs = ks_launch_bytes / (ks_ms * 1e-3) / 1e9
+        # the keyswitch as int8 matrix products: out = (0..b) - sum_c 2^(8c) D K_c over the
+        # 8 byte chunks of every KSK word, D the batch x (kN l) digit matrix: 2 ops per multiply-add
+        ks_ops = 2.0 * 8 * args.batch * (p.big_n * p.ks_level) * (p.n + 1)
+        ks_ks = pmc_ks_record(args.batch, args.config)
+        ks_mfma = {"achieved": round(ks_ops / (ks_ms * 1e-3) / 1e12, 1), "peak": I8_PEAK_TOPS, "unit": "TOP/s",
+                   "frac": round(ks_ops / (ks_ms * 1e-3) / 1e12 / I8_PEAK_TOPS, 4), "ops_per_call": ks_ops,
+                   "note": "algorithmic int8 multiply-adds x 2 (8 byte chunks x batch x kN l x (n + 1)) / the whole "
+                           "call's time (digit kernel + matrix-core kernel); peak = 2x dense BF16 (I8 MFMA rate)"}
+        if ks_ks:
+            ks_mfma["pmc"] = ks_ks
         ks_res = {"metric": f"KS/sec per GPU at kN={p.big_n} -> n={p.n}, l={p.ks_level} logB={p.ks_base_log}",
                   "value": round(ks_rate, 1), "unit": "KS/s", "kernel_ms": round(ks_ms, 4),
                   # not HBM-bound: the unique bytes per launch are a small fraction of the peak, so
                   # no HBM fraction is claimed
                   "hbm": {"achieved": round(ks_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "bytes_per_launch": ks_launch_bytes, "bytes_per_ks_8d": ks_bytes,
-                          "note": "unique bytes per launch (the KSK once + every row in and out)"}}
+                          "note": "unique bytes per launch (the KSK once + every row in and out)"},
+                  "bound": "mfma", "mfma": ks_mfma}
         if rank == 0 and args.verify:
             from oracle import pyoracle as O
             op = O.Params(n=p.n, k=p.k, N=p.N, l=p.level, logB=p.base_log, ks_l=p.ks_level, ks_logB=p.ks_base_log)

@@ -333,9 +333,10 @@ const void* generic_companion_key(const void* primary, uint32_t n, uint32_t k, u
     CHIP_CHECK(hipMemcpyAsync(tmp, e.src, std_bytes, hipMemcpyHostToDevice, s));
     src_dev = (const uint64_t*)tmp;
   }
-  ConvertArgs a{s, d, src_dev, n, k, level, N, generic_key_format(k, N, level).limbs};
+  ConvertArgs a{s, d, src_dev, n, k, level, N, generic_key_format(k, N, level).limbs, key_spectrum_sink(s)};
   int rc = convert_bsk_generic_launch(a);
-  if (rc == 0) rc = key_spectrum_record(s, d, generic_key_format(k, N, level), n, k, N, level);
+  const int rs = key_spectrum_record(s, rc == 0 ? d : nullptr, generic_key_format(k, N, level), n, k, N, level, a.smax);
+  if (rc == 0) rc = rs;
   CHIP_CHECK(hipStreamSynchronize(s));
   if (tmp) CHIP_CHECK(hipFree(tmp));
   if (rc != 0) {
@@ -546,12 +547,14 @@ int concrete_hip_convert_bsk(void* stream, uint32_t gpu_index, void* dest_fourie
     src_dev = (const uint64_t*)tmp;
   }
   ConvertArgs a{s, dest_fourier, src_dev, input_lwe_dim, glwe_dim, level_count, polynomial_size,
-                default_limbs(glwe_dim, polynomial_size, level_count)};
+                default_limbs(glwe_dim, polynomial_size, level_count), key_spectrum_sink(s)};
   int rc = convert_bsk_launch(a);
   // the key's measured spectrum against the certified bound (keycheck.hip; synchronises s, as the
   // reference does after its conversion, context.h:110-113)
-  if (rc == 0) rc = key_spectrum_record(s, dest_fourier, key_format(glwe_dim, polynomial_size, level_count),
-                                        input_lwe_dim, glwe_dim, polynomial_size, level_count);
+  const int rs = key_spectrum_record(s, rc == 0 ? dest_fourier : nullptr,
+                                     key_format(glwe_dim, polynomial_size, level_count), input_lwe_dim, glwe_dim,
+                                     polynomial_size, level_count, a.smax);
+  if (rc == 0) rc = rs;
   else key_spectrum_forget(dest_fourier);
   if (tmp) CHIP_CHECK(hipFreeAsync(tmp, s));
   return rc;
@@ -657,9 +660,12 @@ int concrete_hip_convert_bsk_generic(void* stream, uint32_t gpu_index, void* des
     CHIP_CHECK(hipMemcpyAsync(tmp, src, std_bytes, hipMemcpyHostToDevice, s));
     src_dev = (const uint64_t*)tmp;
   }
-  ConvertArgs a{s, dest, src_dev, input_lwe_dim, glwe_dim, level_count, polynomial_size, f.limbs};
+  ConvertArgs a{s, dest, src_dev, input_lwe_dim, glwe_dim, level_count, polynomial_size, f.limbs,
+                key_spectrum_sink(s)};
   int rc = convert_bsk_generic_launch(a);
-  if (rc == 0) rc = key_spectrum_record(s, dest, f, input_lwe_dim, glwe_dim, polynomial_size, level_count);
+  const int rs = key_spectrum_record(s, rc == 0 ? dest : nullptr, f, input_lwe_dim, glwe_dim, polynomial_size,
+                                     level_count, a.smax);
+  if (rc == 0) rc = rs;
   else key_spectrum_forget(dest);
   if (tmp) CHIP_CHECK(hipFreeAsync(tmp, s));
   return rc;

@@ -18,6 +18,7 @@
 
 #include "common.hpp"
 #include "fft512.hpp"
+#include "keycheck.hpp"
 #include "pbs.hpp"
 
 namespace chip {
@@ -96,22 +97,27 @@ __device__ __forceinline__ void dd_fft(ddc* buf, const ddc* __restrict__ tw_t) {
 // dd_fft, then the scatter into the PBS kernels' register layout: element e = (slot, lane) holds
 // frequency fft512_freq(lane, slot), scaled 1/M, stored at dst(e).
 template <int M, class Dst>
-__device__ __forceinline__ void dd_fft_scatter(ddc* buf, const ddc* __restrict__ tw_t, Dst dst) {
+__device__ __forceinline__ void dd_fft_scatter(ddc* buf, const ddc* __restrict__ tw_t, Dst dst,
+                                               unsigned long long* smax) {
   dd_fft<M>(buf, tw_t);
   const double scale = 1.0 / (double)M;
+  double m2 = 0.0;
   for (int e = threadIdx.x; e < M; e += blockDim.x) {
     const int lane = e & 63, slot = e >> 6;
     const int f = fft512_freq(lane, slot);
     const ddc x = buf[f];
-    *dst(e) = {(x.re.hi + x.re.lo) * scale, (x.im.hi + x.im.lo) * scale};
+    const cplx y = {(x.re.hi + x.re.lo) * scale, (x.im.hi + x.im.lo) * scale};
+    *dst(e) = y;
+    m2 = fmax(m2, spec_mag2(y.re, y.im));
   }
+  spec_max_commit(smax, m2);
 }
 
 // tables: zeta[j] = exp(i pi j / N) for j < N/2 ; tw[t] = exp(-2 pi i t / (N/2)) for t < N/4
 template <int N, int K, int L, int LIMBS>
 __global__ void __launch_bounds__(256) convert_bsk_kernel(cplx* __restrict__ dest, const uint64_t* __restrict__ src,
                                                          const ddc* __restrict__ zeta_t, const ddc* __restrict__ tw_t,
-                                                         uint32_t n) {
+                                                         uint32_t n, unsigned long long* smax) {
   constexpr int M = N / 2, LOGM = (M == 512 ? 9 : (M == 1024 ? 10 : (M == 256 ? 8 : 11)));
   constexpr int K1 = K + 1;
   __shared__ ddc buf[M];
@@ -143,7 +149,7 @@ __global__ void __launch_bounds__(256) convert_bsk_kernel(cplx* __restrict__ des
     const int slot = e >> 6, lane = e & 63;
     const uint32_t co = slot < 4 ? col : 1u - col, ro = slot < 4 ? row : 1u - row;
     return base + (((uint64_t)(limb * 2 + co) * 2 + ro) * L + q) * M + slot * 64 + lane;
-  });
+  }, smax);
 }
 
 // N = 2048, k = 1, l = 1 (pbs2048.hip).  Block = (i, limb, col, row, parity), in the order of
@@ -160,7 +166,8 @@ template <int LIMBS>
 __global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__ dest, const uint64_t* __restrict__ src,
                                                              const ddc* __restrict__ zeta_t,
                                                              const ddc* __restrict__ tw_t,
-                                                             const ddc* __restrict__ sroot_t, uint32_t level) {
+                                                             const ddc* __restrict__ sroot_t, uint32_t level,
+                                                             unsigned long long* smax) {
   constexpr int M = 512, LOGM = 9;
   __shared__ ddc buf[2][M];
   const uint64_t blk = blockIdx.x;
@@ -183,22 +190,27 @@ __global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__
   dd_fft<M>(buf[1], tw_t);
   const double scale = 0.5 / (double)M;
   cplx* base = dest + blk * 2 * M;
+  double m2 = 0.0;
   for (int e = threadIdx.x; e < M; e += blockDim.x) {
     const int f = fft512_freq(e & 63, e >> 6);
     const ddc so = ddc_mul(buf[1][f], sroot_t[f]);
     const ddc ge = buf[0][f];
     const ddc kp{dd_add(ge.re, so.re), dd_add(ge.im, so.im)};
     const ddc km{dd_add(ge.re, dd_neg(so.re)), dd_add(ge.im, dd_neg(so.im))};
-    base[e] = {(kp.re.hi + kp.re.lo) * scale, (kp.im.hi + kp.im.lo) * scale};
-    base[M + e] = {(km.re.hi + km.re.lo) * scale, (km.im.hi + km.im.lo) * scale};
+    const cplx yp = {(kp.re.hi + kp.re.lo) * scale, (kp.im.hi + kp.im.lo) * scale};
+    const cplx ym = {(km.re.hi + km.re.lo) * scale, (km.im.hi + km.im.lo) * scale};
+    base[e] = yp;
+    base[M + e] = ym;
+    m2 = fmax(m2, fmax(spec_mag2(yp.re, yp.im), spec_mag2(ym.re, ym.im)));
   }
+  spec_max_commit(smax, m2);
 }
 #else
 template <int LIMBS>
 __global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__ dest, const uint64_t* __restrict__ src,
                                                              const ddc* __restrict__ zeta_t,
                                                              const ddc* __restrict__ tw_t, const ddc* __restrict__,
-                                                             uint32_t level) {
+                                                             uint32_t level, unsigned long long* smax) {
   constexpr int M = 512, LOGM = 9;
   __shared__ ddc buf[M];
   const uint64_t blk = blockIdx.x;
@@ -217,7 +229,7 @@ __global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__
     buf[r] = z;
   }
   __syncthreads();
-  dd_fft_scatter<M>(buf, tw_t, [&](int e) { return dest + blk * M + e; });
+  dd_fft_scatter<M>(buf, tw_t, [&](int e) { return dest + blk * M + e; }, smax);
 }
 #endif
 
@@ -227,7 +239,8 @@ __global__ void __launch_bounds__(256) convert_bsk2048_kernel(cplx* __restrict__
 __global__ void __launch_bounds__(256) convert_bsk1024k2_kernel(cplx* __restrict__ dest,
                                                                const uint64_t* __restrict__ src,
                                                                const ddc* __restrict__ zeta_t,
-                                                               const ddc* __restrict__ tw_t, uint32_t level) {
+                                                               const ddc* __restrict__ tw_t, uint32_t level,
+                                                               unsigned long long* smax) {
   constexpr int M = 512, LOGM = 9, N = 1024;
   __shared__ ddc buf[M];
   const uint64_t blk = blockIdx.x;
@@ -254,7 +267,7 @@ __global__ void __launch_bounds__(256) convert_bsk1024k2_kernel(cplx* __restrict
     buf[r] = z;
   }
   __syncthreads();
-  dd_fft_scatter<M>(buf, tw_t, [&](int e) { return dest + blk * M + e; });
+  dd_fft_scatter<M>(buf, tw_t, [&](int e) { return dest + blk * M + e; }, smax);
 }
 
 // N = 512, k = 3 / N = 256, k = 5, 6, l <= 3 (pbs_small.hip) and N = 512, k = 4, l = 1, 3 .. 5
@@ -268,7 +281,8 @@ template <int N, int K1, int LIMBS = SM_LIMBS>
 __global__ void __launch_bounds__(256) convert_bsk_small_kernel(cplx* __restrict__ dest,
                                                                const uint64_t* __restrict__ src,
                                                                const ddc* __restrict__ zeta_t,
-                                                               const ddc* __restrict__ tw_t, uint32_t level) {
+                                                               const ddc* __restrict__ tw_t, uint32_t level,
+                                                               unsigned long long* smax) {
   constexpr int M = N / 2, LOGM = N == 512 ? 8 : 7, P = 1024 / N;
   constexpr int GC = sm_gc(N, K1), NCG = K1 / GC;
   __shared__ ddc buf[M];
@@ -307,17 +321,21 @@ __global__ void __launch_bounds__(256) convert_bsk_small_kernel(cplx* __restrict
   __syncthreads();
   dd_fft<M>(buf, tw_t);
   const double scale = 1.0 / (512.0 * P);
+  double m2 = 0.0;
   for (int e = threadIdx.x; e < M; e += blockDim.x) {
     const ddc x = buf[fft512_freq(e & 63, e >> 6)];
-    dest[blk * M + e] = {(x.re.hi + x.re.lo) * scale, (x.im.hi + x.im.lo) * scale};
+    const cplx y = {(x.re.hi + x.re.lo) * scale, (x.im.hi + x.im.lo) * scale};
+    dest[blk * M + e] = y;
+    m2 = fmax(m2, spec_mag2(y.re, y.im));
   }
+  spec_max_commit(smax, m2);
 }
 
 template <int N, int K, int L, int LIMBS>
 static int launch_convert(const ConvertArgs& a, const ddc* zeta, const ddc* tw) {
   const uint64_t blocks = (uint64_t)a.n * L * (K + 1) * (K + 1) * LIMBS;
   hipLaunchKernelGGL((convert_bsk_kernel<N, K, L, LIMBS>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
-                     reinterpret_cast<cplx*>(a.dest), a.src_dev, zeta, tw, a.n);
+                     reinterpret_cast<cplx*>(a.dest), a.src_dev, zeta, tw, a.n, a.smax);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("convert launch failed: %s", hipGetErrorString(e));
@@ -391,7 +409,7 @@ int convert_bsk_launch(const ConvertArgs& a) {
     CHIP_CHECK(hipMemcpyAsync(ds, sr.data(), sr.size() * sizeof(ddc), hipMemcpyHostToDevice, a.stream));
     const uint64_t blocks = (uint64_t)a.n * PBS2_LIMBS * 4 * a.level * (P2_PM ? 1 : 2);
     hipLaunchKernelGGL((convert_bsk2048_kernel<PBS2_LIMBS>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
-                       reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, ds, a.level);
+                       reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, ds, a.level, a.smax);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       set_error("convert launch failed: %s", hipGetErrorString(e));
@@ -401,19 +419,19 @@ int convert_bsk_launch(const ConvertArgs& a) {
     const uint64_t blocks = (uint64_t)a.n * a.limbs * (a.k + 1) * (a.k + 1) * a.level;
     if (a.N == 512 && a.k == 3)
       hipLaunchKernelGGL((convert_bsk_small_kernel<512, 4>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
-                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level);
+                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level, a.smax);
     else if (a.N == 512 && a.limbs == K4_L2_LIMBS)
       hipLaunchKernelGGL((convert_bsk_small_kernel<512, 5, K4_L2_LIMBS>), dim3((uint32_t)blocks), dim3(256), 0,
-                         a.stream, reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level);
+                         a.stream, reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level, a.smax);
     else if (a.N == 512)
       hipLaunchKernelGGL((convert_bsk_small_kernel<512, 5>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
-                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level);
+                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level, a.smax);
     else if (a.k == 5)
       hipLaunchKernelGGL((convert_bsk_small_kernel<256, 6>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
-                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level);
+                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level, a.smax);
     else
       hipLaunchKernelGGL((convert_bsk_small_kernel<256, 7>), dim3((uint32_t)blocks), dim3(256), 0, a.stream,
-                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level);
+                         reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level, a.smax);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       set_error("convert launch failed: %s", hipGetErrorString(e));
@@ -422,7 +440,7 @@ int convert_bsk_launch(const ConvertArgs& a) {
   } else if (k2) {
     const uint64_t blocks = (uint64_t)a.n * K2_LIMBS * 9 * a.level;
     hipLaunchKernelGGL(convert_bsk1024k2_kernel, dim3((uint32_t)blocks), dim3(256), 0, a.stream,
-                       reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level);
+                       reinterpret_cast<cplx*>(a.dest), a.src_dev, dz, dt, a.level, a.smax);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       set_error("convert launch failed: %s", hipGetErrorString(e));

@@ -42,11 +42,12 @@ const void* generic_companion_key(const void* primary, uint32_t n, uint32_t k, u
                                   hipStream_t s);
 
 // keycheck.hip: the exactness gate against the converted key's measured spectrum (round 6).
-// key_spectrum_record reduces max|G| of the key just converted into `dest` on s (synchronises s),
-// records it, and returns -2 when no base_log could use the key exactly; key_bound_check returns -2
+// key_spectrum_record reads the max|G| the conversion kernels left in the sink (synchronises s),
+// records it for `dest`, and returns -2 when no base_log could use the key exactly; key_bound_check returns -2
 // (message set) when the PBS on `key` at logB would not be certified exact (0 without a record).
+unsigned long long* key_spectrum_sink(hipStream_t s);  // zeroed sink for ConvertArgs::smax
 int key_spectrum_record(hipStream_t s, const void* dest, const KeyFormat& f, uint32_t n, uint32_t k, uint32_t N,
-                        uint32_t level);
+                        uint32_t level, unsigned long long* sink);
 int key_bound_check(const void* key, KeyKind kind, uint32_t k, uint32_t N, uint32_t level, uint32_t logB);
 void key_spectrum_copy(const void* dest, const void* src);
 void key_spectrum_forget(const void* key);

@@ -7,9 +7,9 @@
 // max|G| of random-looking keys; an imported key whose spectra are larger (a crafted or degenerate
 // key: constant-coefficient rows reach 8x the random-key value at N = 1024) would round some
 // coefficient the wrong way without any error.  So every conversion (concrete_hip_convert_bsk, the
-// general-format conversions and companions) reduces max|G| over the converted key once — one read
-// pass over the Fourier key, beside the conversion's own transforms — and records it with the key's
-// device address.  Each PBS call then evaluates the certified bound of its kernel for its actual
+// general-format conversions and companions) has its conversion kernels reduce max|G| over the
+// values they store (keycheck.hpp: free beside the transforms, no extra pass over the key) and
+// records it with the key's device address.  Each PBS call then evaluates the certified bound of its kernel for its actual
 // base_log with that max|G| and refuses (-2) when it reaches 1/2 (concrete_hip_pbs: a hand-tuned
 // kernel's key that fails first tries the general path's companion, whose narrower limbs give a
 // smaller bound).  A key the backend did not convert (copied in by the caller) has no record and
@@ -26,30 +26,12 @@
 
 #include "common.hpp"
 #include "companion.hpp"
+#include "keycheck.hpp"
 #include "pbs.hpp"
 
 namespace chip {
 
 void keep_pool_memory();  // abi.hip
-
-// max over complex values of |z| (f64 bit pattern of a non-negative double orders as u64)
-__global__ void __launch_bounds__(256) spectrum_max_kernel(const double2* __restrict__ key, uint64_t count,
-                                                           unsigned long long* __restrict__ out) {
-  double m = 0.0;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
-    const double2 z = key[i];
-    m = fmax(m, hypot(z.x, z.y));
-  }
-  for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
-  __shared__ double part[4];
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    m = fmax(fmax(part[0], part[1]), fmax(part[2], part[3]));
-    atomicMax(out, (unsigned long long)__double_as_longlong(m));
-  }
-}
 
 // scale of the stored spectra (the kernels' inverse normalisation folded into the key)
 static double stored_scale(const KeyFormat& f, uint32_t N) {
@@ -120,36 +102,39 @@ double certified_bound(KeyKind kind, uint32_t k, uint32_t N, uint32_t level, uin
   }
 }
 
-// Reduce max|G| over the Fourier key just converted on s into `dest` (format f of (k, N, l)), wait for
-// it, record it, and refuse (-2) a key that no base_log could use exactly.
-int key_spectrum_record(hipStream_t s, const void* dest, const KeyFormat& f, uint32_t n, uint32_t k, uint32_t N,
-                        uint32_t level) {
-  const uint64_t bytes = f.kind == KeyKind::GENERIC ? generic_fourier_bsk_bytes(n, k, level, N)
-                                                    : fourier_bsk_bytes(n, k, level, N);
-  if (!bytes || !dest) return 0;
-  static thread_local unsigned long long* landing = nullptr;  // page-locked result word of this thread
-  if (!landing) CHIP_CHECK(hipHostMalloc((void**)&landing, sizeof(unsigned long long), hipHostMallocDefault));
+// A zeroed sink for the conversion kernels' max |G|^2 (keycheck.hpp), stream-ordered.
+unsigned long long* key_spectrum_sink(hipStream_t s) {
   unsigned long long* d = nullptr;
   keep_pool_memory();
-  CHIP_CHECK(hipMallocAsync((void**)&d, sizeof(unsigned long long), s));
-  CHIP_CHECK(hipMemsetAsync(d, 0, sizeof(unsigned long long), s));
-  const uint64_t count = bytes / 16;
-  int cus = 256;
-  int dev = 0;
-  CHIP_CHECK(hipGetDevice(&dev));
-  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const uint64_t want = (count + 255) / 256;
-  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus * 8));
-  spectrum_max_kernel<<<grid, 256, 0, s>>>((const double2*)dest, count, d);
-  CHIP_CHECK(hipGetLastError());
-  CHIP_CHECK(hipMemcpyAsync(landing, d, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-  CHIP_CHECK(hipFreeAsync(d, s));
+  CHIP_CHECK(hipMallocAsync((void**)&d, SPEC_SINK_WORDS * sizeof(unsigned long long), s));
+  CHIP_CHECK(hipMemsetAsync(d, 0, SPEC_SINK_WORDS * sizeof(unsigned long long), s));
+  return d;
+}
+
+// The key just converted on s into `dest` (format f of (k, N, l)) left max |G|^2 in `sink` (the
+// conversion kernels reduce it as they store the key: no pass of its own): wait for it, record
+// max |G|, free the sink, and refuse (-2) a key that no base_log could use exactly.
+int key_spectrum_record(hipStream_t s, const void* dest, const KeyFormat& f, uint32_t n, uint32_t k, uint32_t N,
+                        uint32_t level, unsigned long long* sink) {
+  (void)n;
+  if (!sink) return 0;
+  static thread_local unsigned long long* landing = nullptr;  // page-locked words of this thread
+  if (!landing)
+    CHIP_CHECK(hipHostMalloc((void**)&landing, SPEC_SINK_WORDS * sizeof(unsigned long long), hipHostMallocDefault));
+  CHIP_CHECK(hipMemcpyAsync(landing, sink, SPEC_SINK_WORDS * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  CHIP_CHECK(hipFreeAsync(sink, s));
   CHIP_CHECK(hipStreamSynchronize(s));
-  double stored;
-  const unsigned long long bits = *landing;
-  memcpy(&stored, &bits, sizeof stored);
-  // |z| from hypot is within 1 ulp; the margin keeps the recorded value an upper bound
-  const double maxG = stored * stored_scale(f, N) * (1.0 + std::ldexp(1.0, -50));
+  double m2 = 0.0;
+  for (int w = 0; w < SPEC_SINK_WORDS; ++w) {
+    double x;
+    const unsigned long long bits = landing[w];
+    memcpy(&x, &bits, sizeof x);
+    m2 = std::max(m2, x);
+  }
+  // |z|^2 by one FMA and a product is within 2u of the exact square (a relative 1u on |z|); the
+  // margin keeps the recorded value an upper bound of the stored key's largest magnitude
+  const double maxG = std::sqrt(m2) * stored_scale(f, N) * (1.0 + std::ldexp(1.0, -48));
+  if (!dest) return 0;
   {
     std::lock_guard<std::mutex> g(g_spec_mu);
     g_spec[dest] = SpecRec{maxG, f.kind, k, N, level, f.bits};

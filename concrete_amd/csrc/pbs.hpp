@@ -252,6 +252,7 @@ struct ConvertArgs {
   void* dest;               // Fourier key, fourier_bsk_bytes()
   const uint64_t* src_dev;  // standard-domain key on the device [n][l][k+1][k+1][N]
   uint32_t n, k, level, N, limbs;
+  unsigned long long* smax = nullptr;  // keycheck.hpp sink: max |G|^2 of the stored key (or none)
 };
 int convert_bsk_launch(const ConvertArgs& a);
 int convert_bsk_generic_launch(const ConvertArgs& a);  // pbs_generic.hip

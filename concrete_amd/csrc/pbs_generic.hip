@@ -35,6 +35,7 @@
 #include "common.hpp"
 #include "fft512.hpp"
 #include "kernel_util.hpp"
+#include "keycheck.hpp"
 #include "pbs.hpp"
 #include "companion.hpp"
 
@@ -1332,6 +1333,7 @@ struct SplitConvArgs {
   cplx* dest;           // Fourier key [i][c][lim][r][q][M]
   uint64_t poly0;       // first standard polynomial of this batch
   uint32_t polys, k, level, bits, limbs;
+  unsigned long long* smax;  // keycheck.hpp sink (or nullptr)
 };
 
 template <int S>
@@ -1403,6 +1405,7 @@ __global__ void __launch_bounds__(256) gen_split_combine_kernel(SplitConvArgs a)
   const uint64_t total = (uint64_t)a.polys * a.limbs * M;
   const uint32_t K1 = a.k + 1;
   const double scale = 1.0 / (double)M;
+  double m2 = 0.0;  // max |G|^2 of the stored values (keycheck.hpp)
   for (uint64_t gi = blockIdx.x * 256ull + threadIdx.x; gi < total; gi += (uint64_t)gridDim.x * 256) {
     const uint32_t p = (uint32_t)(gi % M);
     const uint64_t item = gi / M;
@@ -1423,7 +1426,9 @@ __global__ void __launch_bounds__(256) gen_split_combine_kernel(SplitConvArgs a)
     const uint64_t i = sp / a.level;
     const uint32_t qq = a.level - 1 - v;
     a.dest[((((i * K1 + c) * a.limbs + lim) * K1 + r) * a.level + qq) * (uint64_t)M + p] = {x.re * scale, x.im * scale};
+    m2 = fmax(m2, spec_mag2(x.re * scale, x.im * scale));
   }
+  spec_max_commit(a.smax, m2);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2570,7 +2575,7 @@ __global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, c
                                                                         const cplx* Wlo,
                                                                         const cplx* Whi, const cplx* Z, uint32_t k,
                                                                         uint32_t level, uint32_t bits, uint32_t limbs,
-                                                                        uint32_t perm) {
+                                                                        uint32_t perm, unsigned long long* smax) {
   constexpr int N = 2 * M, TH = Geo<M>::THREADS, VPT = Geo<M>::VPT;
   constexpr bool PP = M <= 4096;  // as gen_step_kernel
   __shared__ cplx buf[M + (PP ? tile_tw_entries<M, TH>() : tw_entries<M>())];
@@ -2596,6 +2601,7 @@ __global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, c
 #pragma unroll
   for (int e = 0; e < 2 * VPT; ++e) gv[e] = g[tid + (e % VPT) * TH + (e / VPT) * M];
   const double scale = 1.0 / (double)M;
+  double m2 = 0.0;  // max |G|^2 of the stored values (keycheck.hpp)
 #pragma unroll 1
   for (uint32_t lim = 0; lim < limbs; ++lim) {
     // balanced limbs: g = sum_j 2^{jb} g_j mod 2^64, |g_j| <= 2^(b-1); the top limb only matters
@@ -2623,9 +2629,11 @@ __global__ void __launch_bounds__(Geo<M>::THREADS) gen_convert_kernel(cplx* G, c
       const uint32_t p = tid + e * TH;
       const cplx x = buf[sw(perm ? (int)big_freq(p) : (int)p)];
       dst[p] = {x.re * scale, x.im * scale};
+      m2 = fmax(m2, spec_mag2(x.re * scale, x.im * scale));
     }
     __syncthreads();
   }
+  spec_max_commit(smax, m2);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2927,7 +2935,7 @@ static int convert_split_launch(const ConvertArgs& a, const KeyFormat& fmt, cons
   for (uint64_t p0 = 0; p0 < polys; p0 += batch) {
     const uint32_t nb = (uint32_t)std::min<uint64_t>(batch, polys - p0);
     SplitConvArgs c{reinterpret_cast<cplx*>(scratch), a.src_dev, tb.Tau, tb.WR, reinterpret_cast<cplx*>(a.dest), p0,
-                    nb, a.k, a.level, fmt.bits, fmt.limbs};
+                    nb, a.k, a.level, fmt.bits, fmt.limbs, a.smax};
     hipLaunchKernelGGL((gen_split_convert_kernel<S>), dim3(nb * fmt.limbs * S), dim3(512), 0, a.stream, c);
     const uint64_t total = (uint64_t)nb * fmt.limbs * G::M;
     hipLaunchKernelGGL((gen_split_combine_kernel<S>), dim3((uint32_t)std::min<uint64_t>((total + 255) / 256, 65535)),
@@ -3121,7 +3129,7 @@ int convert_bsk_generic_launch(const ConvertArgs& a) {
 #define GEN_CONV(MM)                                                                                        \
   hipLaunchKernelGGL(gen_convert_kernel<MM>, dim3((uint32_t)blocks), dim3(Geo<MM>::THREADS), 0, a.stream, G, \
                      a.src_dev, tb.Wfull, tb.Wlo, tb.Whi, tb.Z, a.k, a.level, fmt.bits, fmt.limbs,        \
-                     four_step(a.N) ? 1u : 0u)
+                     four_step(a.N) ? 1u : 0u, a.smax)
   switch (a.N) {
     case 256: GEN_CONV(128); break;
     case 512: GEN_CONV(256); break;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes over one bench step (run on the GPU box from the repo root).
-# Usage: tools/pmc.sh TAG [PASSES]   PASSES = subset of "abcde" (default all; "de" = HBM traffic only)
+# Usage: tools/pmc.sh TAG [PASSES]   PASSES = subset of "abcdefg" (default abcde; "de" = HBM traffic only)
 set -e
 TAG=${1:-pmc}
 PASSES=${2:-abcde}
@@ -20,4 +20,7 @@ run() {  # name counters...
 [[ $PASSES == *c* ]] && run c SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_CVT SQ_LDS_ADDR_CONFLICT
 [[ $PASSES == *d* ]] && run d FETCH_SIZE
 [[ $PASSES == *e* ]] && run e WRITE_SIZE TCC_HIT TCC_MISS
+# matrix-core and L2 passes (the keyswitch's int8 MFMA kernel, round 6)
+[[ $PASSES == *f* ]] && run f SQ_INSTS_VALU_MFMA_MOPS_I8 SQ_INSTS_VALU_MFMA_I8 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE
+[[ $PASSES == *g* ]] && run g TCP_TCC_READ_REQ_sum TCC_REQ_sum TCC_HIT_sum TCC_MISS_sum
 echo pmc done

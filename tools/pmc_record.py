@@ -59,6 +59,18 @@ def main():
     if "SQ_INSTS_VALU_FMA_F64" in v:
         rec["f64_flop"] = 64.0 * (2 * v["SQ_INSTS_VALU_FMA_F64"] + v.get("SQ_INSTS_VALU_ADD_F64", 0.0)
                                   + v.get("SQ_INSTS_VALU_MUL_F64", 0.0))
+    # round 6: L2 and matrix-core passes (tools/pmc.sh f, g; the keyswitch's int8 MFMA kernel)
+    if "TCP_TCC_READ_REQ_sum" in v:
+        rec["l2_read_requests"] = v["TCP_TCC_READ_REQ_sum"]
+        rec["l2_bytes"] = int(round(v["TCP_TCC_READ_REQ_sum"] * 128))  # 128-B L1 -> L2 read requests
+    if "TCC_HIT_sum" in v and "TCC_MISS_sum" in v and v["TCC_HIT_sum"] + v["TCC_MISS_sum"] > 0:
+        rec["l2_hit"] = round(v["TCC_HIT_sum"] / (v["TCC_HIT_sum"] + v["TCC_MISS_sum"]), 4)
+    if "SQ_INSTS_VALU_MFMA_MOPS_I8" in v:
+        rec["i8_ops"] = v["SQ_INSTS_VALU_MFMA_MOPS_I8"] * 512.0
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in v and v.get("GRBM_GUI_ACTIVE"):
+        # rocprofv3's MfmaUtil: busy cycles summed over the 1,024 SIMDs / (GRBM_GUI_ACTIVE of one XCD
+        # (the collected value sums the 8 XCDs) x 1,024)
+        rec["mfma_busy"] = round(v["SQ_VALU_MFMA_BUSY_CYCLES"] / (v["GRBM_GUI_ACTIVE"] / 8 * 4 * 256), 4)
     json.dump(rec, open(dst, "w"), indent=1)
     print(json.dumps({k: rec[k] for k in rec if k != "counters"}))
 

@@ -48,6 +48,19 @@ prof)
   prof cfg2 bde "--global-batch 512" 240 _b512
   prof cfg4 bde ""
   ;;
+ks)
+  PMC_TIMEOUT=240 step pmc_ks 900 bash tools/pmc.sh $TAG/ks defg --no-sdfg --no-share
+  ;;
+list)
+  cd /tmp
+  step counters 120 rocprofv3 -L
+  ;;
+opt9)
+  CONCRETE_HIP_GEN_STREAMS=1 prof opt9 bde "--batch 1024" 500
+  ;;
+opt10)
+  CONCRETE_HIP_GEN_STREAMS=1 prof opt10 bde "--batch 512" 700
+  ;;
 *)
   echo "unknown part $PART"; exit 2
   ;;

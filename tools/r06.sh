@@ -51,6 +51,27 @@ prof)
 ks)
   PMC_TIMEOUT=240 step pmc_ks 900 bash tools/pmc.sh $TAG/ks defg --no-sdfg --no-share
   ;;
+optprof1)
+  for C in opt1 opt2 opt3 opt4 opt5 opt6; do prof $C bde ""; done
+  ;;
+optprof2)
+  CONCRETE_HIP_GEN_STREAMS=1 prof opt7 bde "--batch 1024" 400
+  CONCRETE_HIP_GEN_STREAMS=1 prof opt8 bde "--batch 1024" 500
+  CONCRETE_HIP_GEN_STREAMS=1 prof opt9 bde "--batch 1024" 500
+  CONCRETE_HIP_GEN_STREAMS=1 prof opt10 bde "--batch 512" 700
+  ;;
+bench1)
+  for C in cfg4 opt1 opt2 opt3 opt4 opt5 opt6; do
+    step bench_$C 400 python -u bench.py --config $C --verify 2 --no-e2e --no-sdfg
+  done
+  ;;
+bench2)
+  for C in opt7 opt8 opt9; do
+    step bench_$C 500 python -u bench.py --config $C --batch 1024 --verify 1 --no-e2e --no-sdfg
+  done
+  CONCRETE_HIP_GEN_COOP=0 step bench_opt7_twolaunch 500 python -u bench.py --config opt7 --batch 1024 --verify 1 --no-e2e --no-sdfg
+  step bench_opt10 700 python -u bench.py --config opt10 --batch 512 --verify 1 --no-e2e --no-sdfg
+  ;;
 list)
   cd /tmp
   step counters 120 rocprofv3 -L

@@ -139,6 +139,17 @@ def pmc_ks_record(batch: int, config: str):
     return None
 
 
+def ref_cost_model(p, pbs_per_s):
+    """SURVEY.md §8(d) secondary compute figure: the reference optimizer's cost model of one PBS,
+    n [(k+1) l (N log2 N + N) + (k+1) (N log2 N + N) + (k+1)^2 l N] operations (concrete-optimizer
+    cmux.rs:31-50, pbs.rs:11-18; cfg2 64,512,000, cfg4 79,020,032), and the rate it implies."""
+    import math
+    k1, N, lg = p.k + 1, p.N, math.log2(p.N)
+    ops = p.n * (k1 * p.level * (N * lg + N) + k1 * (N * lg + N) + k1 * k1 * p.level * N)
+    return {"ops_per_pbs": int(ops), "achieved_gops": round(ops * pbs_per_s / 1e9, 1),
+            "note": "the reference cost model's operation count (not this backend's exact-arithmetic work)"}
+
+
 def host_cpus():
     """CPUs this process may use on this host: the affinity mask, capped by a cgroup CPU quota."""
     n_aff = len(os.sched_getaffinity(0))
@@ -299,7 +310,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_each = [a.elapsed_time(b) for a, b in ev]
+    kern_ms = float(np.mean(kern_each))
+    kern_med = float(np.median(kern_each))  # the median of the timed reps too
     total_done = args.batch * args.steps
     if world > 1:
         t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
@@ -620,8 +633,9 @@ def main():
                        "key_convert_s": round(t_key, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_src": traffic_src,
-                         "kernel_ms": round(kern_ms, 3), "bytes_per_pbs": bytes_per_pbs,
-                         "dram": dram, "valu": valu},
+                         "kernel_ms": round(kern_ms, 3), "kernel_ms_median": round(kern_med, 3),
+                         "bytes_per_pbs": bytes_per_pbs, "dram": dram, "valu": valu,
+                         "ref_cost_model": ref_cost_model(p, value)},
             "cpu_baseline": cpu,
             "secondary": {"keyswitch": ks_res, "sdfg_route": sdfg_res, "weak_scaling": weak_res,
                           "whole_node_share_b512": share_res,

@@ -264,3 +264,43 @@ def test_crafted_key_falls_back_to_the_general_path(env):
             assert rc == -2
     finally:
         ks.close()
+
+
+@pytest.mark.parametrize("shape", [
+    # (k, N, l, logB): one key format each (concrete_hip_bsk_format codes 1, 2, 4, 5, 3)
+    (1, 1024, 3, 7),    # N1024: oracle ora_fft_error_bound
+    (1, 2048, 1, 23),   # N2048: pyoracle.gpu2048_error_bound
+    (2, 1024, 1, 23),   # K2N1024: pyoracle.gpu1024k2_error_bound
+    (3, 512, 1, 18),    # SMALL: pyoracle.gpu_small_error_bound
+    (1, 4096, 1, 22),   # GENERIC: pyoracle.generic_error_bound
+], ids=["N1024", "N2048", "K2N1024", "SMALL", "GENERIC"])
+def test_key_bound_matches_the_oracle_per_format(env, shape):
+    """The gate's bound (keycheck.hip:certified_bound with the max|G| the conversion kernels
+    recorded, times each format's stored scale) equals the bound the GPU tests certify residuals
+    against (oracle/pyoracle.py, computed from the device key itself), for a random key of every key
+    format — so the per-call check refuses exactly where the tests' certificate would fail."""
+    import ctypes as C
+    B, O, L, torch = env["B"], env["O"], env["L"], env["torch"]
+    k, N, lv, logB = shape
+    p = B.PbsParams(n=2, k=k, N=N, level=lv, base_log=logB, ks_level=1, ks_base_log=1)
+    lwe_sk, glwe_sk = B.binary_key(p.n, 7700 + N), B.binary_key(p.big_n, 7701 + N)
+    bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 7702 + N)
+    fk = B.convert_bsk(p, bsk, "cuda:0")
+    torch.cuda.synchronize()
+    got = L.concrete_hip_key_error_bound(fk.data_ptr(), logB)
+    view = B.to_host(fk).view(np.float64)
+    limbs, bits = C.c_uint32(), C.c_uint32()
+    code = L.concrete_hip_bsk_format(k, N, lv, C.byref(limbs), C.byref(bits))
+    if code == 1:
+        op = O.Params(n=p.n, k=k, N=N, l=lv, logB=logB)
+        want = O.fft_error_bound(op, O.bsk_to_fourier(op, bsk))
+    elif code == 2:
+        want = O.gpu2048_error_bound(view, logB, lv)
+    elif code == 4:
+        want = O.gpu1024k2_error_bound(view, logB, lv)
+    elif code == 5:
+        want = O.gpu_small_error_bound(view, N, k, logB, lv)
+    else:
+        assert code == 3
+        want = O.generic_error_bound(k, N, lv, logB, bits.value, fbsk_gpu=view)
+    assert 0 < got < 0.5 and abs(got / want - 1.0) < 1e-6, (code, got, want)

@@ -9,7 +9,7 @@ EXTRA="$*"   # extra bench.py arguments (e.g. --config cfg4)
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp
-export TMPDIR=/tmp
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
 run() {  # name counters...
   local name=$1; shift
   timeout -k 10 ${PMC_TIMEOUT:-240} rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o run -- \

@@ -79,6 +79,10 @@ list)
 opt9)
   CONCRETE_HIP_GEN_STREAMS=1 prof opt9 bde "--batch 1024" 500
   ;;
+keybound)
+  step pytest_keybound 300 python -u -m pytest tests/test_gpu_robustness.py -v --timeout 200 --timeout-method thread
+  CONCRETE_HIP_GEN_STREAMS=1 PMC_TIMEOUT=600 step pmc_opt9 2460 bash tools/pmc.sh $TAG/opt9 bde --config opt9 --no-ks --no-sdfg --batch 1024
+  ;;
 opt10)
   CONCRETE_HIP_GEN_STREAMS=1 prof opt10 bde "--batch 512" 700
   ;;

@@ -80,11 +80,18 @@ def pmc_records(config: str):
     return out
 
 
-def pmc_traffic(batch: int, config: str):
-    """Per-launch HBM bytes from a committed PMC record measured at this batch; else None."""
-    for rec in pmc_records(config):
-        if rec.get("batch") == batch and "traffic_bytes" in rec:
+def pmc_traffic(batch: int, config: str, cus: int = 256):
+    """Per-launch HBM bytes from a committed PMC record measured at this batch; else a record of the
+    same kernel at another batch scaled by the batch ratio (the general path's rows at N >= 32768,
+    whose profiler passes finish only at small batches: labelled as scaled); else None."""
+    recs = [r for r in pmc_records(config) if "traffic_bytes" in r]
+    for rec in recs:
+        if rec.get("batch") == batch:
             return rec["traffic_bytes"], rec["src"]
+    kern = dispatched_kernel(batch, config, cus)
+    for rec in recs:
+        if kern is not None and rec.get("kernel") == kern:
+            return rec["traffic_bytes"] * batch / rec["batch"], rec["src"] + f" (scaled from batch {rec['batch']}, same kernel)"
     return None, None
 
 
@@ -208,6 +215,12 @@ def parse():
 
 
 
+def _progress(msg: str) -> None:
+    """Stage marks on stderr when CONCRETE_BENCH_PROGRESS=1 (long profiler passes show where they are)."""
+    if os.environ.get("CONCRETE_BENCH_PROGRESS") == "1":
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     import torch
@@ -260,8 +273,11 @@ def main():
     fbytes = B.fourier_bsk_bytes(p)
     t0 = time.perf_counter()
     if rank == 0:
+        _progress("keygen")
         bsk = B.bsk_generate(p, lwe_sk, glwe_sk, 3)
+        _progress("key conversion")
         fbsk = B.convert_bsk(p, bsk, dev)
+        _progress("key converted")
     else:
         bsk = None
         fbsk = torch.empty(fbytes // 8, dtype=torch.int64, device=dev)
@@ -292,12 +308,14 @@ def main():
     def step():
         B.pbs(p, fbsk, d_in, d_lut, out=d_out)
 
+    _progress("warm-up")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    _progress("timed steps")
     # kernel events on the stream the kernels are launched on (torch's current stream)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
@@ -560,7 +578,8 @@ def main():
         achieved = bytes_per_pbs * args.batch / (kern_ms * 1e-3) / 1e9
         bitexact = None
         cpu = None
-        traffic, traffic_src = pmc_traffic(args.batch, args.config)
+        traffic, traffic_src = pmc_traffic(args.batch, args.config,
+                                           torch.cuda.get_device_properties(dev).multi_processor_count)
         flop, flop_src = pmc_f64_flop(args.batch, args.config,
                                       torch.cuda.get_device_properties(dev).multi_processor_count)
         kern_s = kern_ms * 1e-3

@@ -83,6 +83,11 @@ keybound)
   step pytest_keybound 300 python -u -m pytest tests/test_gpu_robustness.py -v --timeout 200 --timeout-method thread
   CONCRETE_HIP_GEN_STREAMS=1 PMC_TIMEOUT=600 step pmc_opt9 2460 bash tools/pmc.sh $TAG/opt9 bde --config opt9 --no-ks --no-sdfg --batch 1024
   ;;
+pmc910)
+  export CONCRETE_HIP_GEN_STREAMS=1 PMC_TIMEOUT=240
+  step pmc_opt9_deb 800 bash tools/pmc.sh $TAG/opt9 deb --config opt9 --no-ks --no-sdfg --batch 128
+  step pmc_opt10_deb 800 bash tools/pmc.sh $TAG/opt10 deb --config opt10 --no-ks --no-sdfg --batch 64
+  ;;
 opt10)
   CONCRETE_HIP_GEN_STREAMS=1 prof opt10 bde "--batch 512" 700
   ;;

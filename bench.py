@@ -80,10 +80,22 @@ def pmc_records(config: str):
     return out
 
 
+# environment overrides that change which kernels a call runs (A/B and diagnostic runs): a PMC
+# record taken on the default dispatch does not describe them
+DISPATCH_OVERRIDES = ("CONCRETE_HIP_LIB", "CONCRETE_HIP_GEN_COOP", "CONCRETE_HIP_GEN_FUSED", "CONCRETE_HIP_GEN_FUSEDY",
+                      "CONCRETE_HIP_PBS_PAIRS", "CONCRETE_HIP_PBS_HEX")
+
+
+def dispatch_overridden() -> bool:
+    return any(os.environ.get(v) not in (None, "") for v in DISPATCH_OVERRIDES)
+
+
 def pmc_traffic(batch: int, config: str, cus: int = 256):
     """Per-launch HBM bytes from a committed PMC record measured at this batch; else a record of the
     same kernel at another batch scaled by the batch ratio (the general path's rows at N >= 32768,
     whose profiler passes finish only at small batches: labelled as scaled); else None."""
+    if dispatch_overridden():
+        return None, None
     recs = [r for r in pmc_records(config) if "traffic_bytes" in r]
     for rec in recs:
         if rec.get("batch") == batch:
@@ -119,6 +131,8 @@ def pmc_f64_flop(batch: int, config: str, cus: int = 256):
     batch is used as is; the work is per ciphertext, so a record at another batch is scaled by the
     batch ratio, but only when it was taken on the kernel this batch's call runs (cfg2
     runs the six-wave kernel at <= 2 x CUs, the pair kernel above, and a split between)."""
+    if dispatch_overridden():
+        return None, None
     recs = [r for r in pmc_records(config) if "f64_flop" in r]
     for rec in recs:
         if rec.get("batch") == batch:

@@ -1,4 +1,4 @@
-"""Collect the bench lines of tools/r05_final.sh (parts a and d) into one record:
+"""Collect the bench lines of tools/r06.sh bench1 / bench2 (r05: tools/r05_final.sh) into one record:
 python tools/collect_bench.py gpurun_out/<tag> profiles/<round>_bench_all_configs.json"""
 import glob
 import json
@@ -6,7 +6,7 @@ import os
 import sys
 
 src, dst = sys.argv[1], sys.argv[2]
-out = {"note": "bench.py lines of every config on the final sources, one MI355X box (tools/r05_final.sh); "
+out = {"note": "bench.py lines of every config on the final sources, one MI355X box (tools/r06.sh bench1 + bench2; r05: tools/r05_final.sh); "
                "cfg2 = BASELINE configs[1] (the metric), cfg4 = configs[3], opt8 = configs[4]'s optimizer row; "
                "opt1..opt6 at batch 4096, opt7..opt9 at 1024, opt10 at 512; opt7_twolaunch = opt7 with "
                "CONCRETE_HIP_GEN_COOP=0 (the two-launch path, for the A/B of DESIGN.md §4.12)",

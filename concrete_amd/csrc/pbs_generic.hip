@@ -988,7 +988,25 @@ struct SplitArgs {
   unsigned long long* resid;
   uint32_t base, count, n, k, level, base_log, bits, limbs, subs;
   uint32_t step;  // front: the mask position whose rotation is prepared
+  uint32_t xcd = 1;  // the S class workgroups of a polynomial on one XCD (split_block)
 };
+
+// workgroup -> (polynomial, class h).  Each class workgroup reads its polynomial's whole slot
+// spectra (back) and rotated accumulator (front), so with xcd the S classes of a polynomial are
+// placed on one XCD — workgroups b and b + 8 share one under the round-robin dispatch — and the
+// second to S-th reads can hit that XCD's L2; the last partial group of fewer than 8 polynomials
+// keeps the plain order
+template <int S>
+__device__ __forceinline__ void split_block(uint32_t b, uint32_t polys, bool xcd, uint32_t& poly, uint32_t& h) {
+  const uint32_t g = b / (8 * S), r = b % (8 * S);
+  if (xcd && (g + 1) * 8 <= polys) {
+    poly = g * 8 + (r & 7);
+    h = r >> 3;
+  } else {
+    poly = b / S;
+    h = b % S;
+  }
+}
 
 template <int S>
 struct Split {
@@ -1058,7 +1076,10 @@ __global__ void __launch_bounds__(512) gen_split_front_kernel(SplitArgs a) {
   using St = typename std::conditional<W32, uint32_t, uint64_t>::type;
   using Dg = typename std::conditional<W32, int32_t, int64_t>::type;
   __shared__ cplx lds[G::LDS_CPLX];
-  const uint32_t K1 = a.k + 1, h = blockIdx.x % S, poly = blockIdx.x / S, ct = poly / K1;
+  const uint32_t K1 = a.k + 1;
+  uint32_t poly, h;
+  split_block<S>(blockIdx.x, a.count * K1, a.xcd != 0, poly, h);
+  const uint32_t ct = poly / K1;
   const SplitRows<S> q = split_rows_setup<S>(lds, a, (int)h);
   const int lane = q.lane;
   cplx* xch = q.E + q.w * 2 * RS;  // the wave's first row and its pad
@@ -1138,12 +1159,16 @@ __global__ void __launch_bounds__(512) gen_split_front_kernel(SplitArgs a) {
 }
 
 // back: acc += sum_m 2^{m b} round(iFFT(Y_m) conj(zeta^j)) for the rows of class h
-template <int S>
+// HPRE: the product kernel has already split the slot spectra by class (gen_mac_split_kernel writes
+// H_h[m][k1'][pos] in Y's place), so class h loads its 16 values per slot directly — a third of the
+// loads at S = 2 with no combination — and the next slot's are loaded while this slot is transformed
+template <int S, bool HPRE>
 __global__ void __launch_bounds__(512) gen_split_back_kernel(SplitArgs a) {
   using G = Split<S>;
   constexpr int N = G::N, R = G::R, RS = G::RS, M = G::M, ROWLEN = N / R;
   __shared__ cplx lds[G::LDS_CPLX];
-  const uint32_t h = blockIdx.x % S, poly = blockIdx.x / S;
+  uint32_t poly, h;
+  split_block<S>(blockIdx.x, a.count * (a.k + 1), a.xcd != 0, poly, h);
   const SplitRows<S> q = split_rows_setup<S>(lds, a, (int)h);
   const int lane = q.lane, pos = threadIdx.x;
   cplx* xch = q.E + q.w * 2 * RS;
@@ -1157,22 +1182,43 @@ __global__ void __launch_bounds__(512) gen_split_back_kernel(SplitArgs a) {
   // conj(w_R^{h (k1' + 16 u)}) for this class, k1' < 16, u < S
   const cplx* Yc = a.Y + (uint64_t)poly * a.limbs * M + pos;
   double max_resid = 0.0;
+#ifndef SPLIT_HPF
+// HPRE: load the next slot's values while this slot is transformed.  Off: it spills 39 VGPRs here
+// (256 + 156 B/lane) and measured 258.5 vs 261.4 PBS/s at opt9, 72.2 vs 72.7 at opt10
+#define SPLIT_HPF 0
+#endif
+  constexpr bool PF = HPRE && SPLIT_HPF;
+  cplx pf[HPRE ? SPLIT_ROWS : 1];
+  auto load_h = [&](uint32_t m) {
+    const cplx* Hm = Yc + (uint64_t)m * M + (uint64_t)h * SPLIT_ROWS * 512;
+#pragma unroll
+    for (int k1 = 0; k1 < SPLIT_ROWS; ++k1) pf[k1] = Hm[(uint64_t)k1 * 512];
+    __builtin_amdgcn_sched_barrier(0);  // issued here, not sunk to their first use
+  };
+  if constexpr (PF) load_h(0);
   pair_barrier();  // fft512 tables, beta
 #pragma unroll 1
   for (uint32_t m = 0; m < a.limbs; ++m) {
     const cplx* Ym = Yc + (uint64_t)m * M;
     cplx u[SPLIT_ROWS];
+    if constexpr (HPRE) {
+      if constexpr (!PF) load_h(m);
 #pragma unroll
-    for (int k1 = 0; k1 < SPLIT_ROWS; ++k1) {
-      cplx hsum = {0.0, 0.0};
+      for (int k1 = 0; k1 < SPLIT_ROWS; ++k1) u[k1] = pf[k1];
+      if (PF && m + 1 < a.limbs) load_h(m + 1);
+    } else {
 #pragma unroll
-      for (int uu = 0; uu < S; ++uu) {
-        const int kk = k1 + SPLIT_ROWS * uu;
-        const cplx y = Ym[(uint64_t)kk * 512];
-        const cplx w = a.WR[(h * kk) & (R - 1)];
-        hsum = cadd(hsum, cmulc(y, w));
+      for (int k1 = 0; k1 < SPLIT_ROWS; ++k1) {
+        cplx hsum = {0.0, 0.0};
+#pragma unroll
+        for (int uu = 0; uu < S; ++uu) {
+          const int kk = k1 + SPLIT_ROWS * uu;
+          const cplx y = Ym[(uint64_t)kk * 512];
+          const cplx w = a.WR[(h * kk) & (R - 1)];
+          hsum = cadd(hsum, cmulc(y, w));
+        }
+        u[k1] = hsum;
       }
-      u[k1] = hsum;
     }
     dft_col<SPLIT_ROWS, true>(u);
 #pragma unroll
@@ -1224,16 +1270,33 @@ struct MacSplitArgs {
   uint32_t i;
 };
 
+// The slot spectra leave already split by class for gen_split_back_kernel<S, true>.  A wave covers
+// 64 / S positions of one k1' < 16 at its S frequencies k1' + 16 u (lane = u 64 / S + position), so
+// the S values of a position meet inside the wave: the digit spectra are combined from the S class
+// transforms (each lane loads its own class's value, the others arrive by lane shuffles), and lane
+// (u, position) writes class h = u's H_h[k1'] = sum_u' conj(w_R^{h (k1' + 16 u')}) Y[k1' + 16 u'] —
+// the back kernel's former combination, same terms in the same order — at [ct][c][m][h][k1'][pos], in
+// Y's place and size.  (Exchanging through LDS behind a workgroup barrier per ciphertext instead:
+// 1018 vs 798 us per step at opt10.)
 template <int KL, int L, int T, int S>
 __global__ void __launch_bounds__(256) gen_mac_split_kernel(MacSplitArgs a) {
-  const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+  constexpr int QW = 64 / S, PB = 256 / S;  // positions per wave / per block
+  const uint32_t b = blockIdx.x, kl = b / (2 * S), lane = threadIdx.x & 63;
+  const uint32_t u = lane / QW, pl = lane % QW;
+  const uint32_t pos = (b % (2 * S)) * PB + (threadIdx.x >> 6) * QW + pl;
+  const uint32_t k1 = kl + SPLIT_ROWS * u, p = k1 * 512 + pos;
   const uint32_t c = blockIdx.y, K1 = a.k + 1;
   const uint64_t M = a.M;
-  if (p >= M) return;
-  const uint32_t k1 = p >> 9, pos = p & 511, kl = k1 & (SPLIT_ROWS - 1);
-  cplx wr[S];
+  cplx wr[S], wi[S];
 #pragma unroll
-  for (int h = 0; h < S; ++h) wr[h] = a.WR[(h * k1) & (a.R - 1)];
+  for (int hh = 0; hh < S; ++hh) {
+    wr[hh] = a.WR[(hh * k1) & (a.R - 1)];
+    wi[hh] = a.WR[(u * (kl + SPLIT_ROWS * hh)) & (a.R - 1)];
+  }
+  auto from = [&](cplx v, int hh) -> cplx {  // lane (hh, pl)'s value
+    const int src = hh * QW + (int)pl;
+    return {__shfl(v.re, src, 64), __shfl(v.im, src, 64)};
+  };
   cplx kv[L][KL];
 #pragma unroll
   for (int lim = 0; lim < L; ++lim)
@@ -1241,23 +1304,28 @@ __global__ void __launch_bounds__(256) gen_mac_split_kernel(MacSplitArgs a) {
     for (int rq = 0; rq < KL; ++rq) kv[lim][rq] = a.G[((((uint64_t)a.i * K1 + c) * L + lim) * KL + rq) * M + p];
   const uint32_t ct0 = blockIdx.z * MAC_CTS;
   for (uint32_t ct = ct0; ct < ct0 + MAC_CTS && ct < a.count; ++ct) {
-    const cplx* Xct = a.X + (uint64_t)ct * KL * T * M + (uint64_t)kl * 512 + pos;
+    // my class's transform value at (k1', pos) of every digit polynomial
+    const cplx* Xct = a.X + (uint64_t)ct * KL * T * M + (uint64_t)u * SPLIT_ROWS * 512 + (uint64_t)kl * 512 + pos;
     cplx xv[KL][T];
 #pragma unroll
     for (int rq = 0; rq < KL; ++rq)
 #pragma unroll
-      for (int t = 0; t < T; ++t) {
-        const cplx* g = Xct + (uint64_t)(rq * T + t) * M;
-        cplx x = g[0];  // class 0: w_R^0 = 1
+      for (int t = 0; t < T; ++t) xv[rq][t] = Xct[(uint64_t)(rq * T + t) * M];
 #pragma unroll
-        for (int h = 1; h < S; ++h) {
-          const cplx gh = g[(uint64_t)h * SPLIT_ROWS * 512], w = wr[h];
+    for (int rq = 0; rq < KL; ++rq)
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const cplx g = xv[rq][t];
+        cplx x = from(g, 0);  // class 0: w_R^0 = 1
+#pragma unroll
+        for (int hh = 1; hh < S; ++hh) {
+          const cplx gh = from(g, hh), w = wr[hh];
           x.re = __builtin_fma(gh.re, w.re, __builtin_fma(-gh.im, w.im, x.re));
           x.im = __builtin_fma(gh.re, w.im, __builtin_fma(gh.im, w.re, x.im));
         }
         xv[rq][t] = x;
       }
-    cplx* Yct = a.Y + ((uint64_t)ct * K1 + c) * L * M + p;
+    cplx* Hct = a.Y + ((uint64_t)ct * K1 + c) * L * M + (uint64_t)(u * SPLIT_ROWS + kl) * 512 + pos;
 #pragma unroll
     for (int m = 0; m < L; ++m) {
       cplx y = {0.0, 0.0};
@@ -1271,7 +1339,10 @@ __global__ void __launch_bounds__(256) gen_mac_split_kernel(MacSplitArgs a) {
           y.im = __builtin_fma(xg.re, g.im, __builtin_fma(xg.im, g.re, y.im));
         }
       }
-      Yct[(uint64_t)m * M] = y;
+      cplx hsum = {0.0, 0.0};
+#pragma unroll
+      for (int uu = 0; uu < S; ++uu) hsum = cadd(hsum, cmulc(from(y, uu), wi[uu]));
+      Hct[(uint64_t)m * M] = hsum;
     }
   }
 }
@@ -2852,15 +2923,17 @@ static bool coop_dispatch(const PbsArgs& a, const Tables& tb, uint32_t T, uint32
 // N >= 32768: the split path (S = N / 16384 workgroups per polynomial), one stream, chunks of
 // <= 2 GB of scratch run one after another: init, then per CMUX step the product, the back half
 // and the next step's front half.
+// true: the register-tiled product ran, which leaves the slot spectra split by class (HPRE)
 template <int S>
-static void launch_split_mac(const MacSplitArgs& m, uint32_t KL, uint32_t cnt, hipStream_t st) {
+static bool launch_split_mac(const MacSplitArgs& m, uint32_t KL, uint32_t cnt, hipStream_t st) {
   const dim3 g1((m.M + 255) / 256, m.k + 1, (cnt + MAC_CTS - 1) / MAC_CTS);
   if (KL == 4 && m.limbs == 7 && m.subs == 2) {
     hipLaunchKernelGGL((gen_mac_split_kernel<4, 7, 2, S>), g1, dim3(256), 0, st, m);
-    return;
+    return true;
   }
   const dim3 g2((m.M + 255) / 256, (m.k + 1) * m.limbs, (cnt + MAC_CTS - 1) / MAC_CTS);
   hipLaunchKernelGGL((gen_mac_split_generic_kernel<S>), g2, dim3(256), 0, st, m);
+  return false;
 }
 
 template <int S>
@@ -2887,6 +2960,8 @@ static int pbs_split_launch(const PbsArgs& a, const KeyFormat& fmt, const Tables
   keep_pool_memory();
   CHIP_CHECK(hipMallocAsync(&scratch, per_ct * chunk, a.stream));
   hipStream_t st = a.stream;
+  const char* xe = getenv("CONCRETE_HIP_SPLIT_XCD");  // 0: plain workgroup order (A/B)
+  const bool xcd = !(xe && atoi(xe) == 0);
   for (uint32_t base = 0; base < a.num_samples; base += chunk) {
     const uint32_t cnt = std::min(chunk, a.num_samples - base);
     cplx* X = reinterpret_cast<cplx*>(scratch);
@@ -2894,6 +2969,7 @@ static int pbs_split_launch(const PbsArgs& a, const KeyFormat& fmt, const Tables
     uint64_t* acc = reinterpret_cast<uint64_t*>(Y + (uint64_t)chunk * K1 * L * M);
     SplitArgs sa{acc, X, Y, tb.Tau, tb.WR, a.in, a.in_idx, a.luts, a.lut_idx, a.resid,
                  base, cnt, a.n, a.k, a.level, a.base_log, fmt.bits, L, T, 0};
+    sa.xcd = xcd ? 1u : 0u;
     MacSplitArgs ma{X, Y, reinterpret_cast<const cplx*>(a.fbsk), tb.WR, cnt, a.k, a.level, L, T, M, G::R, 0};
     const uint64_t elems = (uint64_t)cnt * K1 * a.N;
     hipLaunchKernelGGL((gen_split_init_kernel<S>), dim3((uint32_t)std::min<uint64_t>((elems + 255) / 256, 65535)),
@@ -2901,8 +2977,10 @@ static int pbs_split_launch(const PbsArgs& a, const KeyFormat& fmt, const Tables
     launch_split_front<S>(sa, K1, st);
     for (uint32_t i = 0; i < a.n; ++i) {
       ma.i = i;
-      launch_split_mac<S>(ma, K1 * a.level, cnt, st);
-      hipLaunchKernelGGL((gen_split_back_kernel<S>), dim3(cnt * K1 * S), dim3(512), 0, st, sa);
+      if (launch_split_mac<S>(ma, K1 * a.level, cnt, st))
+        hipLaunchKernelGGL((gen_split_back_kernel<S, true>), dim3(cnt * K1 * S), dim3(512), 0, st, sa);
+      else
+        hipLaunchKernelGGL((gen_split_back_kernel<S, false>), dim3(cnt * K1 * S), dim3(512), 0, st, sa);
       if (i + 1 < a.n) {
         sa.step = i + 1;
         launch_split_front<S>(sa, K1, st);

@@ -125,6 +125,8 @@ bool generic_pbs_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
   return generic_error_bound(k, N, level, base_log, f.bits, 0.0) < 0.25;
 }
 
+static hipStream_t side_stream(int idx);  // a library stream per device (defined below)
+
 namespace gen {
 
 // ------------------------------------------------------------------------------------------
@@ -2945,6 +2947,10 @@ static void launch_split_front(const SplitArgs& s, uint32_t K1, hipStream_t st) 
     hipLaunchKernelGGL((gen_split_front_kernel<S, false>), grid, dim3(512), 0, st, s);
 }
 
+// Chunks run in groups of NS on NS streams (the caller's and library streams, as the two-launch
+// path), their launches interleaved, so one chunk's product kernel (HBM streaming) runs beside
+// another's back / front kernels (one LDS-filling workgroup per CU).  CONCRETE_HIP_GEN_STREAMS=n
+// (1..4, default 2) sets NS.
 template <int S>
 static int pbs_split_launch(const PbsArgs& a, const KeyFormat& fmt, const Tables& tb, uint32_t T) {
   using G = Split<S>;
@@ -2954,51 +2960,95 @@ static int pbs_split_launch(const PbsArgs& a, const KeyFormat& fmt, const Tables
   const uint64_t budget = be && atoi(be) > 0 ? (uint64_t)atoi(be) << 20 : 2ull << 30;
   const char* ce = getenv("CONCRETE_HIP_GEN_CHUNK");
   const uint64_t cap = ce && atoi(ce) > 0 ? (uint64_t)atoi(ce) : 65536;
-  const uint32_t chunk = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(a.num_samples, cap),
-                                                      std::max<uint64_t>(1, budget / per_ct));
+  const uint32_t chunk_max = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(a.num_samples, cap),
+                                                          std::max<uint64_t>(1, budget / per_ct));
+  uint32_t nchunks = (a.num_samples + chunk_max - 1) / chunk_max;
+  constexpr int MAX_NS = 4;
+  const char* se = getenv("CONCRETE_HIP_GEN_STREAMS");
+  const int want = se && atoi(se) >= 1 ? std::min(atoi(se), MAX_NS) : 2;
+  const int NS = (int)std::min<uint32_t>((uint32_t)want, nchunks);
+  nchunks = (nchunks + NS - 1) / NS * NS;  // balanced groups of NS chunks
+  const uint32_t chunk = (a.num_samples + nchunks - 1) / nchunks;
+  hipStream_t st[MAX_NS];
+  for (int q = 0; q < MAX_NS; ++q) st[q] = q == 0 || q >= NS ? a.stream : side_stream(q);
   void* scratch = nullptr;
   keep_pool_memory();
-  CHIP_CHECK(hipMallocAsync(&scratch, per_ct * chunk, a.stream));
-  hipStream_t st = a.stream;
+  CHIP_CHECK(hipMallocAsync(&scratch, per_ct * chunk * NS, a.stream));
+  hipEvent_t ev_in = nullptr;
+  if (NS > 1) {  // the library streams start after the caller's prior work and the allocation
+    CHIP_CHECK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+    CHIP_CHECK(hipEventRecord(ev_in, a.stream));
+    for (int q = 1; q < NS; ++q) CHIP_CHECK(hipStreamWaitEvent(st[q], ev_in, 0));
+  }
   const char* xe = getenv("CONCRETE_HIP_SPLIT_XCD");  // 0: plain workgroup order (A/B)
   const bool xcd = !(xe && atoi(xe) == 0);
-  for (uint32_t base = 0; base < a.num_samples; base += chunk) {
-    const uint32_t cnt = std::min(chunk, a.num_samples - base);
-    cplx* X = reinterpret_cast<cplx*>(scratch);
-    cplx* Y = X + (uint64_t)chunk * K1 * a.level * T * M;
-    uint64_t* acc = reinterpret_cast<uint64_t*>(Y + (uint64_t)chunk * K1 * L * M);
-    SplitArgs sa{acc, X, Y, tb.Tau, tb.WR, a.in, a.in_idx, a.luts, a.lut_idx, a.resid,
-                 base, cnt, a.n, a.k, a.level, a.base_log, fmt.bits, L, T, 0};
-    sa.xcd = xcd ? 1u : 0u;
-    MacSplitArgs ma{X, Y, reinterpret_cast<const cplx*>(a.fbsk), tb.WR, cnt, a.k, a.level, L, T, M, G::R, 0};
-    const uint64_t elems = (uint64_t)cnt * K1 * a.N;
-    hipLaunchKernelGGL((gen_split_init_kernel<S>), dim3((uint32_t)std::min<uint64_t>((elems + 255) / 256, 65535)),
-                       dim3(256), 0, st, sa);
-    launch_split_front<S>(sa, K1, st);
+  struct Lane {
+    SplitArgs s;
+    MacSplitArgs m;
+    uint32_t cnt;
+  };
+  int rc = 0;
+  for (uint32_t base0 = 0; base0 < a.num_samples && rc == 0; base0 += NS * chunk) {
+    Lane ln[MAX_NS];
+    int nl = 0;
+    for (int q = 0; q < NS; ++q) {
+      const uint32_t base = base0 + q * chunk;
+      if (base >= a.num_samples) break;
+      const uint32_t cnt = std::min(chunk, a.num_samples - base);
+      cplx* X = reinterpret_cast<cplx*>(static_cast<char*>(scratch) + (uint64_t)q * per_ct * chunk);
+      cplx* Y = X + (uint64_t)chunk * K1 * a.level * T * M;
+      uint64_t* acc = reinterpret_cast<uint64_t*>(Y + (uint64_t)chunk * K1 * L * M);
+      ln[q].s = SplitArgs{acc, X, Y, tb.Tau, tb.WR, a.in, a.in_idx, a.luts, a.lut_idx, a.resid,
+                          base, cnt, a.n, a.k, a.level, a.base_log, fmt.bits, L, T, 0};
+      ln[q].s.xcd = xcd ? 1u : 0u;
+      ln[q].m = MacSplitArgs{X, Y, reinterpret_cast<const cplx*>(a.fbsk), tb.WR, cnt, a.k, a.level, L, T, M, G::R, 0};
+      ln[q].cnt = cnt;
+      ++nl;
+    }
+    for (int q = 0; q < nl; ++q) {
+      const uint64_t elems = (uint64_t)ln[q].cnt * K1 * a.N;
+      hipLaunchKernelGGL((gen_split_init_kernel<S>), dim3((uint32_t)std::min<uint64_t>((elems + 255) / 256, 65535)),
+                         dim3(256), 0, st[q], ln[q].s);
+      launch_split_front<S>(ln[q].s, K1, st[q]);
+    }
     for (uint32_t i = 0; i < a.n; ++i) {
-      ma.i = i;
-      if (launch_split_mac<S>(ma, K1 * a.level, cnt, st))
-        hipLaunchKernelGGL((gen_split_back_kernel<S, true>), dim3(cnt * K1 * S), dim3(512), 0, st, sa);
-      else
-        hipLaunchKernelGGL((gen_split_back_kernel<S, false>), dim3(cnt * K1 * S), dim3(512), 0, st, sa);
-      if (i + 1 < a.n) {
-        sa.step = i + 1;
-        launch_split_front<S>(sa, K1, st);
+      for (int q = 0; q < nl; ++q) {
+        Lane& l = ln[q];
+        l.m.i = i;
+        if (launch_split_mac<S>(l.m, K1 * a.level, l.cnt, st[q]))
+          hipLaunchKernelGGL((gen_split_back_kernel<S, true>), dim3(l.cnt * K1 * S), dim3(512), 0, st[q], l.s);
+        else
+          hipLaunchKernelGGL((gen_split_back_kernel<S, false>), dim3(l.cnt * K1 * S), dim3(512), 0, st[q], l.s);
+        if (i + 1 < a.n) {
+          l.s.step = i + 1;
+          launch_split_front<S>(l.s, K1, st[q]);
+        }
       }
     }
-    const uint64_t total = ((uint64_t)a.k * a.N + 1) * cnt;
-    const uint32_t eb = (uint32_t)std::min<uint64_t>((total + 255) / 256, 65535);
-    hipLaunchKernelGGL(gen_extract_kernel, dim3(eb), dim3(256), 0, st, a.out, a.out_idx, acc, base, cnt, a.k, a.N,
-                       (uint32_t)G::LOGR);
+    for (int q = 0; q < nl; ++q) {
+      const uint64_t total = ((uint64_t)a.k * a.N + 1) * ln[q].cnt;
+      const uint32_t eb = (uint32_t)std::min<uint64_t>((total + 255) / 256, 65535);
+      hipLaunchKernelGGL(gen_extract_kernel, dim3(eb), dim3(256), 0, st[q], a.out, a.out_idx, ln[q].s.acc,
+                         ln[q].s.base, ln[q].cnt, a.k, a.N, (uint32_t)G::LOGR);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       set_error("generic pbs (split) launch failed: %s", hipGetErrorString(e));
-      CHIP_CHECK(hipFreeAsync(scratch, a.stream));
-      return -1;
+      rc = -1;
     }
   }
+  if (NS > 1) {  // the caller's stream resumes after the library streams' chunks
+    for (int q = 1; q < NS; ++q) {
+      hipEvent_t ev = nullptr;
+      CHIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      CHIP_CHECK(hipEventRecord(ev, st[q]));
+      CHIP_CHECK(hipStreamWaitEvent(a.stream, ev, 0));
+      CHIP_CHECK(hipEventDestroy(ev));
+    }
+    CHIP_CHECK(hipEventDestroy(ev_in));
+  }
   CHIP_CHECK(hipFreeAsync(scratch, a.stream));
-  return 0;
+  return rc;
 }
 
 template <int S>
@@ -3037,8 +3087,8 @@ uint64_t generic_scratch_bytes_per_sample(uint32_t k, uint32_t N, uint32_t level
   return K1 * level * T * M * 16 + K1 * f.limbs * M * 16 + K1 * N * 8;
 }
 
-// A second stream per device for the two-launch path's chunk pairs (created once, never destroyed:
-// it lives as long as the process, like the device tables).
+// A second stream per device for the two-launch and split paths' chunk groups (created once, never
+// destroyed: it lives as long as the process, like the device tables).
 static hipStream_t side_stream(int idx) {
   static std::mutex mu;
   static std::map<std::pair<int, int>, hipStream_t> streams;

@@ -201,9 +201,10 @@ def test_generic_legacy_step_kernel(B, oracle, torch_cuda):
 
 
 @pytest.mark.parametrize("streams", [0, 1, 2, 3])
-@pytest.mark.parametrize("ci", [5, 7], ids=[CASES[i][0] for i in (5, 7)])
+@pytest.mark.parametrize("ci", [5, 7, 13, 14], ids=[CASES[i][0] for i in (5, 7, 13, 14)])
 def test_generic_chunked_two_streams(B, oracle, torch_cuda, ci, streams, monkeypatch):
-    """The two-launch path over several chunks (CONCRETE_HIP_GEN_CHUNK=3 on 7 ciphertexts: 3
+    """The two-launch path (N = 4096 / 16384) and the split path (N = 2^15 / 2^16, chunk groups on
+    several streams since round 6) over several chunks (CONCRETE_HIP_GEN_CHUNK=3 on 7 ciphertexts: 3
     chunks of 3 + 3 + 1 on one or three streams, evened to 4 chunks of 2 + 2 + 2 + 1 for two
     streams: groups of chunks on the caller's and library streams), with permuted input / output
     rows and mapped LUTs: bit-exact vs the exact oracle."""

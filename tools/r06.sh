@@ -83,6 +83,13 @@ keybound)
   step pytest_keybound 300 python -u -m pytest tests/test_gpu_robustness.py -v --timeout 200 --timeout-method thread
   CONCRETE_HIP_GEN_STREAMS=1 PMC_TIMEOUT=600 step pmc_opt9 2460 bash tools/pmc.sh $TAG/opt9 bde --config opt9 --no-ks --no-sdfg --batch 1024
   ;;
+genprof)  # every general-path row after the round-6 split-path change (pbs_generic.hip)
+  prof opt6 bde ""
+  CONCRETE_HIP_GEN_STREAMS=1 prof opt7 bde "--batch 1024" 400
+  CONCRETE_HIP_GEN_STREAMS=1 prof opt8 bde "--batch 1024" 500
+  CONCRETE_HIP_GEN_STREAMS=1 prof opt9 bde "--batch 128" 240
+  CONCRETE_HIP_GEN_STREAMS=1 prof opt10 bde "--batch 64" 240
+  ;;
 pmc910)
   export CONCRETE_HIP_GEN_STREAMS=1 PMC_TIMEOUT=240
   step pmc_opt9_deb 800 bash tools/pmc.sh $TAG/opt9 deb --config opt9 --no-ks --no-sdfg --batch 128

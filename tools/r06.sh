@@ -72,6 +72,14 @@ bench2)
   CONCRETE_HIP_GEN_COOP=0 step bench_opt7_twolaunch 500 python -u bench.py --config opt7 --batch 1024 --verify 1 --no-e2e --no-sdfg
   step bench_opt10 700 python -u bench.py --config opt10 --batch 512 --verify 1 --no-e2e --no-sdfg
   ;;
+bench3)  # the general-path rows (opt6 .. opt10) after the split-path change
+  step bench_opt6 400 python -u bench.py --config opt6 --verify 2 --no-e2e --no-sdfg
+  for C in opt7 opt8 opt9; do
+    step bench_$C 500 python -u bench.py --config $C --batch 1024 --verify 1 --no-e2e --no-sdfg
+  done
+  CONCRETE_HIP_GEN_COOP=0 step bench_opt7_twolaunch 500 python -u bench.py --config opt7 --batch 1024 --verify 1 --no-e2e --no-sdfg
+  step bench_opt10 700 python -u bench.py --config opt10 --batch 512 --verify 1 --no-e2e --no-sdfg
+  ;;
 list)
   cd /tmp
   step counters 120 rocprofv3 -L

@@ -1185,26 +1185,32 @@ __global__ void __launch_bounds__(512) gen_split_back_kernel(SplitArgs a) {
   const cplx* Yc = a.Y + (uint64_t)poly * a.limbs * M + pos;
   double max_resid = 0.0;
 #ifndef SPLIT_HPF
-// HPRE: load the next slot's values while this slot is transformed.  Off: it spills 39 VGPRs here
-// (256 + 156 B/lane) and measured 258.5 vs 261.4 PBS/s at opt9, 72.2 vs 72.7 at opt10
-#define SPLIT_HPF 0
+// HPRE: how the next slot's values are loaded ahead.  3 (kept): half of them, issued once this slot's
+// columns are in LDS (254 VGPRs; +2 % against none at opt9 and opt10, profiles/r06/split_path);
+// 1: all of them before this slot's transforms (spills 39 VGPRs, -1 %); 2: all of them after the
+// columns (spills 29, -1 %); 0: none
+#define SPLIT_HPF 3
 #endif
-  constexpr bool PF = HPRE && SPLIT_HPF;
+  constexpr bool PF = HPRE && SPLIT_HPF == 1;
+  constexpr bool LATE = HPRE && (SPLIT_HPF == 2 || SPLIT_HPF == 3);  // variant: issued after this slot's columns are in LDS
+  constexpr int NPF = SPLIT_HPF == 3 ? SPLIT_ROWS / 2 : SPLIT_ROWS;  // values loaded ahead (3: half)
   cplx pf[HPRE ? SPLIT_ROWS : 1];
-  auto load_h = [&](uint32_t m) {
+  auto load_h = [&](uint32_t m, int k0 = 0, int k9 = SPLIT_ROWS) {
     const cplx* Hm = Yc + (uint64_t)m * M + (uint64_t)h * SPLIT_ROWS * 512;
 #pragma unroll
-    for (int k1 = 0; k1 < SPLIT_ROWS; ++k1) pf[k1] = Hm[(uint64_t)k1 * 512];
+    for (int k1 = 0; k1 < SPLIT_ROWS; ++k1)
+      if (k1 >= k0 && k1 < k9) pf[k1] = Hm[(uint64_t)k1 * 512];
     __builtin_amdgcn_sched_barrier(0);  // issued here, not sunk to their first use
   };
-  if constexpr (PF) load_h(0);
+  if constexpr (PF || LATE) load_h(0, 0, NPF);
   pair_barrier();  // fft512 tables, beta
 #pragma unroll 1
   for (uint32_t m = 0; m < a.limbs; ++m) {
     const cplx* Ym = Yc + (uint64_t)m * M;
     cplx u[SPLIT_ROWS];
     if constexpr (HPRE) {
-      if constexpr (!PF) load_h(m);
+      if constexpr (!PF && !LATE) load_h(m);
+      if constexpr (LATE && NPF < SPLIT_ROWS) load_h(m, NPF, SPLIT_ROWS);
 #pragma unroll
       for (int k1 = 0; k1 < SPLIT_ROWS; ++k1) u[k1] = pf[k1];
       if (PF && m + 1 < a.limbs) load_h(m + 1);
@@ -1225,6 +1231,7 @@ __global__ void __launch_bounds__(512) gen_split_back_kernel(SplitArgs a) {
     dft_col<SPLIT_ROWS, true>(u);
 #pragma unroll
     for (int jl = 0; jl < SPLIT_ROWS; ++jl) q.E[jl * RS + pos] = u[jl];
+    if (LATE && m + 1 < a.limbs) load_h(m + 1, 0, NPF);
     pair_barrier();
     const uint32_t sh = (m * a.bits) & 63u;
 #pragma unroll

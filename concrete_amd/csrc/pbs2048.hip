@@ -79,6 +79,9 @@ __device__ __forceinline__ void quad_sync(uint32_t* flags, int ctl, int v, uint3
 #define D4_NOQS 0
 #endif
 
+#ifndef P2_DEFER_INV
+#define P2_DEFER_INV 1  // limb li's inverse after limb li + 1's first key-window barrier, no quad sync (+1.0 %)
+#endif
 #ifndef P2_SPLIT_XSYNC
 #define P2_SPLIT_XSYNC 1  // split second sync of the sub-0 exchange (+1.1 %)
 #endif
@@ -341,6 +344,40 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
     for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) Ya[cc][0][jj] = Ya[cc][1][jj] = Pa[cc][jj] = {0.0, 0.0};
+    // inverse transform of output (c, par) for limb LJ from my mailbox, exact rounding into A
+    auto inverse_limb = [&](auto LJc) __attribute__((always_inline)) {
+      constexpr int lj = decltype(LJc)::value;
+      cplx V[8];
+#pragma unroll
+      for (int vv = 0; vv < 4; ++vv)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) V[2 * vv + jj] = xch[(vv * 2 + jj) * 64 + lane];
+      if (!D4_NOINV) {
+        // stage twiddles ahead of the transpose, output twiddles after it (as pbs.hip): +0.8 %
+        cplx gi2[4];
+        inv_p2_stage_tw(gi2, T, lane & 7);
+        fft512_inv_tw(V, xch, T, lane, gi2, 0);
+      }
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const double tr = V[m].re + RND_MAGIC, ti = V[m].im + RND_MAGIC;
+        if constexpr (RESID) {
+          max_resid = fmax(max_resid, fabs(V[m].re - (tr - RND_MAGIC)));
+          max_resid = fmax(max_resid, fabs(V[m].im - (ti - RND_MAGIC)));
+        }
+        if constexpr (lj == 0) {
+          A[m] += (uint64_t)__double_as_longlong(tr) - P2_MAGIC_ALL;
+          A[m + 8] += (uint64_t)__double_as_longlong(ti) - P2_MAGIC_ALL;
+        } else {
+          A[m] += (uint64_t)__double_as_longlong(tr) << (16 * lj);
+          A[m + 8] += (uint64_t)__double_as_longlong(ti) << (16 * lj);
+        }
+      }
+      // materialise A here (else the inverse tail sinks into the next limb's key windows)
+#pragma unroll
+      for (int m = 0; m < 16; ++m) pin(A[m]);
+      if constexpr (RESID) pin(max_resid);
+    };
     static_for<0, PBS2_LIMBS>([&](auto LI) __attribute__((always_inline)) {
       constexpr int li = decltype(LI)::value;
       constexpr bool HI = NQ == 1 && li + 1 < PBS2_LIMBS;  // d_hi * g_3 lands at 2^64: vanishes
@@ -394,6 +431,9 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
           // refill the slot of group r - 1 with group r + DIST (RS = DIST + 1)
           if (r + DIST < NGRP) issue_group(key_step, r + DIST);
           else if (!last_step) issue_group(key_step + PER_I, r + DIST - NGRP);
+          if constexpr (P2_DEFER_INV && li > 0) {
+            if (cc == 0 && rq == 0) inverse_limb(std::integral_constant<int, li - 1>{});
+          }
           if constexpr (li == 0) {
             if (cc == 0 && rq == 0) {  // the last digit polynomial's spectra (see above)
 #pragma unroll
@@ -465,40 +505,12 @@ pbs2048_quad_kernel(uint64_t* __restrict__ out, const uint64_t* __restrict__ out
             pin(Ya[cc][0][jj]), pin(Ya[cc][1][jj]);
           }
       }
-      cplx V[8];
-      quad_sync(qflags, ctl, v, qcnt, guard);
-      {
-#pragma unroll
-        for (int vv = 0; vv < 4; ++vv)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj) V[2 * vv + jj] = xch[(vv * 2 + jj) * 64 + lane];
-      }
-      {
-        if (!D4_NOINV) {
-          // stage twiddles ahead of the transpose, output twiddles after it (as pbs.hip): +0.8 %
-          cplx gi2[4];
-          inv_p2_stage_tw(gi2, T, lane & 7);
-          fft512_inv_tw(V, xch, T, lane, gi2, 0);
-        }
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-          const double tr = V[m].re + RND_MAGIC, ti = V[m].im + RND_MAGIC;
-          if constexpr (RESID) {
-            max_resid = fmax(max_resid, fabs(V[m].re - (tr - RND_MAGIC)));
-            max_resid = fmax(max_resid, fabs(V[m].im - (ti - RND_MAGIC)));
-          }
-          if constexpr (li == 0) {
-            A[m] += (uint64_t)__double_as_longlong(tr) - P2_MAGIC_ALL;
-            A[m + 8] += (uint64_t)__double_as_longlong(ti) - P2_MAGIC_ALL;
-          } else {
-            A[m] += (uint64_t)__double_as_longlong(tr) << (16 * li);
-            A[m + 8] += (uint64_t)__double_as_longlong(ti) << (16 * li);
-          }
-        }
-        // materialise A here (else the inverse tail sinks into the next limb's key windows)
-#pragma unroll
-        for (int m = 0; m < 16; ++m) pin(A[m]);
-        if constexpr (RESID) pin(max_resid);
+      // limb li's outputs are in the mailboxes: its inverse runs here for the last limb, and for the
+      // others after the next limb's first key-window barrier (P2_DEFER_INV), which publishes the
+      // mailboxes as this quad sync does
+      if constexpr (!P2_DEFER_INV || li + 1 == PBS2_LIMBS) {
+        quad_sync(qflags, ctl, v, qcnt, guard);
+        inverse_limb(LI);
       }
     });
   }

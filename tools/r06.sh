@@ -98,6 +98,11 @@ genprof)  # every general-path row after the round-6 split-path change (pbs_gene
   CONCRETE_HIP_GEN_STREAMS=1 prof opt9 bde "--batch 128" 240
   CONCRETE_HIP_GEN_STREAMS=1 prof opt10 bde "--batch 64" 240
   ;;
+p2prof)  # cfg4 / opt5 after the deferred limb inverses (pbs2048.hip)
+  prof cfg4 bde ""
+  prof opt5 bde ""
+  step bench_cfg4 400 python -u bench.py --config cfg4 --verify 2 --no-e2e --no-sdfg
+  ;;
 pmc910)
   export CONCRETE_HIP_GEN_STREAMS=1 PMC_TIMEOUT=240
   step pmc_opt9_deb 800 bash tools/pmc.sh $TAG/opt9 deb --config opt9 --no-ks --no-sdfg --batch 128

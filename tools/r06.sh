@@ -103,6 +103,10 @@ p2prof)  # cfg4 / opt5 after the deferred limb inverses (pbs2048.hip)
   prof opt5 bde ""
   step bench_cfg4 400 python -u bench.py --config cfg4 --verify 2 --no-e2e --no-sdfg
   ;;
+bench45)
+  step bench_cfg4 400 python -u bench.py --config cfg4 --verify 2 --no-e2e --no-sdfg
+  step bench_opt5 400 python -u bench.py --config opt5 --verify 2 --no-e2e --no-sdfg
+  ;;
 pmc910)
   export CONCRETE_HIP_GEN_STREAMS=1 PMC_TIMEOUT=240
   step pmc_opt9_deb 800 bash tools/pmc.sh $TAG/opt9 deb --config opt9 --no-ks --no-sdfg --batch 128

@@ -1,4 +1,4 @@
-R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r06so; mkdir -p $O; export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${TAG:-r06so}; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_pbs_generic.py -q --timeout 300 --timeout-method thread > $O/pytest_generic.log 2>&1; rc=$?; tail -2 $O/pytest_generic.log; [ $rc -eq 0 ] || exit $rc
 cd /tmp
 for C in "opt9 1024" "opt10 512"; do set -- $C

@@ -38,7 +38,7 @@ METRIC = "PBS/sec (whole node) at N=1024 batch=4096; achieved HBM GB/s"
 KERNEL_HEADERS = ("concrete_amd/csrc/pbs.hpp", "concrete_amd/csrc/fft512.hpp", "concrete_amd/csrc/kernel_util.hpp",
                   "concrete_amd/csrc/common.hpp")
 KERNEL_SOURCES = {"cfg2": ("concrete_amd/csrc/pbs.hip", "concrete_amd/csrc/pbs1024_hex.hip",
-                           "concrete_amd/csrc/pbs_hex.hpp") + KERNEL_HEADERS,
+                           "concrete_amd/csrc/pbs_hex.hpp", "concrete_amd/csrc/Makefile") + KERNEL_HEADERS,
                   "cfg4": ("concrete_amd/csrc/pbs2048.hip",) + KERNEL_HEADERS,
                   "opt4": ("concrete_amd/csrc/pbs1024k2.hip",) + KERNEL_HEADERS,
                   "opt5": ("concrete_amd/csrc/pbs2048.hip",) + KERNEL_HEADERS,

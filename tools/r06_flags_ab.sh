@@ -6,4 +6,4 @@ R=$GRAFT_REPO_ROOT; cd $R
 ENVS=(); for V in $VS; do ENVS+=("CONCRETE_HIP_LIB=$R/variants/libconcrete_hip_$V.so"); done
 BENCH_ARGS="--global-batch 4096 --steps 10 --warmup 2" bash tools/r05_ab.sh $TAG/b4096 "${ENVS[@]}" || exit 1
 BENCH_ARGS="--global-batch 512 --steps 10 --warmup 2" bash tools/r05_ab.sh $TAG/b512 "${ENVS[@]}" || exit 1
-BENCH_ARGS="--config cfg4 --steps 5 --warmup 2" bash tools/r05_ab.sh $TAG/cfg4 "${ENVS[@]}" || exit 1
+[ -n "$NOCFG4" ] || BENCH_ARGS="--config cfg4 --steps 5 --warmup 2" bash tools/r05_ab.sh $TAG/cfg4 "${ENVS[@]}" || exit 1

@@ -39,6 +39,16 @@
 #include "pbs.hpp"
 #include "companion.hpp"
 
+// Streaming (non-temporal) accesses of the per-call spectra and accumulators, which cross HBM once
+// per CMUX step and are not re-read from L2 (round 6, A/B in DESIGN.md §4.5): GEN_NT_STORES 2 = every
+// X / Y / H / accumulator store of the two-launch and split paths (1: X and Y of the two-launch path
+// only); GEN_NT_LOADS 1 = the two-launch path's X and Y loads (the split path's measured slower)
+#ifndef GEN_NT_STORES
+#define GEN_NT_STORES 2
+#endif
+#ifndef GEN_NT_LOADS
+#define GEN_NT_LOADS 1
+#endif
 #ifndef MAC_CTS
 #define MAC_CTS 16  // ciphertexts per block (key values loaded once per tile)
 #endif
@@ -128,6 +138,16 @@ bool generic_pbs_ok(uint32_t k, uint32_t N, uint32_t level, uint32_t base_log) {
 static hipStream_t side_stream(int idx);  // a library stream per device (defined below)
 
 namespace gen {
+
+// a spectrum value read once (the previous launch's X / Y): streaming load under GEN_NT_LOADS
+__device__ __forceinline__ cplx ld_once(const cplx* p) {
+#if GEN_NT_LOADS
+  return {__builtin_nontemporal_load(&p->re), __builtin_nontemporal_load(&p->im)};
+#else
+  return *p;
+#endif
+}
+
 
 // ------------------------------------------------------------------------------------------
 // block FFT (LDS, in place, radix-8 Stockham passes after one radix-2/4 pass; radix-4 for M <= 256)
@@ -773,7 +793,7 @@ __global__ void __launch_bounds__(Big<M>::NT) gen_big_step_kernel(StepArgs a) {
 #ifdef DG_NOY  // timing diagnostic only (wrong results)
         pf[p][k1] = cplx{(double)(k1 + m), (double)pos_of(p)};
 #else
-        pf[p][k1] = Ym[k1 * 512 + pos_of(p)];
+        pf[p][k1] = ld_once(&Ym[k1 * 512 + pos_of(p)]);
 #endif
       }
     __builtin_amdgcn_sched_barrier(0);  // issued here, not sunk to their first use
@@ -856,7 +876,13 @@ __global__ void __launch_bounds__(Big<M>::NT) gen_big_step_kernel(StepArgs a) {
 #pragma unroll
     for (int sr = 0; sr < SPW; ++sr)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[jrow(sr) * ROWLEN + jcol(e)] = A[sr][e];
+      for (int e = 0; e < 16; ++e) {
+#if GEN_NT_STORES >= 2
+        __builtin_nontemporal_store(A[sr][e], &acc[jrow(sr) * ROWLEN + jcol(e)]);
+#else
+        acc[jrow(sr) * ROWLEN + jcol(e)] = A[sr][e];
+#endif
+      }
   }
 
   if constexpr ((MODE & MODE_FRONT) != 0) {
@@ -944,7 +970,14 @@ __global__ void __launch_bounds__(Big<M>::NT) gen_big_step_kernel(StepArgs a) {
           dft_col<R, false>(u);
 #endif
 #pragma unroll
-          for (int k1 = 0; k1 < R; ++k1) dst[k1 * 512 + pos_of(p)] = u[k1];
+          for (int k1 = 0; k1 < R; ++k1) {
+#if GEN_NT_STORES  // variant: streaming (non-temporal) stores of the spectra the next launch reads
+            __builtin_nontemporal_store(u[k1].re, &dst[k1 * 512 + pos_of(p)].re);
+            __builtin_nontemporal_store(u[k1].im, &dst[k1 * 512 + pos_of(p)].im);
+#else
+            dst[k1 * 512 + pos_of(p)] = u[k1];
+#endif
+          }
         }
         pair_barrier();
       }
@@ -1154,7 +1187,14 @@ __global__ void __launch_bounds__(512) gen_split_front_kernel(SplitArgs a) {
       for (int jl = 0; jl < SPLIT_ROWS; ++jl) u[jl] = q.E[jl * RS + pos];
       dft_col<SPLIT_ROWS, false>(u);
 #pragma unroll
-      for (int k1 = 0; k1 < SPLIT_ROWS; ++k1) dst[k1 * 512 + pos] = u[k1];
+      for (int k1 = 0; k1 < SPLIT_ROWS; ++k1) {
+#if GEN_NT_STORES >= 2
+        __builtin_nontemporal_store(u[k1].re, &dst[k1 * 512 + pos].re);
+        __builtin_nontemporal_store(u[k1].im, &dst[k1 * 512 + pos].im);
+#else
+        dst[k1 * 512 + pos] = u[k1];
+#endif
+      }
       pair_barrier();
     }
   }
@@ -1260,7 +1300,13 @@ __global__ void __launch_bounds__(512) gen_split_back_kernel(SplitArgs a) {
 #pragma unroll
   for (int sr = 0; sr < 2; ++sr)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[(uint64_t)q.jg(sr) * ROWLEN + jcol(e)] = A[sr][e];
+    for (int e = 0; e < 16; ++e) {
+#if GEN_NT_STORES >= 2
+      __builtin_nontemporal_store(A[sr][e], &acc[(uint64_t)q.jg(sr) * ROWLEN + jcol(e)]);
+#else
+      acc[(uint64_t)q.jg(sr) * ROWLEN + jcol(e)] = A[sr][e];
+#endif
+    }
   if (a.resid) {
     for (int off = 32; off > 0; off >>= 1) max_resid = fmax(max_resid, __shfl_xor(max_resid, off));
     if (lane == 0) atomicMax(a.resid, (unsigned long long)__double_as_longlong(max_resid));
@@ -1351,7 +1397,12 @@ __global__ void __launch_bounds__(256) gen_mac_split_kernel(MacSplitArgs a) {
       cplx hsum = {0.0, 0.0};
 #pragma unroll
       for (int uu = 0; uu < S; ++uu) hsum = cadd(hsum, cmulc(from(y, uu), wi[uu]));
+#if GEN_NT_STORES >= 2
+      __builtin_nontemporal_store(hsum.re, &Hct[(uint64_t)m * M].re);
+      __builtin_nontemporal_store(hsum.im, &Hct[(uint64_t)m * M].im);
+#else
       Hct[(uint64_t)m * M] = hsum;
+#endif
     }
   }
 }
@@ -2227,7 +2278,7 @@ __global__ void __launch_bounds__(256) gen_mac2k1_kernel(MacArgs a) {
 #pragma unroll
     for (int rq = 0; rq < KL; ++rq)
 #pragma unroll
-      for (int t = 0; t < T; ++t) xv[rq][t] = Xct[(uint64_t)(rq * T + t) * M];
+      for (int t = 0; t < T; ++t) xv[rq][t] = ld_once(&Xct[(uint64_t)(rq * T + t) * M]);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       cplx* Yct = a.Y + ((uint64_t)ct * 2 + c) * L * M + f;
@@ -2244,7 +2295,12 @@ __global__ void __launch_bounds__(256) gen_mac2k1_kernel(MacArgs a) {
             y.im = __builtin_fma(xg.re, g.im, __builtin_fma(xg.im, g.re, y.im));
           }
         }
+        #if GEN_NT_STORES
+        __builtin_nontemporal_store(y.re, &Yct[(uint64_t)m * M].re);
+        __builtin_nontemporal_store(y.im, &Yct[(uint64_t)m * M].im);
+#else
         Yct[(uint64_t)m * M] = y;
+#endif
       }
     }
   }

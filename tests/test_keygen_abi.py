@@ -168,6 +168,22 @@ def test_committed_pmc_records_match_the_kernel_sources():
         assert bench.pmc_f64_flop(4096, config)[0], f"no PMC f64 record for the current {config} sources"
 
 
+def test_pmc_records_not_attached_under_dispatch_overrides(monkeypatch):
+    """A record measured on the default dispatch does not describe a run whose environment switches
+    kernels (an A/B library, the two-launch path at N = 8192, a forced cfg2 kernel): bench.py then
+    reports no traffic / f64 fields rather than another kernel's."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    assert bench.pmc_traffic(1024, "opt7")[0]
+    for var, val in (("CONCRETE_HIP_GEN_COOP", "0"), ("CONCRETE_HIP_LIB", "/tmp/x.so"), ("CONCRETE_HIP_PBS_HEX", "2")):
+        monkeypatch.setenv(var, val)
+        assert bench.pmc_traffic(1024, "opt7") == (None, None) and bench.pmc_f64_flop(1024, "opt7") == (None, None)
+        monkeypatch.delenv(var)
+    # cfg2 at a batch split over two kernels has no single-kernel record to scale
+    assert bench.dispatched_kernel(1280, "cfg2", 256) is None or bench.pmc_f64_flop(1280, "cfg2")[0] is None
+
+
 def test_optimizer_table_coverage():
     """Every row of the optimizer's reference table (tests/golden/v0_last_128_rows.json, from
     v0-parameters/ref/v0_last_128 by tests/golden/make_v0_rows.py) from 1 to 8 bits, at every log
